@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric: Mrays/s (primary + secondary) on dragon at 1920x1080, 1/2/4/8 MI355X.
+
+One step = one full frame of the hot path (ray generation, BVH traversal, ray-triangle intersection,
+shading with shadow rays, 4 reflection bounces, clamp) for the workload below, with the scene resident
+in HBM before timing starts; for N > 1 the frame's rows are dealt cyclically over the ranks (row y on
+rank y % N: cost-balanced) and gathered to rank 0 over RCCL inside the step.
+
+Rays counted as the reference defines its work: primary + traced reflection + traced
+shadow rays (light_v calls past the back-face test), from the kernel's own counters (equal to the
+oracle's; tests/test_gpu_parity.py).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 via torch.distributed.run (one rank
+per GPU, RCCL). Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import math
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "parallel-ray-tracer_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mrays/sec (primary+secondary) on dragon at 1920×1080, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def alg_bytes(st, pixels, n_lights):
+    """Algorithmic bytes of one launch from the kernel's traversal counters:
+    64 B per interior visit (child-pair node), 8 B per leaf visit (leaf table), 48 B per triangle
+    test (v0, e1, e2, n), per closest hit 4 + 32 + 48 B (tri_orig, normals + material id, material),
+    32 B per light per hit, 20 B per pixel written (rgb + hit + t)."""
+    inner = st["ch_inner"] + st["sh_inner"]
+    leaf = st["ch_leaf"] + st["sh_leaf"]
+    tri = st["ch_tri"] + st["sh_tri"]
+    return 64 * inner + 8 * leaf + 48 * tri + (84 + 32 * n_lights) * st["hits"] + 12 * pixels
+
+
+def cpu_baseline(scene_files, W, H, gpu_rays_for_rows, args):
+    """The reference itself (oracle/_ref/rt_ref_fast: cpu/src/*.c built with the makefile's flags) timed
+    on this host, pthreads with the reference's atomic row scheduler; falls back to the C restatement
+    built the same way (kind "port") when the prebuilt reference binary is absent."""
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    stride = args.cpu_row_stride
+    ref = os.path.join(ROOT, "oracle", "_ref", "rt_ref_fast")
+    obj, mtl, lts = scene_files
+    if os.path.exists(ref) and os.access(ref, os.X_OK):
+        kind = "reference"
+
+        def run(rows_stride, reps):
+            out = subprocess.run([ref, "time", obj, mtl, lts, str(W), str(H), str(threads), "0", str(rows_stride),
+                                  str(reps)], check=True, capture_output=True, text=True, timeout=600)
+            return json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    else:
+        kind = "port"
+        from tests.oracle_bind import OracleScene
+
+        o = OracleScene.load(obj, mtl, lts, flavour="fast")
+        o.build_bvh(3)
+
+        def run(rows_stride, reps):
+            nr = (H + rows_stride - 1) // rows_stride
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                o.render(W, H, rows=(0, rows_stride, nr), threads=threads)
+                ts.append((time.perf_counter() - t0) * 1e3)
+            ts.sort()
+            return {"median_ms": ts[len(ts) // 2], "rows": nr, "threads": threads, "reps": reps}
+    if not stride:  # calibrate: aim at ~15 s of CPU work in total
+        probe = run(16, 1)
+        frame_s = probe["median_ms"] / 1e3 * 16
+        stride = max(1, min(H, int(math.ceil(frame_s / 5.0))))
+        reps = max(1, min(5, int(15.0 / max(frame_s / stride, 1e-3))))
+    else:
+        reps = args.cpu_reps
+    res = run(stride, reps)
+    rays = gpu_rays_for_rows(stride)
+    return {"value": rays / (res["median_ms"] / 1e3) / 1e6, "unit": "Mrays/s", "cores": threads, "kind": kind,
+            "sample": f"rows y = k*{stride} of the same {W}x{H} frame ({res['rows']} rows, {rays} rays), "
+                      f"median of {reps} frames, {threads} pthreads, reference atomic row scheduler, "
+                      f"heuristic-3 BVH (build untimed)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--scene", default="dragon")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--bounces", type=int, default=4)
+    ap.add_argument("--spp", type=int, default=1)
+    ap.add_argument("--bvh", default="binned_sah")
+    ap.add_argument("--kernel", default="fast")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-row-stride", type=int, default=0)
+    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from prt import device, host
+    from prt.scenes import is_standin, scene_paths
+
+    W, H = args.width, args.height
+    files = scene_paths(args.scene)
+    scene = host.Scene.load(*files).build_bvh(args.bvh)
+    stream = torch.cuda.current_stream().cuda_stream
+    r = device.Renderer(local, stream=stream)
+    r.upload(scene)
+    cam = host.camera(W, H)
+    n_r = (H - rank + world - 1) // world  # cyclic rows: y = rank + k * world
+    n_max = (H + world - 1) // world
+    out = torch.zeros((n_max, W, 3), dtype=torch.float32, device="cuda")
+    frame = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda") if rank == 0 else None
+    parts = [torch.empty_like(out) for _ in range(world)] if (rank == 0 and world > 1) else None
+
+    def step():
+        r.render(cam, W, H, rows=(rank, world, n_r), bounces=args.bounces, spp=args.spp, kernel=args.kernel,
+                 rgb=out)
+        if world > 1:
+            dist.gather(out, parts, dst=0)
+            if rank == 0:
+                for q in range(world):
+                    nq = (H - q + world - 1) // world
+                    frame[q::world] = parts[q][:nq]
+        elif rank == 0:
+            frame.copy_(out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ktimes = r.kernel_times(min(args.steps, 64))
+    st = r.stats()
+    # whole-job ray count per frame (identical every step: the render is deterministic)
+    rays_local = st["rays"]
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    rays_t = torch.tensor([rays_local], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(rays_t, op=dist.ReduceOp.SUM)
+    elapsed = el.item()
+    rays_frame = int(rays_t.item())
+
+    # algorithmic bytes of this rank's launch: one extra untimed launch with traversal counters
+    rc = device.Renderer(local, counters=True, stream=stream)
+    rc.upload(scene)
+    rc.render(cam, W, H, rows=(rank, world, n_r), bounces=args.bounces, spp=args.spp, kernel=args.kernel, rgb=out)
+    stc = rc.stats()
+    rc.close()
+    bytes_launch = alg_bytes(stc, W * n_r, len(scene.lights))
+    k_avg_ms = sum(ktimes) / len(ktimes)
+
+    if rank == 0:
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json))
+                key = f"{args.scene}_{W}x{H}_{args.kernel}_{args.bvh}"
+                if key in tj:
+                    traffic = tj[key]["hbm_bytes_per_launch"]
+            except Exception:
+                traffic = None
+        achieved = bytes_launch / (k_avg_ms / 1e3) / 1e9
+        result = {
+            "metric": METRIC,
+            "value": rays_frame * args.steps / elapsed / 1e6,
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": ("synthetic stand-in mesh: the reference snapshot has no assets/dragon/triangles.obj "
+                     "(.MISSING_LARGE_BLOBS); prt/scenes.py generates a Cornell room + 98,304-tri knot with the "
+                     "real dragon .mtl and lights.obj" if is_standin(args.scene) else "reference asset"),
+            "config": {"workload": f"{args.scene} {W}x{H}, {args.spp} spp, {args.bounces} bounces, one fused "
+                                   f"traversal+intersect+shade kernel per frame",
+                       "scene": args.scene, "triangles": scene.n_triangles, "lights": len(scene.lights),
+                       "width": W, "height": H, "bvh": args.bvh, "kernel": args.kernel,
+                       "rays_per_frame": rays_frame, "parallelism": f"rows-cyclic x{world} + RCCL gather"
+                       if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel_ms": k_avg_ms, "alg_bytes_per_launch": bytes_launch,
+                         "note": "algorithmic bytes (node/triangle/shading records the kernel reads) / HIP-event "
+                                 "kernel time; the ~10 MB scene stays L2/MALL-resident, so HBM traffic is far lower"},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            def gpu_rays_for_rows(stride):
+                nr = (H + stride - 1) // stride
+                rr = device.Renderer(local, stream=stream)
+                rr.upload(scene)
+                tmp = torch.empty((nr, W, 3), dtype=torch.float32, device="cuda")
+                rr.render(cam, W, H, rows=(0, stride, nr), bounces=args.bounces, kernel=args.kernel, rgb=tmp)
+                n = rr.stats()["rays"]
+                rr.close()
+                return n
+            try:
+                result["cpu_baseline"] = cpu_baseline(files, W, H, gpu_rays_for_rows, args)
+            except Exception as e:  # reported, never silently replaced
+                result["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(result), flush=True)
+    r.close()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,114 @@
+/*
+ * rt_hip.h — C-ABI of librt_hip.so, the device half of the drop-in (HIP, gfx950 / MI355X).
+ *
+ * It replaces the reference's render seam:
+ *   GPU  gpu/include/gpu.cuh:23-26   void load_to_gpu(void); float render_frame(bool,int,int);
+ *                                     void load_from_gpu(void);
+ *   CPU  cpu/src/main.c:214-264       void render_frame(void) over the globals cam, triangles,
+ *                                     lights, amb_light, bvh, tri_idx -> vec_t pixels[W*H]
+ * with explicit, reentrant calls: state lives in an rt_ctx (one per device), inputs are the
+ * reference's own data (triangle_t / bvh_t / light_t layouts, rt_types.h), every call returns an
+ * int status (0 = ok, < 0 = RT_E_*), nothing calls exit(). A context is not thread-safe; distinct
+ * contexts may be driven from distinct host threads.
+ *
+ * The per-pixel hot path (ray generation, BVH traversal, ray-triangle intersection, Lambert/Blinn
+ * shading with shadow rays, the BOUNCES reflection loop, clamp) runs in ONE HIP kernel per frame.
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include "rt_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rt_ctx rt_ctx;
+
+/* rt_opts.flags */
+enum {
+    RT_FLAG_COUNTERS = 1 /* also count traversal work (node visits, triangle tests): slower */
+};
+
+typedef struct rt_opts {
+    int device;      /* HIP device ordinal */
+    unsigned flags;  /* RT_FLAG_* */
+    void* stream;    /* hipStream_t to launch on; NULL = the context creates its own */
+} rt_opts;
+
+/* Scene = the globals load_to_gpu() reads (gpu/src/gpu.cu:16-29, 129-201). Deep-copied by
+ * rt_upload_scene; the caller keeps ownership. bvh/tri_idx are bvh_build()'s output
+ * (cpu/src/bvh.c:360-388) for ANY builder that keeps the reference layout. */
+typedef struct rt_scene {
+    const rt_triangle* triangles;
+    int n_triangles;
+    const rt_bvh_node* bvh;
+    int n_nodes;
+    const int* tri_idx;
+    const rt_light* lights;
+    int n_lights;
+    rt_vec3 amb; /* amb_light (cpu/src/main.c:37): 0.5, 0.5, 0.5 */
+} rt_scene;
+
+/* rt_frame.kernel */
+enum {
+    RT_KERNEL_AUTO = 0,   /* RT_KERNEL_FAST */
+    RT_KERNEL_STRICT = 1, /* reference-order traversal, exact slab divisions: bit-exact by construction */
+    RT_KERNEL_FAST = 2    /* persistent wavefront kernel, reciprocal slab test (same results; tests) */
+};
+
+/* Rows rendered: y = row_offset + k * row_stride for k in [0, n_rows). Output rows are compact:
+ * row k of the output holds image row y. A full frame is {W, H, 0, 1, H, ...}. */
+typedef struct rt_frame {
+    int width, height;
+    int row_offset, row_stride, n_rows;
+    int bounces; /* BOUNCES (cpu/include/options.h:52), 1..8; the reference uses 4 */
+    int spp;     /* 1 = the reference's pixel-corner ray; s*s = s x s stratified grid, mean of clamped samples */
+    int kernel;  /* RT_KERNEL_* */
+} rt_frame;
+
+/* Device output pointers (all nullable). rgb: [n_rows][width][3] f32 in [0,1] = vec_t pixels
+ * (main.c:39); NULL -> a buffer owned by the context (read it with rt_download).
+ * hit: [n_rows][width] int32 primary closest-hit triangle index (-1 = miss); t: its distance. */
+typedef struct rt_outputs {
+    float* rgb;
+    int* hit;
+    float* t;
+} rt_outputs;
+
+typedef struct rt_stats {
+    unsigned long long primary;        /* primary rays                                     */
+    unsigned long long reflection;     /* traced reflection rays                           */
+    unsigned long long shadow;         /* traced shadow rays (past the back-face test)     */
+    unsigned long long shadow_skipped; /* light_v early-outs (raytracer.c:66-67)           */
+    unsigned long long hits;           /* closest-hit rays that hit a triangle             */
+    unsigned long long ch_inner, ch_leaf, ch_tri; /* closest-hit interior visits / leaf visits / tri tests (RT_FLAG_COUNTERS) */
+    unsigned long long sh_inner, sh_leaf, sh_tri; /* same for shadow rays (RT_FLAG_COUNTERS)             */
+    unsigned long long pixels;         /* pixels written                                    */
+    unsigned long long reserved[4];
+} rt_stats;
+
+int rt_device_count(void);
+const char* rt_version(void);
+
+int rt_create(const rt_opts* opts, rt_ctx** out);
+/* load_to_gpu(): converts the reference layouts into the device layout and uploads */
+int rt_upload_scene(rt_ctx* ctx, const rt_scene* scene);
+/* render_frame(): enqueues ONE kernel on the context stream (asynchronous) */
+int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* frame, const rt_outputs* out);
+/* load_from_gpu(): copies the last frame's compact rows to host (synchronous); nullable args */
+int rt_download(rt_ctx* ctx, float* h_rgb, int* h_hit);
+/* waits for the stream; kernel_ms (nullable) = the last render's kernel time from HIP events */
+int rt_sync(rt_ctx* ctx, float* kernel_ms);
+/* per-launch kernel times (HIP events recorded on the context stream around each kernel) of the last
+ * n launches (n <= 64), oldest first; synchronises; returns the number written or < 0 */
+int rt_kernel_times(rt_ctx* ctx, float* ms, int n);
+/* counters of the last rendered frame (synchronises) */
+int rt_get_stats(rt_ctx* ctx, rt_stats* stats);
+const char* rt_last_error(rt_ctx* ctx);
+void rt_destroy(rt_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,132 @@
+// rt_device.hpp — device-side data layout and the exact-arithmetic primitives of the hot path.
+//
+// Everything here is written for CDNA4 (gfx950, wave64) and compiled with -ffp-contract=off,
+// no fast-math and IEEE-correct fp32 division / sqrt, so that each primitive rounds exactly like the
+// reference's C (cpu/src/vec.c, raytracer.c, bvh.c) compiled strict (SURVEY §8c "O-strict").
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace rtd {
+
+constexpr float EPS = 1e-3f;             // EPSILON, cpu/src/raytracer.c:19
+constexpr float FMAX = 3.402823466e+38f; // FLT_MAX
+constexpr int EMPTY_REF = (int)0x80000000; // empty child (bvh_t child == 0 && tr_len == 0): never pushed
+
+// ---------------------------------------------------------------- device scene (HBM layout)
+// nodes   : one 64-B record per INTERIOR reference node (child-pair layout): both child boxes +
+//           both child refs, loaded with 4 x global_load_dwordx4 per visit.
+//             f4[0] = lo0.x lo0.y lo0.z hi0.x   f4[1] = hi0.y hi0.z lo1.x lo1.y
+//             f4[2] = lo1.z hi1.x hi1.y hi1.z   f4[3] = ref0 ref1 (int bits) 0 0
+//           ref >= 0: interior record index; ref < 0: leaf ~ref; EMPTY_REF: empty node.
+// leaves  : int2 (first, count) into the leaf-ordered triangle arrays (= bvh_t tr_idx, tr_len)
+// tris    : 48 B per leaf-ordered triangle: v0, e1 = v1 - v0, e2 = v2 - v0, n = e1 x e2
+//             f4[0] = v0.x v0.y v0.z e1.x  f4[1] = e1.y e1.z e2.x e2.y  f4[2] = e2.z n.x n.y n.z
+//           (the reference recomputes e1, e2, n per test, raytracer.c:36-38; same roundings)
+// tri_orig: leaf position -> original triangle index (= tri_idx)
+// shade   : 32 B per ORIGINAL triangle: f4[0] = norm[0].xyz, material id (int bits); f4[1] = norm[1].xyz, 0
+// mats    : 48 B per distinct (ks, kd, kr): f4[0] = ks, f4[1] = kd, f4[2] = kr
+// lights  : 32 B per light: f4[0] = pos, f4[1] = kl
+struct DScene {
+    const float4* __restrict__ nodes;
+    const int2* __restrict__ leaves;
+    const float4* __restrict__ tris;
+    const int* __restrict__ tri_orig;
+    const float4* __restrict__ shade;
+    const float4* __restrict__ mats;
+    const float4* __restrict__ lights;
+    int n_lights;
+    int root;  // ref of bvh[0]
+    float amb_x, amb_y, amb_z;
+};
+
+struct KArgs {
+    DScene s;
+    float pos[3], ul[3], ix[3], iy[3];
+    int W, H, row_offset, row_stride, n_rows, bounces, spp, spp_grid;
+    float* rgb;
+    int* hit;
+    float* t;
+    unsigned long long* counters;  // RT_NCOUNT slots (rt_stats order)
+    unsigned int* work;            // persistent-kernel tile counter
+    int n_tiles, tiles_x;
+};
+
+// ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)
+struct v3 {
+    float x, y, z;
+};
+__device__ __forceinline__ v3 mk(float x, float y, float z) { return v3{x, y, z}; }
+__device__ __forceinline__ v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ v3 mul(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ v3 dvs(v3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float mag(v3 a) { return __builtin_sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }
+__device__ __forceinline__ v3 cross(v3 a, v3 b) {
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ v3 normalize(v3 a) { return dvs(a, mag(a)); }
+__device__ __forceinline__ v3 xyz(float4 f) { return mk(f.x, f.y, f.z); }
+
+// ---------------------------------------------------------------- ray-triangle (raytracer.c:35-59)
+// v0, e1, e2, n precomputed on the host with the reference's own roundings.
+__device__ __forceinline__ float hit_triangle(v3 o, v3 d, const float4* __restrict__ tri, int& nd) {
+    const float4 a = tri[0], b = tri[1], c = tri[2];
+    const v3 v0 = mk(a.x, a.y, a.z), e1 = mk(a.w, b.x, b.y), e2 = mk(b.z, b.w, c.x), n = mk(c.y, c.z, c.w);
+    const float det = -dot(d, n);
+    nd = det < 0.0f;
+    if (__builtin_fabsf(det) < EPS) return FMAX;
+    const float inv = 1.0f / det;
+    const v3 ao = sub(o, v0);
+    const v3 dao = cross(ao, d);
+    const float u = dot(e2, dao) * inv;
+    const float v = -dot(e1, dao) * inv;
+    const float t = dot(ao, n) * inv;
+    if (t > EPS && u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f) return t;
+    return FMAX;
+}
+
+// ---------------------------------------------------------------- exact slab test (bvh.c:48-59)
+__device__ __forceinline__ float box_exact(v3 lo, v3 hi, v3 o, v3 d) {
+    float tx1 = (lo.x - o.x) / d.x, tx2 = (hi.x - o.x) / d.x;
+    float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
+    float ty1 = (lo.y - o.y) / d.y, ty2 = (hi.y - o.y) / d.y;
+    tmin = fmaxf(tmin, fminf(ty1, ty2));
+    tmax = fminf(tmax, fmaxf(ty1, ty2));
+    float tz1 = (lo.z - o.z) / d.z, tz2 = (hi.z - o.z) / d.z;
+    tmin = fmaxf(tmin, fminf(tz1, tz2));
+    tmax = fminf(tmax, fmaxf(tz1, tz2));
+    return (tmax >= tmin && tmax > 0) ? tmin : FMAX;
+}
+
+// ---------------------------------------------------------------- reciprocal slab test (fast kernel)
+// t = lo * inv - o * inv via one FMA per plane; tmax widened by 2 ulp so that the test never rejects
+// a box the exact test accepts (culling/order only; triangle tests stay exact).
+struct RayPre {
+    float ix, iy, iz, ox, oy, oz;  // 1/d and o/d (as o * (1/d))
+};
+// A zero direction component would give inf * 0 = NaN planes (and a NaN-swallowing fminf/fmaxf
+// could then reject a box the ray passes through): such components are replaced by +1e-20, for which
+// the slab degenerates to [-huge, +huge] (ray inside) or a same-signed huge pair (ray outside).
+__device__ __forceinline__ float safe_dir(float x) { return __builtin_fabsf(x) < 1e-20f ? 1e-20f : x; }
+__device__ __forceinline__ RayPre ray_pre(v3 o, v3 d) {
+    RayPre p;
+    p.ix = 1.0f / safe_dir(d.x);
+    p.iy = 1.0f / safe_dir(d.y);
+    p.iz = 1.0f / safe_dir(d.z);
+    p.ox = o.x * p.ix;
+    p.oy = o.y * p.iy;
+    p.oz = o.z * p.iz;
+    return p;
+}
+__device__ __forceinline__ float box_fast(float lx, float ly, float lz, float hx, float hy, float hz,
+                                          const RayPre& p) {
+    const float tx1 = __builtin_fmaf(lx, p.ix, -p.ox), tx2 = __builtin_fmaf(hx, p.ix, -p.ox);
+    const float ty1 = __builtin_fmaf(ly, p.iy, -p.oy), ty2 = __builtin_fmaf(hy, p.iy, -p.oy);
+    const float tz1 = __builtin_fmaf(lz, p.iz, -p.oz), tz2 = __builtin_fmaf(hz, p.iz, -p.oz);
+    const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2)) * 1.00000024f;
+    return (tmax >= tmin && tmax > 0) ? tmin : FMAX;
+}
+
+}  // namespace rtd

@@ -1,0 +1,453 @@
+// librt_hip.so — the rt_* C-ABI (include/rt_hip.h) over the HIP kernels in rt_kernels.hpp.
+//
+// Replaces load_to_gpu / render_frame / load_from_gpu (gpu/include/gpu.cuh:23-26, gpu/src/gpu.cu:98-228)
+// and the CPU render_frame (cpu/src/main.c:214-264). All state is per context; every call returns a
+// status; HIP errors are captured into rt_last_error() instead of being printed and ignored.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "rt_hip.h"
+#include "rt_kernels.hpp"
+
+struct rt_ctx {
+    int device = 0;
+    unsigned flags = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string err;
+    // device scene
+    float4* d_nodes = nullptr;
+    int2* d_leaves = nullptr;
+    float4* d_tris = nullptr;
+    int* d_orig = nullptr;
+    float4* d_shade = nullptr;
+    float4* d_mats = nullptr;
+    float4* d_lights = nullptr;
+    int n_lights = 0, root = 0, n_tris = 0, n_inner = 0, n_leaves = 0;
+    float amb[3] = {0.5f, 0.5f, 0.5f};
+    bool has_scene = false;
+    // outputs / bookkeeping
+    float* d_rgb_own = nullptr;
+    size_t rgb_cap = 0;
+    float* last_rgb = nullptr;
+    int* last_hit = nullptr;
+    size_t last_pixels = 0;
+    unsigned long long* d_counters = nullptr;  // rtd::NCOUNT
+    unsigned int* d_work = nullptr;
+    static constexpr int NEV = 64;       // ring of per-launch event pairs (rt_kernel_times)
+    hipEvent_t ev0s[NEV] = {}, ev1s[NEV] = {};
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;  // the last launch's pair
+    long long launches = 0;
+    bool rendered = false;
+};
+
+namespace {
+
+int fail(rt_ctx* c, hipError_t e, const char* what) {
+    if (c) c->err = std::string(what) + ": " + hipGetErrorString(e);
+    return RT_E_HIP;
+}
+#define HIPC(call)                                          \
+    do {                                                    \
+        hipError_t e_ = (call);                             \
+        if (e_ != hipSuccess) return fail(ctx, e_, #call); \
+    } while (0)
+
+int arg_err(rt_ctx* c, const char* msg) {
+    if (c) c->err = msg;
+    return RT_E_ARG;
+}
+
+void free_scene(rt_ctx* ctx) {
+    for (void* p : {(void*)ctx->d_nodes, (void*)ctx->d_leaves, (void*)ctx->d_tris, (void*)ctx->d_orig,
+                    (void*)ctx->d_shade, (void*)ctx->d_mats, (void*)ctx->d_lights})
+        if (p) (void)hipFree(p);
+    ctx->d_nodes = nullptr;
+    ctx->d_leaves = nullptr;
+    ctx->d_tris = nullptr;
+    ctx->d_orig = nullptr;
+    ctx->d_shade = nullptr;
+    ctx->d_mats = nullptr;
+    ctx->d_lights = nullptr;
+    ctx->has_scene = false;
+}
+
+template <class T>
+int upload(rt_ctx* ctx, T** dst, const std::vector<T>& src) {
+    size_t bytes = sizeof(T) * (src.empty() ? 1 : src.size());
+    HIPC(hipMalloc((void**)dst, bytes));
+    if (!src.empty()) HIPC(hipMemcpy(*dst, src.data(), sizeof(T) * src.size(), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+inline int f2i(float f) {
+    int i;
+    std::memcpy(&i, &f, 4);
+    return i;
+}
+inline float i2f(int i) {
+    float f;
+    std::memcpy(&f, &i, 4);
+    return f;
+}
+
+}  // namespace
+
+extern "C" int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+extern "C" const char* rt_version(void) { return "prt-mi355x 0.1 (gfx950)"; }
+
+extern "C" int rt_create(const rt_opts* opts, rt_ctx** out) {
+    if (!out) return RT_E_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return RT_E_NODEVICE;
+    rt_ctx* ctx = new rt_ctx();
+    if (opts) {
+        ctx->device = opts->device;
+        ctx->flags = opts->flags;
+        ctx->stream = (hipStream_t)opts->stream;
+    }
+    if (ctx->device < 0 || ctx->device >= n) {
+        delete ctx;
+        return RT_E_ARG;
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess && !ctx->stream) {
+        e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+        ctx->own_stream = true;
+    }
+    for (int i = 0; i < rt_ctx::NEV && e == hipSuccess; i++) {
+        e = hipEventCreate(&ctx->ev0s[i]);
+        if (e == hipSuccess) e = hipEventCreate(&ctx->ev1s[i]);
+    }
+    if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_counters, sizeof(unsigned long long) * rtd::NCOUNT);
+    if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_work, 256);
+    if (e == hipSuccess) e = hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT);
+    if (e != hipSuccess) {
+        rt_destroy(ctx);
+        return RT_E_HIP;
+    }
+    *out = ctx;
+    return RT_OK;
+}
+
+// load_to_gpu (gpu/src/gpu.cu:129-201): reference layouts -> device layout (rt_device.hpp).
+extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
+    if (!ctx) return RT_E_ARG;
+    if (!sc || !sc->triangles || !sc->bvh || !sc->tri_idx || sc->n_triangles <= 0 || sc->n_nodes <= 0)
+        return arg_err(ctx, "rt_upload_scene: empty scene or missing bvh");
+    if (sc->n_lights < 0 || (sc->n_lights > 0 && !sc->lights)) return arg_err(ctx, "rt_upload_scene: bad lights");
+    HIPC(hipSetDevice(ctx->device));
+    const int n = sc->n_triangles, nn = sc->n_nodes;
+    const rt_bvh_node* B = sc->bvh;
+    // validate tri_idx (a permutation of [0, n))
+    {
+        std::vector<char> seen(n, 0);
+        for (int i = 0; i < n; i++) {
+            int t = sc->tri_idx[i];
+            if (t < 0 || t >= n || seen[t]) return arg_err(ctx, "rt_upload_scene: tri_idx is not a permutation");
+            seen[t] = 1;
+        }
+    }
+    // assign refs: interior -> record index (DFS preorder), leaf -> ~leaf id, empty -> EMPTY_REF
+    std::vector<int> ref(nn, rtd::EMPTY_REF);
+    std::vector<int2> leaves;
+    std::vector<int> inner_order;  // reference node index per record
+    std::vector<int> st{0};
+    std::vector<char> visited(nn, 0);
+    while (!st.empty()) {
+        int i = st.back();
+        st.pop_back();
+        if (i < 0 || i >= nn || visited[i]) return arg_err(ctx, "rt_upload_scene: malformed bvh (child index)");
+        visited[i] = 1;
+        const rt_bvh_node& b = B[i];
+        if (b.tr_len > 0) {
+            if (b.child < 0 || (long long)b.child + b.tr_len > n)
+                return arg_err(ctx, "rt_upload_scene: leaf range outside tri_idx");
+            ref[i] = ~(int)leaves.size();
+            leaves.push_back(make_int2(b.child, b.tr_len));
+        } else if (b.child != 0) {
+            if (b.child < 1 || b.child + 1 >= nn) return arg_err(ctx, "rt_upload_scene: child index out of range");
+            ref[i] = (int)inner_order.size();
+            inner_order.push_back(i);
+            st.push_back(b.child + 1);
+            st.push_back(b.child);  // left visited first (preorder, near-first locality)
+        }
+    }
+    std::vector<float4> nodes(4 * inner_order.size());
+    for (size_t r = 0; r < inner_order.size(); r++) {
+        const rt_bvh_node& p = B[inner_order[r]];
+        const rt_bvh_node& L = B[p.child];
+        const rt_bvh_node& R = B[p.child + 1];
+        nodes[4 * r + 0] = make_float4(L.min.x, L.min.y, L.min.z, L.max.x);
+        nodes[4 * r + 1] = make_float4(L.max.y, L.max.z, R.min.x, R.min.y);
+        nodes[4 * r + 2] = make_float4(R.min.z, R.max.x, R.max.y, R.max.z);
+        nodes[4 * r + 3] = make_float4(i2f(ref[p.child]), i2f(ref[p.child + 1]), 0.0f, 0.0f);
+    }
+    // leaf-ordered triangle planes: v0, e1, e2, n = e1 x e2 (raytracer.c:36-38, same roundings)
+    std::vector<float4> tris(3 * (size_t)n);
+    std::vector<int> orig(n);
+    for (int i = 0; i < n; i++) {
+        const rt_triangle& t = sc->triangles[sc->tri_idx[i]];
+        orig[i] = sc->tri_idx[i];
+        const rt_vec3 &a = t.coords[0], &b = t.coords[1], &c = t.coords[2];
+        const float e1x = b.x - a.x, e1y = b.y - a.y, e1z = b.z - a.z;
+        const float e2x = c.x - a.x, e2y = c.y - a.y, e2z = c.z - a.z;
+        const float nx = e1y * e2z - e1z * e2y, ny = e1z * e2x - e1x * e2z, nz = e1x * e2y - e1y * e2x;
+        tris[3 * i + 0] = make_float4(a.x, a.y, a.z, e1x);
+        tris[3 * i + 1] = make_float4(e1y, e1z, e2x, e2y);
+        tris[3 * i + 2] = make_float4(e2z, nx, ny, nz);
+    }
+    // materials: distinct (ks, kd, kr) triples of triangle_t (the reference stores them per triangle)
+    std::unordered_map<std::string, int> mat_id;
+    std::vector<float4> mats;
+    std::vector<float4> shade(2 * (size_t)n);
+    for (int i = 0; i < n; i++) {
+        const rt_triangle& t = sc->triangles[i];
+        std::string key((const char*)&t.ks, 36);
+        auto it = mat_id.find(key);
+        int m;
+        if (it == mat_id.end()) {
+            m = (int)(mats.size() / 3);
+            mat_id.emplace(key, m);
+            mats.push_back(make_float4(t.ks.x, t.ks.y, t.ks.z, 0.0f));
+            mats.push_back(make_float4(t.kd.x, t.kd.y, t.kd.z, 0.0f));
+            mats.push_back(make_float4(t.kr.x, t.kr.y, t.kr.z, 0.0f));
+        } else {
+            m = it->second;
+        }
+        shade[2 * i + 0] = make_float4(t.norm[0].x, t.norm[0].y, t.norm[0].z, i2f(m));
+        shade[2 * i + 1] = make_float4(t.norm[1].x, t.norm[1].y, t.norm[1].z, 0.0f);
+    }
+    std::vector<float4> lights(2 * (size_t)sc->n_lights);
+    for (int j = 0; j < sc->n_lights; j++) {
+        const rt_light& l = sc->lights[j];
+        lights[2 * j] = make_float4(l.pos.x, l.pos.y, l.pos.z, 0.0f);
+        lights[2 * j + 1] = make_float4(l.kl.x, l.kl.y, l.kl.z, 0.0f);
+    }
+    free_scene(ctx);
+    int rc;
+    if ((rc = upload(ctx, &ctx->d_nodes, nodes)) || (rc = upload(ctx, &ctx->d_leaves, leaves)) ||
+        (rc = upload(ctx, &ctx->d_tris, tris)) || (rc = upload(ctx, &ctx->d_orig, orig)) ||
+        (rc = upload(ctx, &ctx->d_shade, shade)) || (rc = upload(ctx, &ctx->d_mats, mats)) ||
+        (rc = upload(ctx, &ctx->d_lights, lights))) {
+        free_scene(ctx);
+        return rc;
+    }
+    ctx->n_lights = sc->n_lights;
+    ctx->root = ref[0];
+    if (ctx->root == rtd::EMPTY_REF) return arg_err(ctx, "rt_upload_scene: empty root");
+    ctx->n_tris = n;
+    ctx->n_inner = (int)inner_order.size();
+    ctx->n_leaves = (int)leaves.size();
+    ctx->amb[0] = sc->amb.x;
+    ctx->amb[1] = sc->amb.y;
+    ctx->amb[2] = sc->amb.z;
+    ctx->has_scene = true;
+    (void)f2i;
+    return RT_OK;
+}
+
+namespace {
+
+template <int MAXB>
+void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int persist_blocks, hipStream_t s) {
+    if (kernel == RT_KERNEL_STRICT) {
+        if (count) rtd::k_tiles<MAXB, true, true><<<grid_tiles, rtd::BLOCK, 0, s>>>(A);
+        else rtd::k_tiles<MAXB, true, false><<<grid_tiles, rtd::BLOCK, 0, s>>>(A);
+    } else {
+        if (count) rtd::k_persist<MAXB, false, true><<<persist_blocks, rtd::BLOCK, 0, s>>>(A);
+        else rtd::k_persist<MAXB, false, false><<<persist_blocks, rtd::BLOCK, 0, s>>>(A);
+    }
+}
+
+}  // namespace
+
+extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, const rt_outputs* out) {
+    if (!ctx) return RT_E_ARG;
+    if (!ctx->has_scene) {
+        ctx->err = "rt_render: no scene uploaded";
+        return RT_E_STATE;
+    }
+    if (!cam || !f) return arg_err(ctx, "rt_render: null camera/frame");
+    if (f->width <= 0 || f->height <= 0 || f->row_stride <= 0 || f->n_rows <= 0 || f->row_offset < 0 ||
+        (long long)f->row_offset + (long long)(f->n_rows - 1) * f->row_stride >= f->height)
+        return arg_err(ctx, "rt_render: rows outside the frame");
+    if (f->bounces < 1 || f->bounces > 8) return arg_err(ctx, "rt_render: bounces must be 1..8");
+    int g = 1;
+    while (g * g < f->spp) g++;
+    if (f->spp < 1 || g * g != f->spp || g > 16) return arg_err(ctx, "rt_render: spp must be a square 1..256");
+    if (f->kernel < RT_KERNEL_AUTO || f->kernel > RT_KERNEL_FAST) return arg_err(ctx, "rt_render: bad kernel");
+    HIPC(hipSetDevice(ctx->device));
+    const size_t pixels = (size_t)f->width * f->n_rows;
+    float* rgb = out ? out->rgb : nullptr;
+    if (!rgb) {
+        if (ctx->rgb_cap < pixels) {
+            if (ctx->d_rgb_own) HIPC(hipFree(ctx->d_rgb_own));
+            ctx->d_rgb_own = nullptr;
+            ctx->rgb_cap = 0;
+            HIPC(hipMalloc((void**)&ctx->d_rgb_own, sizeof(float) * 3 * pixels));
+            ctx->rgb_cap = pixels;
+        }
+        rgb = ctx->d_rgb_own;
+    }
+    rtd::KArgs A;
+    std::memset(&A, 0, sizeof A);
+    A.s.nodes = ctx->d_nodes;
+    A.s.leaves = ctx->d_leaves;
+    A.s.tris = ctx->d_tris;
+    A.s.tri_orig = ctx->d_orig;
+    A.s.shade = ctx->d_shade;
+    A.s.mats = ctx->d_mats;
+    A.s.lights = ctx->d_lights;
+    A.s.n_lights = ctx->n_lights;
+    A.s.root = ctx->root;
+    A.s.amb_x = ctx->amb[0];
+    A.s.amb_y = ctx->amb[1];
+    A.s.amb_z = ctx->amb[2];
+    const rt_vec3* cv[4] = {&cam->pos, &cam->ul, &cam->inc_x, &cam->inc_y};
+    float* dst[4] = {A.pos, A.ul, A.ix, A.iy};
+    for (int i = 0; i < 4; i++) {
+        dst[i][0] = cv[i]->x;
+        dst[i][1] = cv[i]->y;
+        dst[i][2] = cv[i]->z;
+    }
+    A.W = f->width;
+    A.H = f->height;
+    A.row_offset = f->row_offset;
+    A.row_stride = f->row_stride;
+    A.n_rows = f->n_rows;
+    A.bounces = f->bounces;
+    A.spp = f->spp;
+    A.spp_grid = g;
+    A.rgb = rgb;
+    A.hit = out ? out->hit : nullptr;
+    A.t = out ? out->t : nullptr;
+    A.counters = ctx->d_counters;
+    A.work = ctx->d_work;
+    A.tiles_x = (f->width + 7) / 8;
+    A.n_tiles = A.tiles_x * ((f->n_rows + 7) / 8);
+    const int kernel = f->kernel == RT_KERNEL_AUTO ? RT_KERNEL_FAST : f->kernel;
+    const bool count = (ctx->flags & RT_FLAG_COUNTERS) != 0;
+    dim3 grid((f->width + 15) / 16, (f->n_rows + 15) / 16);
+    int dev_cus = 256;
+    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    int persist_blocks = dev_cus * 4;  // 4 x 256-thread workgroups per CU (LDS stack 34 KiB each)
+    if (persist_blocks * 4 > A.n_tiles) persist_blocks = (A.n_tiles + 3) / 4;
+    if (persist_blocks < 1) persist_blocks = 1;
+    HIPC(hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT, ctx->stream));
+    HIPC(hipMemsetAsync(ctx->d_work, 0, 256, ctx->stream));
+    const int slot = (int)(ctx->launches % rt_ctx::NEV);
+    ctx->ev0 = ctx->ev0s[slot];
+    ctx->ev1 = ctx->ev1s[slot];
+    HIPC(hipEventRecord(ctx->ev0, ctx->stream));
+    if (f->bounces <= 4) launch<4>(A, kernel, count, grid, persist_blocks, ctx->stream);
+    else launch<8>(A, kernel, count, grid, persist_blocks, ctx->stream);
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(ctx->ev1, ctx->stream));
+    ctx->launches++;
+    ctx->last_rgb = rgb;
+    ctx->last_hit = A.hit;
+    ctx->last_pixels = pixels;
+    ctx->rendered = true;
+    return RT_OK;
+}
+
+extern "C" int rt_sync(rt_ctx* ctx, float* kernel_ms) {
+    if (!ctx) return RT_E_ARG;
+    HIPC(hipSetDevice(ctx->device));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    if (kernel_ms) {
+        *kernel_ms = 0.0f;
+        if (ctx->rendered) HIPC(hipEventElapsedTime(kernel_ms, ctx->ev0, ctx->ev1));
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_kernel_times(rt_ctx* ctx, float* ms, int n) {
+    if (!ctx || !ms || n < 0) return RT_E_ARG;
+    HIPC(hipSetDevice(ctx->device));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    long long avail = ctx->launches < rt_ctx::NEV ? ctx->launches : rt_ctx::NEV;
+    if (n > avail) n = (int)avail;
+    for (int i = 0; i < n; i++) {  // oldest first among the last n launches
+        int slot = (int)((ctx->launches - n + i) % rt_ctx::NEV);
+        HIPC(hipEventElapsedTime(&ms[i], ctx->ev0s[slot], ctx->ev1s[slot]));
+    }
+    return n;
+}
+
+extern "C" int rt_download(rt_ctx* ctx, float* h_rgb, int* h_hit) {
+    if (!ctx) return RT_E_ARG;
+    if (!ctx->rendered) {
+        ctx->err = "rt_download: nothing rendered";
+        return RT_E_STATE;
+    }
+    HIPC(hipSetDevice(ctx->device));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    if (h_rgb)
+        HIPC(hipMemcpy(h_rgb, ctx->last_rgb, sizeof(float) * 3 * ctx->last_pixels, hipMemcpyDeviceToHost));
+    if (h_hit) {
+        if (!ctx->last_hit) {
+            ctx->err = "rt_download: last frame had no hit output";
+            return RT_E_STATE;
+        }
+        HIPC(hipMemcpy(h_hit, ctx->last_hit, sizeof(int) * ctx->last_pixels, hipMemcpyDeviceToHost));
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_get_stats(rt_ctx* ctx, rt_stats* st) {
+    if (!ctx || !st) return RT_E_ARG;
+    HIPC(hipSetDevice(ctx->device));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    unsigned long long c[rtd::NCOUNT];
+    HIPC(hipMemcpy(c, ctx->d_counters, sizeof c, hipMemcpyDeviceToHost));
+    std::memset(st, 0, sizeof *st);
+    st->primary = c[rtd::C_PRIM];
+    st->reflection = c[rtd::C_REFL];
+    st->shadow = c[rtd::C_SHAD];
+    st->shadow_skipped = c[rtd::C_SKIP];
+    st->hits = c[rtd::C_HITS];
+    st->ch_inner = c[rtd::C_CHI];
+    st->ch_leaf = c[rtd::C_CHL];
+    st->ch_tri = c[rtd::C_CHT];
+    st->sh_inner = c[rtd::C_SHI];
+    st->sh_leaf = c[rtd::C_SHL];
+    st->sh_tri = c[rtd::C_SHT];
+    st->pixels = c[rtd::C_PIX];
+    st->reserved[0] = c[rtd::C_ERR];  // traversal-stack overflows (must be 0)
+    if (c[rtd::C_ERR]) {
+        ctx->err = "traversal stack overflow: BVH deeper than 32 levels";
+        return RT_E_STATE;
+    }
+    return RT_OK;
+}
+
+extern "C" const char* rt_last_error(rt_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+extern "C" void rt_destroy(rt_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    free_scene(ctx);
+    if (ctx->d_rgb_own) (void)hipFree(ctx->d_rgb_own);
+    if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->d_work) (void)hipFree(ctx->d_work);
+    for (int i = 0; i < rt_ctx::NEV; i++) {
+        if (ctx->ev0s[i]) (void)hipEventDestroy(ctx->ev0s[i]);
+        if (ctx->ev1s[i]) (void)hipEventDestroy(ctx->ev1s[i]);
+    }
+    if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}

@@ -1,0 +1,367 @@
+// rt_kernels.hpp — the per-pixel hot path as HIP kernels for gfx950.
+//
+// One kernel per frame does everything the reference does per pixel (cpu/src/main.c:228-239 +
+// cpu/src/raytracer.c:101-177): primary ray, closest-hit BVH traversal, Lambert/Blinn shading with
+// one any-hit shadow ray per light, up to BOUNCES reflection rays, and the clamp.
+//
+// The reference recursion  raytrace(o,d,i) = c_i + kr_i * raytrace(P_i, r_i, i+1)  is evaluated
+// iteratively: each level's colour c_i and material are kept in registers and the chain is folded
+// from the deepest level outwards, so every float add/mul happens in the reference's order
+// (the GPU reference's forward accumulation, gpu/src/raytracer.cu:61-116, does not: it differs by
+// ~1e-7). Kernels:
+//   k_tiles  : one thread per pixel, 16x16-pixel workgroups (4 waves of 8x8), LDS traversal stack.
+//              STRICT = reference child order + exact slab divisions (bit-exact by construction);
+//              otherwise reciprocal-FMA slab test (conservative, 2-ulp widened).
+//   k_persist: persistent waves pulling 8x8 pixel tiles from an atomic counter (dynamic load
+//              balance across CUs).
+#pragma once
+#include "rt_device.hpp"
+
+namespace rtd {
+
+constexpr int BLOCK = 256;
+constexpr int STACK = 34;  // max stack = max depth (32, bvh.c:84) + 2
+enum { C_PRIM, C_REFL, C_SHAD, C_SKIP, C_HITS, C_CHI, C_CHL, C_CHT, C_SHI, C_SHL, C_SHT, C_PIX, C_ERR, NCOUNT = 16 };
+
+struct Ctr {
+    unsigned prim, refl, shad, skip, hits, chi, chl, cht, shi, shl, sht, pix, err;
+};
+
+__device__ __forceinline__ unsigned wave_sum(unsigned v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void flush(const Ctr& c, unsigned long long* g) {
+    const bool l0 = (threadIdx.x & 63) == 0;
+    unsigned v[NCOUNT] = {c.prim, c.refl, c.shad, c.skip, c.hits, c.chi, c.chl, c.cht,
+                          c.shi, c.shl, c.sht, c.pix, c.err, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 13; i++) {
+        if (!COUNT && i >= C_CHI && i <= C_SHT) continue;
+        unsigned s = wave_sum(v[i]);
+        if (l0 && s) atomicAdd(g + i, (unsigned long long)s);
+    }
+}
+
+// ---------------------------------------------------------------- traversal
+// Closest hit: bvh_traverse, cpu/src/bvh.c:317-358. Stack of node refs in LDS, [depth][lane] so
+// that the 64 lanes of a wave always hit 64 distinct banks whatever their stack depths.
+template <bool STRICT, bool COUNT>
+__device__ __forceinline__ void closest(const DScene& s, v3 o, v3 d, float& best, int& hp, int& nd,
+                                        int* __restrict__ stk, Ctr& c) {
+    RayPre p;
+    if (!STRICT) p = ray_pre(o, d);
+    int sp = 1;
+    stk[0] = s.root;
+    while (sp > 0) {
+        const int ref = stk[(--sp) * BLOCK];
+        if (ref < 0) {
+            const int2 lf = s.leaves[~ref];
+            if (COUNT) c.chl++;
+            for (int i = lf.x; i < lf.x + lf.y; ++i) {
+                int k;
+                const float tt = hit_triangle(o, d, s.tris + 3 * i, k);
+                if (COUNT) c.cht++;
+                if (tt < best) {
+                    best = tt;
+                    nd = k;
+                    hp = i;
+                }
+            }
+        } else {
+            if (COUNT) c.chi++;
+            const float4* N = s.nodes + 4 * ref;
+            const float4 a = N[0], b = N[1], e = N[2], r = N[3];
+            int ni = __float_as_int(r.x), fi = __float_as_int(r.y);
+            float nt, ft;
+            if (STRICT) {
+                nt = box_exact(mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), o, d);
+                ft = box_exact(mk(b.z, b.w, e.x), mk(e.y, e.z, e.w), o, d);
+            } else {
+                nt = box_fast(a.x, a.y, a.z, a.w, b.x, b.y, p);
+                ft = box_fast(b.z, b.w, e.x, e.y, e.z, e.w, p);
+            }
+            if (ni == EMPTY_REF) nt = FMAX;
+            if (fi == EMPTY_REF) ft = FMAX;
+            if (ft < nt) {
+                const int ti = ni;
+                const float tt = nt;
+                ni = fi;
+                nt = ft;
+                fi = ti;
+                ft = tt;
+            }
+            if (sp + 2 > STACK) {  // cannot happen for depth <= 32 BVHs; reported, never silent
+                c.err++;
+                break;
+            }
+            if (ft < best) stk[(sp++) * BLOCK] = fi;
+            if (nt < best) stk[(sp++) * BLOCK] = ni;
+        }
+    }
+}
+
+// Any hit toward a light: bvh_light_traverse, cpu/src/bvh.c:269-315 (returns visibility).
+template <bool STRICT, bool COUNT>
+__device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c) {
+    RayPre p;
+    if (!STRICT) p = ray_pre(o, d);
+    float best = FMAX;
+    int sp = 1;
+    stk[0] = s.root;
+    while (sp > 0) {
+        const int ref = stk[(--sp) * BLOCK];
+        if (ref < 0) {
+            const int2 lf = s.leaves[~ref];
+            if (COUNT) c.shl++;
+            for (int i = lf.x; i < lf.x + lf.y; ++i) {
+                int k;
+                const float tt = hit_triangle(o, d, s.tris + 3 * i, k);
+                if (COUNT) c.sht++;
+                if (tt < best) {
+                    best = tt;
+                    const v3 ip = add(o, mul(d, best));
+                    const v3 oi = sub(o, ip);
+                    if (ld2 > dot(oi, oi)) return false;
+                }
+            }
+        } else {
+            if (COUNT) c.shi++;
+            const float4* N = s.nodes + 4 * ref;
+            const float4 a = N[0], b = N[1], e = N[2], r = N[3];
+            int ni = __float_as_int(r.x), fi = __float_as_int(r.y);
+            float nt, ft;
+            if (STRICT) {
+                nt = box_exact(mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), o, d);
+                ft = box_exact(mk(b.z, b.w, e.x), mk(e.y, e.z, e.w), o, d);
+            } else {
+                nt = box_fast(a.x, a.y, a.z, a.w, b.x, b.y, p);
+                ft = box_fast(b.z, b.w, e.x, e.y, e.z, e.w, p);
+            }
+            if (ni == EMPTY_REF) nt = FMAX;
+            if (fi == EMPTY_REF) ft = FMAX;
+            if (ft < nt) {
+                const int ti = ni;
+                const float tt = nt;
+                ni = fi;
+                nt = ft;
+                fi = ti;
+                ft = tt;
+            }
+            if (sp + 2 > STACK) {
+                c.err++;
+                break;
+            }
+            if (ft < best) stk[(sp++) * BLOCK] = fi;
+            if (nt < best) stk[(sp++) * BLOCK] = ni;
+        }
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------- one path (raytrace, iterative)
+template <int MAXB>
+__device__ __forceinline__ void set3(v3 (&a)[MAXB], int i, v3 v) {
+#pragma unroll
+    for (int k = 0; k < MAXB; k++)
+        if (k == i) a[k] = v;
+}
+template <int MAXB>
+__device__ __forceinline__ void seti(int (&a)[MAXB], int i, int v) {
+#pragma unroll
+    for (int k = 0; k < MAXB; k++)
+        if (k == i) a[k] = v;
+}
+
+template <int MAXB, bool STRICT, bool COUNT>
+__device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0) {
+    const DScene& s = A.s;
+    v3 o = mk(A.pos[0], A.pos[1], A.pos[2]);
+    const v3 amb = mk(s.amb_x, s.amb_y, s.amb_z);
+    v3 cols[MAXB];
+    int mats[MAXB];
+#pragma unroll
+    for (int k = 0; k < MAXB; k++) {
+        cols[k] = mk(0.0f, 0.0f, 0.0f);
+        mats[k] = 0;
+    }
+    int L = 0;
+    bool tail = false;
+    for (int it = 0; it < A.bounces; ++it) {
+        float best = FMAX;
+        int hp = -1, nd = 0;
+        if (it == 0) c.prim++;
+        else c.refl++;
+        closest<STRICT, COUNT>(s, o, d, best, hp, nd, stk, c);
+        const int orig = hp >= 0 ? s.tri_orig[hp] : -1;
+        if (it == 0) {
+            hit0 = orig;
+            t0 = best;
+        }
+        if (hp < 0) {  // raytracer.c:132-135
+            set3<MAXB>(cols, it, mk(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z));
+            L = it + 1;
+            break;
+        }
+        c.hits++;
+        const v3 ip = add(o, mul(d, best));  // raytracer.c:137-138
+        const float4 sh0 = s.shade[2 * orig], sh1 = s.shade[2 * orig + 1];
+        const int m = __float_as_int(sh0.w);
+        const v3 n = nd ? xyz(sh1) : xyz(sh0);
+        const v3 ks = xyz(s.mats[3 * m]), kd = xyz(s.mats[3 * m + 1]), kr = xyz(s.mats[3 * m + 2]);
+        v3 col = mk(0.0f + kd.x * amb.x, 0.0f + kd.y * amb.y, 0.0f + kd.z * amb.z);  // :144-146
+        const v3 v = mul(d, -1.0f);                                                      // :147
+        for (int j = 0; j < s.n_lights; ++j) {                                           // :149-160
+            const v3 Lp = xyz(s.lights[2 * j]), kl = xyz(s.lights[2 * j + 1]);
+            v3 l = sub(Lp, ip);
+            float mg = mag(l);
+            l = dvs(l, mg);
+            mg *= mg;
+            const float ndl = dot(n, l);
+            const v3 h = normalize(add(l, v));  // lambert_blinn, raytracer.c:21-33
+            const float coeff = fmaxf(0.0f, dot(n, h));
+            const v3 cr = mk(kd.x * fmaxf(0.0f, ndl) + ks.x * coeff, kd.y * fmaxf(0.0f, ndl) + ks.y * coeff,
+                             kd.z * fmaxf(0.0f, ndl) + ks.z * coeff);
+            const v3 tmp = sub(ip, Lp), tmp2 = sub(Lp, ip);  // light_v, raytracer.c:62-99
+            const float ld2 = dot(tmp, tmp);
+            int V;
+            if (dot(tmp2, n) < 0) {
+                V = 0;
+                c.skip++;
+            } else {
+                c.shad++;
+                V = visible<STRICT, COUNT>(s, ip, l, ld2, stk, c) ? 1 : 0;
+            }
+            const float fV = (float)V;
+            col.x = col.x + fV * kl.x * cr.x / mg;
+            col.y = col.y + fV * kl.y * cr.y / mg;
+            col.z = col.z + fV * kl.z * cr.z / mg;
+        }
+        const v3 dd = mul(v, -1.0f);  // raytracer.c:163-166
+        const v3 ns = mul(n, 2.0f * __builtin_fabsf(dot(dd, n)));
+        const v3 r = normalize(add(dd, ns));
+        set3<MAXB>(cols, it, col);
+        seti<MAXB>(mats, it, m);
+        if (!(mag(kr) > 0.0f)) {  // raytracer.c:168
+            L = it + 1;
+            break;
+        }
+        if (it + 1 == A.bounces) {  // raytrace(.., BOUNCES) returns {0,0,0}: col += kr * 0
+            L = it + 1;
+            tail = true;
+            break;
+        }
+        o = ip;
+        d = r;
+    }
+    // fold: R_i = c_i + kr_i * R_{i+1}, deepest level first (raytracer.c:169-172)
+    v3 acc = mk(0.0f, 0.0f, 0.0f);
+    bool have = false;
+#pragma unroll
+    for (int i = MAXB - 1; i >= 0; --i) {
+        if (i < L) {
+            if (!have) {
+                acc = cols[i];
+                if (tail) {
+                    const v3 kr = xyz(s.mats[3 * mats[i] + 2]);
+                    acc = mk(acc.x + kr.x * 0.0f, acc.y + kr.y * 0.0f, acc.z + kr.z * 0.0f);
+                }
+                have = true;
+            } else {
+                const v3 kr = xyz(s.mats[3 * mats[i] + 2]);
+                acc = mk(cols[i].x + kr.x * acc.x, cols[i].y + kr.y * acc.y, cols[i].z + kr.z * acc.z);
+            }
+        }
+    }
+    return acc;
+}
+
+__device__ __forceinline__ v3 clamp01(v3 c) {  // vec_constrain(col, 0, 1), vec.c:47-54
+    return mk(fminf(fmaxf(c.x, 0.0f), 1.0f), fminf(fmaxf(c.y, 0.0f), 1.0f), fminf(fmaxf(c.z, 0.0f), 1.0f));
+}
+
+// primary direction, main.c:229-233: ((ul - pos) + inc_x * x) + inc_y * y
+__device__ __forceinline__ v3 primary_dir(const KArgs& A, float fx, float fy) {
+    v3 d = sub(mk(A.ul[0], A.ul[1], A.ul[2]), mk(A.pos[0], A.pos[1], A.pos[2]));
+    d = add(d, mul(mk(A.ix[0], A.ix[1], A.ix[2]), fx));
+    d = add(d, mul(mk(A.iy[0], A.iy[1], A.iy[2]), fy));
+    return d;
+}
+
+template <int MAXB, bool STRICT, bool COUNT>
+__device__ __forceinline__ void render_pixel(const KArgs& A, int x, int k, int* __restrict__ stk, Ctr& c) {
+    const int y = A.row_offset + k * A.row_stride;
+    const size_t o = (size_t)k * A.W + x;
+    int hit0 = -1;
+    float t0 = FMAX;
+    v3 col;
+    if (A.spp <= 1) {
+        col = clamp01(trace_path<MAXB, STRICT, COUNT>(A, primary_dir(A, (float)x, (float)y), stk, c, hit0, t0));
+    } else {  // stratified g x g sub-pixel grid, mean of clamped samples
+        const int g = A.spp_grid;
+        v3 acc = mk(0.0f, 0.0f, 0.0f);
+        for (int sj = 0; sj < g; ++sj)
+            for (int si = 0; si < g; ++si) {
+                const float fx = (float)x + ((float)si + 0.5f) / (float)g;
+                const float fy = (float)y + ((float)sj + 0.5f) / (float)g;
+                int h;
+                float tt;
+                const v3 cs = clamp01(trace_path<MAXB, STRICT, COUNT>(A, primary_dir(A, fx, fy), stk, c, h, tt));
+                acc = add(acc, cs);
+                if (si == 0 && sj == 0) {
+                    hit0 = h;
+                    t0 = tt;
+                }
+            }
+        const float nn = (float)(g * g);
+        col = mk(acc.x / nn, acc.y / nn, acc.z / nn);
+    }
+    c.pix++;
+    if (A.rgb) {
+        A.rgb[3 * o] = col.x;
+        A.rgb[3 * o + 1] = col.y;
+        A.rgb[3 * o + 2] = col.z;
+    }
+    if (A.hit) A.hit[o] = hit0;
+    if (A.t) A.t[o] = t0;
+}
+
+// ---------------------------------------------------------------- kernels
+template <int MAXB, bool STRICT, bool COUNT>
+__global__ __launch_bounds__(BLOCK) void k_tiles(KArgs A) {
+    __shared__ int lds[STACK * BLOCK];
+    int* stk = lds + threadIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7);
+    const int k = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
+    Ctr c = {};
+    if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT>(A, x, k, stk, c);
+    flush<COUNT>(c, A.counters);
+}
+
+// Persistent variant: each wave repeatedly takes the next 8x8 tile from a global counter
+// (one returning atomic per wave per tile; microarch row "dequeue"). Tiles are dealt in row-major
+// order of 8x8 blocks so that concurrently running waves trace neighbouring pixels (shared L1/L2
+// lines for the upper BVH levels).
+template <int MAXB, bool STRICT, bool COUNT>
+__global__ __launch_bounds__(BLOCK) void k_persist(KArgs A) {
+    __shared__ int lds[STACK * BLOCK];
+    int* stk = lds + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    Ctr c = {};
+    for (;;) {
+        unsigned tile = 0;
+        if (lane == 0) tile = atomicAdd(A.work, 1u);
+        tile = __shfl(tile, 0, 64);
+        if (tile >= (unsigned)A.n_tiles) break;
+        const int tx = (int)(tile % (unsigned)A.tiles_x), ty = (int)(tile / (unsigned)A.tiles_x);
+        const int x = tx * 8 + (lane & 7), k = ty * 8 + (lane >> 3);
+        if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT>(A, x, k, stk, c);
+    }
+    flush<COUNT>(c, A.counters);
+}
+
+}  // namespace rtd

@@ -1,0 +1,120 @@
+"""ctypes bindings to the two C-ABI libraries (include/rt_host.h, include/rt_hip.h).
+
+The libraries are built in-tree by the root Makefile into parallel-ray-tracer_amd/lib/. Loading
+fails loudly (RuntimeError) when a library is missing: there is no Python or CPU fallback for
+anything on the render path.
+"""
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+
+
+class Vec3(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("z", ctypes.c_float)]
+
+
+class Triangle(ctypes.Structure):  # triangle_t, cpu/include/triangle.h:8-16
+    _fields_ = [("coords", Vec3 * 3), ("centroid", ctypes.c_float * 3), ("ks", Vec3), ("kd", Vec3),
+                ("kr", Vec3), ("norm", Vec3 * 2)]
+
+
+class Light(ctypes.Structure):  # light_t, cpu/include/light.h:8-11
+    _fields_ = [("pos", Vec3), ("kl", Vec3)]
+
+
+class BvhNode(ctypes.Structure):  # bvh_t, cpu/include/bvh.h:9-23
+    _fields_ = [("min", Vec3), ("max", Vec3), ("tr_len", ctypes.c_int), ("child", ctypes.c_int)]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("pos", Vec3), ("ul", Vec3), ("inc_x", Vec3), ("inc_y", Vec3)]
+
+
+class Rng(ctypes.Structure):
+    _fields_ = [("r", ctypes.c_int32 * 34), ("pos", ctypes.c_int)]
+
+
+class BvhStats(ctypes.Structure):
+    _fields_ = [("leaves", ctypes.c_int), ("min_leaf", ctypes.c_int), ("max_leaf", ctypes.c_int),
+                ("max_depth", ctypes.c_int), ("avg_leaf", ctypes.c_double)]
+
+
+class Opts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("flags", ctypes.c_uint), ("stream", ctypes.c_void_p)]
+
+
+class SceneDesc(ctypes.Structure):
+    _fields_ = [("triangles", ctypes.POINTER(Triangle)), ("n_triangles", ctypes.c_int),
+                ("bvh", ctypes.POINTER(BvhNode)), ("n_nodes", ctypes.c_int),
+                ("tri_idx", ctypes.POINTER(ctypes.c_int)),
+                ("lights", ctypes.POINTER(Light)), ("n_lights", ctypes.c_int), ("amb", Vec3)]
+
+
+class Frame(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("row_offset", ctypes.c_int),
+                ("row_stride", ctypes.c_int), ("n_rows", ctypes.c_int), ("bounces", ctypes.c_int),
+                ("spp", ctypes.c_int), ("kernel", ctypes.c_int)]
+
+
+STAT_FIELDS = ["primary", "reflection", "shadow", "shadow_skipped", "hits", "ch_inner", "ch_leaf",
+               "ch_tri", "sh_inner", "sh_leaf", "sh_tri", "pixels"]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_ulonglong) for f in STAT_FIELDS] + [("reserved", ctypes.c_ulonglong * 4)]
+
+
+_host = None
+_hip = None
+
+
+def _load(name):
+    path = os.path.join(LIB_DIR, name)
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it with `make -j8` (or __graft_entry__.build())")
+    return ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
+def host():
+    global _host
+    if _host is None:
+        L = _load("librt_host.so")
+        P = ctypes.POINTER
+        L.rth_srand.argtypes = [P(Rng), ctypes.c_uint]
+        L.rth_rand.argtypes = [P(Rng)]
+        L.rth_triangles_load.argtypes = [ctypes.c_char_p, ctypes.c_char_p, P(P(Triangle)), P(ctypes.c_size_t)]
+        L.rth_lights_load.argtypes = [ctypes.c_char_p, P(P(Light)), P(ctypes.c_size_t)]
+        L.rth_triangles_random.argtypes = [ctypes.c_size_t, P(Rng), P(P(Triangle))]
+        L.rth_bvh_build.argtypes = [P(Triangle), ctypes.c_size_t, ctypes.c_int, P(Rng), P(P(BvhNode)),
+                                    P(ctypes.c_int), P(P(ctypes.c_int)), P(BvhStats)]
+        L.rth_camera.argtypes = [ctypes.c_int, ctypes.c_int, P(Camera)]
+        L.rth_bmp_write.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
+        L.rth_bmp_encode.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
+        L.rth_free.argtypes = [ctypes.c_void_p]
+        L.rth_free.restype = None
+        _host = L
+    return _host
+
+
+def hip():
+    global _hip
+    if _hip is None:
+        L = _load("librt_hip.so")
+        P = ctypes.POINTER
+        L.rt_create.argtypes = [P(Opts), P(ctypes.c_void_p)]
+        L.rt_upload_scene.argtypes = [ctypes.c_void_p, P(SceneDesc)]
+        L.rt_render.argtypes = [ctypes.c_void_p, P(Camera), P(Frame), ctypes.c_void_p]
+        L.rt_download.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.rt_sync.argtypes = [ctypes.c_void_p, P(ctypes.c_float)]
+        L.rt_kernel_times.argtypes = [ctypes.c_void_p, P(ctypes.c_float), ctypes.c_int]
+        L.rt_get_stats.argtypes = [ctypes.c_void_p, P(Stats)]
+        L.rt_last_error.argtypes = [ctypes.c_void_p]
+        L.rt_last_error.restype = ctypes.c_char_p
+        L.rt_destroy.argtypes = [ctypes.c_void_p]
+        L.rt_destroy.restype = None
+        L.rt_device_count.argtypes = []
+        L.rt_version.restype = ctypes.c_char_p
+        _hip = L
+    return _hip

@@ -1,0 +1,122 @@
+"""Device mirror of the render seam over librt_hip.so (include/rt_hip.h):
+load_to_gpu -> Renderer.upload, render_frame -> Renderer.render, load_from_gpu -> Renderer.download.
+
+No fallback: if librt_hip.so is missing or no GPU is visible, constructing a Renderer raises.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import BvhNode, Camera, Frame, Light, Opts, SceneDesc, Stats, Triangle, Vec3
+
+P = ctypes.POINTER
+
+KERNELS = {"auto": 0, "strict": 1, "fast": 2}
+FLAG_COUNTERS = 1
+
+
+class RtError(RuntimeError):
+    pass
+
+
+class Outputs(ctypes.Structure):
+    _fields_ = [("rgb", ctypes.c_void_p), ("hit", ctypes.c_void_p), ("t", ctypes.c_void_p)]
+
+
+_lib.hip()  # fail loudly at import if the HIP library is absent
+_L = _lib.hip()
+_L.rt_render.argtypes = [ctypes.c_void_p, P(Camera), P(Frame), P(Outputs)]
+
+
+def device_count():
+    return _L.rt_device_count()
+
+
+def _ptr(x):
+    """device pointer of a torch tensor / int / None"""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    return x.data_ptr()
+
+
+class Renderer:
+    """One rt_ctx on one device (gpu.cuh:23-26 seam, explicit instead of global)."""
+
+    def __init__(self, device=0, counters=False, stream=None):
+        self._ctx = ctypes.c_void_p()
+        opts = Opts(device, FLAG_COUNTERS if counters else 0, stream)
+        rc = _L.rt_create(ctypes.byref(opts), ctypes.byref(self._ctx))
+        if rc != 0:
+            raise RtError(f"rt_create(device={device}) failed with status {rc}")
+        self.device = device
+        self.scene = None
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            raise RtError(f"{what}: status {rc}: {_L.rt_last_error(self._ctx).decode()}")
+
+    def upload(self, scene):
+        """load_to_gpu(): scene = prt.host.Scene with a built BVH"""
+        if scene.nodes is None:
+            raise RtError("upload: build the BVH first")
+        tris = np.ascontiguousarray(scene.triangles)
+        nodes = np.ascontiguousarray(scene.nodes)
+        idx = np.ascontiguousarray(scene.tri_idx, dtype=np.int32)
+        lights = np.ascontiguousarray(scene.lights)
+        d = SceneDesc(tris.ctypes.data_as(P(Triangle)), len(tris), nodes.ctypes.data_as(P(BvhNode)), len(nodes),
+                      idx.ctypes.data_as(P(ctypes.c_int)),
+                      lights.ctypes.data_as(P(Light)) if len(lights) else None, len(lights), Vec3(*scene.amb))
+        self._chk(_L.rt_upload_scene(self._ctx, ctypes.byref(d)), "rt_upload_scene")
+        self.scene = scene
+        return self
+
+    def render(self, cam, width, height, rows=None, bounces=4, spp=1, kernel="auto", rgb=None, hit=None, t=None):
+        """render_frame(): asynchronous. rows = (offset, stride, n) or None for the full frame.
+        rgb / hit / t: optional device tensors (torch) or raw device pointers."""
+        ro, rs, nr = rows if rows is not None else (0, 1, height)
+        f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel))
+        out = Outputs(_ptr(rgb), _ptr(hit), _ptr(t))
+        self._chk(_L.rt_render(self._ctx, ctypes.byref(cam), ctypes.byref(f), ctypes.byref(out)), "rt_render")
+        self._last = (width, nr)
+
+    def sync(self):
+        ms = ctypes.c_float()
+        self._chk(_L.rt_sync(self._ctx, ctypes.byref(ms)), "rt_sync")
+        return ms.value
+
+    def kernel_times(self, n):
+        """per-launch kernel ms of the last n renders (HIP events on the launch stream)"""
+        buf = (ctypes.c_float * max(n, 1))()
+        got = _L.rt_kernel_times(self._ctx, buf, n)
+        if got < 0:
+            self._chk(got, "rt_kernel_times")
+        return [buf[i] for i in range(got)]
+
+    def download(self, hit=False):
+        """load_from_gpu(): the last frame's compact rows -> (rgb[n_rows, W, 3], hit or None)"""
+        W, nr = self._last
+        rgb = np.zeros((nr, W, 3), np.float32)
+        h = np.zeros((nr, W), np.int32) if hit else None
+        self._chk(_L.rt_download(self._ctx, rgb.ctypes.data, h.ctypes.data if hit else None), "rt_download")
+        return rgb, h
+
+    def stats(self):
+        s = Stats()
+        self._chk(_L.rt_get_stats(self._ctx, ctypes.byref(s)), "rt_get_stats")
+        d = {f: getattr(s, f) for f in _lib.STAT_FIELDS}
+        d["rays"] = d["primary"] + d["reflection"] + d["shadow"]
+        return d
+
+    def close(self):
+        if self._ctx:
+            _L.rt_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,157 @@
+"""Host mirror of the reference cpu/ front end (loader, random mode, BVH, camera, BMP) over
+librt_host.so (include/rt_host.h). Names follow the reference: triangles_load, lights_load,
+bvh_build, cam_* -> camera(), bmp_write_file.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import BvhNode, BvhStats, Camera, Light, Rng, Triangle
+
+P = ctypes.POINTER
+
+TRI_DTYPE = np.dtype([("coords", np.float32, (3, 3)), ("centroid", np.float32, 3), ("ks", np.float32, 3),
+                      ("kd", np.float32, 3), ("kr", np.float32, 3), ("norm", np.float32, (2, 3))])
+NODE_DTYPE = np.dtype([("min", np.float32, 3), ("max", np.float32, 3), ("tr_len", np.int32), ("child", np.int32)])
+LIGHT_DTYPE = np.dtype([("pos", np.float32, 3), ("kl", np.float32, 3)])
+assert TRI_DTYPE.itemsize == 108 and NODE_DTYPE.itemsize == 32 and LIGHT_DTYPE.itemsize == 24
+
+HEURISTICS = {"axis0": 0, "largest": 1, "random": 3, "sah32": 6, "binned_sah": 16}
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with status {rc}")
+
+
+class Rand:
+    """glibc srand/rand restatement (rth_srand / rth_rand)."""
+
+    def __init__(self, seed=1):
+        self.state = Rng()
+        _lib.host().rth_srand(ctypes.byref(self.state), seed)
+
+    def rand(self):
+        return _lib.host().rth_rand(ctypes.byref(self.state))
+
+
+def _take(ptr, n, dtype):
+    """copy n records from a malloc'd C array into numpy and free it"""
+    L = _lib.host()
+    if n:
+        arr = np.frombuffer(ctypes.string_at(ptr, n * dtype.itemsize), dtype=dtype).copy()
+    else:
+        arr = np.zeros(0, dtype)
+    L.rth_free(ptr)
+    return arr
+
+
+def triangles_load(obj, mtl):
+    """triangles_load(objname, mtlname, &size), cpu/src/triangle.c:74-126 -> structured array"""
+    L = _lib.host()
+    out = P(Triangle)()
+    n = ctypes.c_size_t()
+    _check(L.rth_triangles_load(obj.encode(), mtl.encode(), ctypes.byref(out), ctypes.byref(n)),
+           f"triangles_load({obj})")
+    return _take(out, n.value, TRI_DTYPE)
+
+
+def lights_load(path):
+    """lights_load(filename, &size), cpu/src/light.c:6-29"""
+    L = _lib.host()
+    out = P(Light)()
+    n = ctypes.c_size_t()
+    _check(L.rth_lights_load(path.encode(), ctypes.byref(out), ctypes.byref(n)), f"lights_load({path})")
+    return _take(out, n.value, LIGHT_DTYPE)
+
+
+def triangles_random(n, rng):
+    """random-triangle mode, cpu/src/main.c:115-131"""
+    L = _lib.host()
+    out = P(Triangle)()
+    _check(L.rth_triangles_random(n, ctypes.byref(rng.state), ctypes.byref(out)), "triangles_random")
+    return _take(out, n, TRI_DTYPE)
+
+
+def bvh_build(tris, heuristic=3, rng=None):
+    """bvh_build(triangles, n), cpu/src/bvh.c:360-388 -> (nodes, tri_idx, stats dict)"""
+    L = _lib.host()
+    h = HEURISTICS.get(heuristic, heuristic)
+    tris = np.ascontiguousarray(tris, dtype=TRI_DTYPE)
+    nodes = P(BvhNode)()
+    idx = P(ctypes.c_int)()
+    nlen = ctypes.c_int()
+    st = BvhStats()
+    _check(L.rth_bvh_build(tris.ctypes.data_as(P(Triangle)), len(tris), h,
+                           ctypes.byref(rng.state) if rng is not None else None,
+                           ctypes.byref(nodes), ctypes.byref(nlen), ctypes.byref(idx), ctypes.byref(st)),
+           "bvh_build")
+    nodes_np = _take(nodes, nlen.value, NODE_DTYPE)
+    idx_np = _take(idx, len(tris), np.dtype(np.int32))
+    stats = {"leaves": st.leaves, "min_leaf": st.min_leaf, "max_leaf": st.max_leaf,
+             "max_depth": st.max_depth, "avg_leaf": st.avg_leaf, "nodes": nlen.value}
+    return nodes_np, idx_np, stats
+
+
+def camera(width, height):
+    """cam_init + cam_calculate_screen_coords + inc_x/inc_y (cpu/src/cam.c, main.c:105-106,243-250)"""
+    c = Camera()
+    _check(_lib.host().rth_camera(width, height, ctypes.byref(c)), "camera")
+    return c
+
+
+def camera_array(cam):
+    return np.array([[cam.pos.x, cam.pos.y, cam.pos.z], [cam.ul.x, cam.ul.y, cam.ul.z],
+                     [cam.inc_x.x, cam.inc_x.y, cam.inc_x.z], [cam.inc_y.x, cam.inc_y.y, cam.inc_y.z]], np.float32)
+
+
+def bmp_encode(rgb):
+    """bmp_writer.c:148-175 -> bytes (32-bpp BGRA, bottom-up)"""
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    H, W = rgb.shape[:2]
+    buf = np.zeros(54 + 4 * W * H, np.uint8)
+    _check(_lib.host().rth_bmp_encode(rgb.ctypes.data, W, H, buf.ctypes.data, buf.size), "bmp_encode")
+    return buf.tobytes()
+
+
+def bmp_write_file(rgb, path):
+    """bmp_write_file(pixels, width, height, filename), cpu/src/bmp_writer.c:177-211"""
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    H, W = rgb.shape[:2]
+    _check(_lib.host().rth_bmp_write(rgb.ctypes.data, W, H, path.encode()), "bmp_write_file")
+
+
+class Scene:
+    """A loaded scene + its BVH: what the reference's main() holds in globals (main.c:27-43)."""
+
+    def __init__(self, triangles, lights, seed=1, rng=None):
+        self.triangles = triangles
+        self.lights = lights
+        self.rng = rng if rng is not None else Rand(seed)
+        self.nodes = self.tri_idx = None
+        self.bvh_stats = None
+        self.amb = (0.5, 0.5, 0.5)  # amb_light, main.c:37
+
+    @classmethod
+    def load(cls, obj, mtl, lights, seed=1):
+        rng = Rand(seed)  # srand(SEED) precedes loading, main.c:91-95
+        return cls(triangles_load(obj, mtl), lights_load(lights) if lights else np.zeros(0, LIGHT_DTYPE), rng=rng)
+
+    @classmethod
+    def named(cls, name, seed=1):
+        from .scenes import scene_paths
+        return cls.load(*scene_paths(name), seed=seed)
+
+    @classmethod
+    def random(cls, ntris, seed=1):
+        rng = Rand(seed)
+        return cls(triangles_random(ntris, rng), np.zeros(0, LIGHT_DTYPE), rng=rng)
+
+    def build_bvh(self, heuristic=3):
+        self.nodes, self.tri_idx, self.bvh_stats = bvh_build(self.triangles, heuristic, self.rng)
+        return self
+
+    @property
+    def n_triangles(self):
+        return len(self.triangles)
