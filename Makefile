@@ -30,9 +30,10 @@ $(LIB)/librt_host.so: $(CSRC)/host/rt_host.cpp include/rt_host.h include/rt_type
 HIP_SRCS := $(CSRC)/hip/rt_hip.hip
 HIP_HDRS := $(wildcard $(CSRC)/hip/*.hpp) include/rt_hip.h include/rt_types.h
 
-$(LIB)/librt_hip.so: $(HIP_SRCS) $(HIP_HDRS)
+$(LIB)/librt_hip.so: $(HIP_SRCS) $(HIP_HDRS) $(LIB)/librt_host.so
 	@mkdir -p $(LIB)
-	$(HIPCC) $(HIP_FLAGS) -shared -o $@ $(HIP_SRCS)
+	$(HIPCC) $(HIP_FLAGS) -shared -o $@ $(HIP_SRCS) -L$(LIB) -lrt_host -Wl,-rpath,'$$ORIGIN'
+
 
 $(BIN)/raytracer: $(CSRC)/cli/raytracer.cpp $(LIB)/librt_host.so $(LIB)/librt_hip.so
 	@mkdir -p $(BIN)

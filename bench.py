@@ -96,7 +96,8 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--bounces", type=int, default=4)
     ap.add_argument("--spp", type=int, default=1)
-    ap.add_argument("--bvh", default="binned_sah")
+    ap.add_argument("--bvh", default="random", help="bvh_build heuristic handed over (reference default: 3 = random)")
+    ap.add_argument("--accel", default="auto", help="auto: the library builds a binned-SAH BVH for the fast walk")
     ap.add_argument("--kernel", default="fast")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -125,7 +126,7 @@ def main():
     scene = host.Scene.load(*files).build_bvh(args.bvh)
     stream = torch.cuda.current_stream().cuda_stream
     r = device.Renderer(local, stream=stream)
-    r.upload(scene)
+    r.upload(scene, accel=args.accel)
     cam = host.camera(W, H)
     n_r = (H - rank + world - 1) // world  # cyclic rows: y = rank + k * world
     n_max = (H + world - 1) // world
@@ -173,7 +174,7 @@ def main():
 
     # algorithmic bytes of this rank's launch: one extra untimed launch with traversal counters
     rc = device.Renderer(local, counters=True, stream=stream)
-    rc.upload(scene)
+    rc.upload(scene, accel=args.accel)
     rc.render(cam, W, H, rows=(rank, world, n_r), bounces=args.bounces, spp=args.spp, kernel=args.kernel, rgb=out)
     stc = rc.stats()
     rc.close()
@@ -209,7 +210,7 @@ def main():
             "config": {"workload": f"{args.scene} {W}x{H}, {args.spp} spp, {args.bounces} bounces, one fused "
                                    f"traversal+intersect+shade kernel per frame",
                        "scene": args.scene, "triangles": scene.n_triangles, "lights": len(scene.lights),
-                       "width": W, "height": H, "bvh": args.bvh, "kernel": args.kernel,
+                       "width": W, "height": H, "bvh": args.bvh, "accel": args.accel, "kernel": args.kernel,
                        "rays_per_frame": rays_frame, "parallelism": f"rows-cyclic x{world} + RCCL gather"
                        if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -222,7 +223,7 @@ def main():
             def gpu_rays_for_rows(stride):
                 nr = (H + stride - 1) // stride
                 rr = device.Renderer(local, stream=stream)
-                rr.upload(scene)
+                rr.upload(scene, accel=args.accel)
                 tmp = torch.empty((nr, W, 3), dtype=torch.float32, device="cuda")
                 rr.render(cam, W, H, rows=(0, stride, nr), bounces=args.bounces, kernel=args.kernel, rgb=tmp)
                 n = rr.stats()["rays"]

@@ -48,7 +48,14 @@ typedef struct rt_scene {
     const rt_light* lights;
     int n_lights;
     rt_vec3 amb; /* amb_light (cpu/src/main.c:37): 0.5, 0.5, 0.5 */
+    int accel;   /* RT_ACCEL_*: acceleration structure of the fast kernel */
 } rt_scene;
+
+/* rt_scene.accel */
+enum {
+    RT_ACCEL_AUTO = 0,     /* build a binned-SAH BVH on upload for the fast walk; `bvh` serves the strict walk */
+    RT_ACCEL_REFERENCE = 1 /* traverse the given `bvh` in both walks */
+};
 
 /* rt_frame.kernel */
 enum {
@@ -85,7 +92,9 @@ typedef struct rt_stats {
     unsigned long long ch_inner, ch_leaf, ch_tri; /* closest-hit interior visits / leaf visits / tri tests (RT_FLAG_COUNTERS) */
     unsigned long long sh_inner, sh_leaf, sh_tri; /* same for shadow rays (RT_FLAG_COUNTERS)             */
     unsigned long long pixels;         /* pixels written                                    */
-    unsigned long long reserved[4];
+    unsigned long long fallbacks;      /* fast-kernel rays re-walked strictly (zero direction component or exact tie) */
+    unsigned long long stack_overflows; /* must be 0 (rt_get_stats fails otherwise)          */
+    unsigned long long reserved[2];
 } rt_stats;
 
 int rt_device_count(void);

@@ -254,16 +254,20 @@ static void split(orc_scene* s, int heuristic, int ni, int depth) {
             okA = okB = 0;
             axis = rand() % 4;
             if (axis == 3) {
-                /* center.arr[3] / size.arr[3] / centroid[3] read past the arrays in the reference
-                 * (SURVEY §3.3): every such attempt fails on the shipped scenes (verified against the
-                 * reference BVH dumps). It still consumes its second rand() draw. */
-                (void)rand();
-                continue;
+                /* rand() % 4 == 3 reads center.arr[3], size.arr[3] and centroid[3] past their arrays
+                 * (bvh.c:229-231,237,247). O-strict (gcc -O2) keeps `size` right after
+                 * `center` on the stack and the vec_add(min, max) temporary right after `size`, so it
+                 * reads center.arr[3] = size.x and size.arr[3] = (min + max).x; centroid[3] is ks.r by
+                 * the triangle_t layout. Pinned by the reference's own BVH dumps (tests/golden). */
+                pos = size.x;
+                pos += ((float)rand() / RAND_MAX - 0.5f) * (p->min.x + p->max.x);
+            } else {
+                pos = comp(center, axis);
+                pos += ((float)rand() / RAND_MAX - 0.5f) * (comp(size, axis));
             }
-            pos = comp(center, axis);
-            pos += ((float)rand() / RAND_MAX - 0.5f) * (comp(size, axis));
             for (int i = p->idx; i < p->idx + p->tr_len && (!okA || !okB); i++) {
-                int inA = s->tris[s->tri_idx[i]].centroid[axis] < pos;
+                const tri_t* t = &s->tris[s->tri_idx[i]];
+                int inA = (axis == 3 ? t->ks.x : t->centroid[axis]) < pos;
                 okA |= inA;
                 okB |= !inA;
             }
@@ -279,7 +283,7 @@ static void split(orc_scene* s, int heuristic, int ni, int depth) {
     }
     for (int i = p->idx; i < p->idx + p->tr_len; i++) {           /* bvh.c:244-259 */
         int t = s->tri_idx[i];
-        int inA = s->tris[t].centroid[axis] < pos;
+        int inA = (axis == 3 ? s->tris[t].ks.x : s->tris[t].centroid[axis]) < pos;
         node_t* c = inA ? L : R;
         grow_tri(s, &c->min, &c->max, t);
         c->tr_len += 1;

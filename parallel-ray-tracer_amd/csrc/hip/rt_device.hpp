@@ -26,16 +26,23 @@ constexpr int EMPTY_REF = (int)0x80000000; // empty child (bvh_t child == 0 && t
 // shade   : 32 B per ORIGINAL triangle: f4[0] = norm[0].xyz, material id (int bits); f4[1] = norm[1].xyz, 0
 // mats    : 48 B per distinct (ks, kd, kr): f4[0] = ks, f4[1] = kd, f4[2] = kr
 // lights  : 32 B per light: f4[0] = pos, f4[1] = kl
-struct DScene {
+// One BVH in device layout. A scene carries two: `ref`, the reference's own bvh_build output
+// (traversed by the strict walk, in the reference's order), and `acc`, the acceleration BVH the fast
+// walk uses (binned SAH by default; may alias `ref`). Triangle planes are stored per BVH in its leaf order.
+struct DBvh {
     const float4* __restrict__ nodes;
     const int2* __restrict__ leaves;
     const float4* __restrict__ tris;
     const int* __restrict__ tri_orig;
+    int root;
+};
+
+struct DScene {
+    DBvh ref, acc;
     const float4* __restrict__ shade;
     const float4* __restrict__ mats;
     const float4* __restrict__ lights;
     int n_lights;
-    int root;  // ref of bvh[0]
     float amb_x, amb_y, amb_z;
 };
 

@@ -5,6 +5,8 @@
 // status; HIP errors are captured into rt_last_error() instead of being printed and ignored.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -12,7 +14,29 @@
 #include <vector>
 
 #include "rt_hip.h"
+#include "rt_host.h"
 #include "rt_kernels.hpp"
+
+namespace {
+
+// One BVH view in device memory (rt_device.hpp DBvh) and its host-side build.
+struct DevView {
+    float4* nodes = nullptr;
+    int2* leaves = nullptr;
+    float4* tris = nullptr;
+    int* orig = nullptr;
+    int root = 0, n_inner = 0, n_leaves = 0;
+    size_t bytes = 0;
+};
+
+struct HostView {
+    std::vector<float4> nodes, tris;
+    std::vector<int2> leaves;
+    std::vector<int> orig;
+    int root = 0;
+};
+
+}  // namespace
 
 struct rt_ctx {
     int device = 0;
@@ -21,14 +45,11 @@ struct rt_ctx {
     bool own_stream = false;
     std::string err;
     // device scene
-    float4* d_nodes = nullptr;
-    int2* d_leaves = nullptr;
-    float4* d_tris = nullptr;
-    int* d_orig = nullptr;
+    DevView ref, acc;  // acc.nodes == nullptr: acc aliases ref
     float4* d_shade = nullptr;
     float4* d_mats = nullptr;
     float4* d_lights = nullptr;
-    int n_lights = 0, root = 0, n_tris = 0, n_inner = 0, n_leaves = 0;
+    int n_lights = 0, n_tris = 0;
     float amb[3] = {0.5f, 0.5f, 0.5f};
     bool has_scene = false;
     // outputs / bookkeeping
@@ -39,7 +60,7 @@ struct rt_ctx {
     size_t last_pixels = 0;
     unsigned long long* d_counters = nullptr;  // rtd::NCOUNT
     unsigned int* d_work = nullptr;
-    static constexpr int NEV = 64;       // ring of per-launch event pairs (rt_kernel_times)
+    static constexpr int NEV = 64;  // ring of per-launch event pairs (rt_kernel_times)
     hipEvent_t ev0s[NEV] = {}, ev1s[NEV] = {};
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // the last launch's pair
     long long launches = 0;
@@ -63,14 +84,17 @@ int arg_err(rt_ctx* c, const char* msg) {
     return RT_E_ARG;
 }
 
-void free_scene(rt_ctx* ctx) {
-    for (void* p : {(void*)ctx->d_nodes, (void*)ctx->d_leaves, (void*)ctx->d_tris, (void*)ctx->d_orig,
-                    (void*)ctx->d_shade, (void*)ctx->d_mats, (void*)ctx->d_lights})
+void free_view(DevView& v) {
+    for (void* p : {(void*)v.nodes, (void*)v.leaves, (void*)v.tris, (void*)v.orig})
         if (p) (void)hipFree(p);
-    ctx->d_nodes = nullptr;
-    ctx->d_leaves = nullptr;
-    ctx->d_tris = nullptr;
-    ctx->d_orig = nullptr;
+    v = DevView();
+}
+
+void free_scene(rt_ctx* ctx) {
+    free_view(ctx->ref);
+    free_view(ctx->acc);
+    for (void* p : {(void*)ctx->d_shade, (void*)ctx->d_mats, (void*)ctx->d_lights})
+        if (p) (void)hipFree(p);
     ctx->d_shade = nullptr;
     ctx->d_mats = nullptr;
     ctx->d_lights = nullptr;
@@ -78,22 +102,102 @@ void free_scene(rt_ctx* ctx) {
 }
 
 template <class T>
-int upload(rt_ctx* ctx, T** dst, const std::vector<T>& src) {
-    size_t bytes = sizeof(T) * (src.empty() ? 1 : src.size());
-    HIPC(hipMalloc((void**)dst, bytes));
+int upload(rt_ctx* ctx, T** dst, const std::vector<T>& src, size_t* bytes = nullptr) {
+    size_t b = sizeof(T) * (src.empty() ? 1 : src.size());
+    HIPC(hipMalloc((void**)dst, b));
     if (!src.empty()) HIPC(hipMemcpy(*dst, src.data(), sizeof(T) * src.size(), hipMemcpyHostToDevice));
+    if (bytes) *bytes += b;
     return RT_OK;
 }
 
-inline int f2i(float f) {
-    int i;
-    std::memcpy(&i, &f, 4);
-    return i;
-}
 inline float i2f(int i) {
     float f;
     std::memcpy(&f, &i, 4);
     return f;
+}
+
+// Reference-layout BVH (bvh_t[], tri_idx) -> device view. `inflate` > 0 grows every child box by that
+// absolute amount (acceleration BVH: keeps the reciprocal-FMA slab test conservative); 0 keeps the
+// reference's boxes bit-for-bit (strict walk).
+int build_view(rt_ctx* ctx, const rt_bvh_node* B, int nn, const int* tri_idx, const rt_triangle* T, int n,
+               float inflate, HostView& v) {
+    std::vector<char> seen(n, 0);
+    for (int i = 0; i < n; i++) {
+        int t = tri_idx[i];
+        if (t < 0 || t >= n || seen[t]) return arg_err(ctx, "rt_upload_scene: tri_idx is not a permutation");
+        seen[t] = 1;
+    }
+    // refs: interior -> record index (DFS preorder), leaf -> ~leaf id, empty -> EMPTY_REF
+    std::vector<int> ref(nn, rtd::EMPTY_REF);
+    std::vector<int> inner;
+    std::vector<int> st{0};
+    std::vector<char> visited(nn, 0);
+    while (!st.empty()) {
+        int i = st.back();
+        st.pop_back();
+        if (i < 0 || i >= nn || visited[i]) return arg_err(ctx, "rt_upload_scene: malformed bvh (child index)");
+        visited[i] = 1;
+        const rt_bvh_node& b = B[i];
+        if (b.tr_len > 0) {
+            if (b.child < 0 || (long long)b.child + b.tr_len > n)
+                return arg_err(ctx, "rt_upload_scene: leaf range outside tri_idx");
+            ref[i] = ~(int)v.leaves.size();
+            v.leaves.push_back(make_int2(b.child, b.tr_len));
+        } else if (b.child != 0) {
+            if (b.child < 1 || b.child + 1 >= nn) return arg_err(ctx, "rt_upload_scene: child index out of range");
+            ref[i] = (int)inner.size();
+            inner.push_back(i);
+            st.push_back(b.child + 1);
+            st.push_back(b.child);  // left first: preorder, near-first locality
+        }
+    }
+    if (ref[0] == rtd::EMPTY_REF) return arg_err(ctx, "rt_upload_scene: empty root");
+    v.root = ref[0];
+    v.nodes.resize(4 * inner.size());
+    for (size_t r = 0; r < inner.size(); r++) {
+        const rt_bvh_node& p = B[inner[r]];
+        rt_bvh_node L = B[p.child], R = B[p.child + 1];
+        if (inflate > 0)
+            for (rt_bvh_node* c : {&L, &R}) {
+                c->min.x -= inflate;
+                c->min.y -= inflate;
+                c->min.z -= inflate;
+                c->max.x += inflate;
+                c->max.y += inflate;
+                c->max.z += inflate;
+            }
+        v.nodes[4 * r + 0] = make_float4(L.min.x, L.min.y, L.min.z, L.max.x);
+        v.nodes[4 * r + 1] = make_float4(L.max.y, L.max.z, R.min.x, R.min.y);
+        v.nodes[4 * r + 2] = make_float4(R.min.z, R.max.x, R.max.y, R.max.z);
+        v.nodes[4 * r + 3] = make_float4(i2f(ref[p.child]), i2f(ref[p.child + 1]), 0.0f, 0.0f);
+    }
+    // leaf-ordered triangle planes: v0, e1, e2, n = e1 x e2 (raytracer.c:36-38, same roundings)
+    v.tris.resize(3 * (size_t)n);
+    v.orig.resize(n);
+    for (int i = 0; i < n; i++) {
+        const rt_triangle& t = T[tri_idx[i]];
+        v.orig[i] = tri_idx[i];
+        const rt_vec3 &a = t.coords[0], &b = t.coords[1], &c = t.coords[2];
+        const float e1x = b.x - a.x, e1y = b.y - a.y, e1z = b.z - a.z;
+        const float e2x = c.x - a.x, e2y = c.y - a.y, e2z = c.z - a.z;
+        const float nx = e1y * e2z - e1z * e2y, ny = e1z * e2x - e1x * e2z, nz = e1x * e2y - e1y * e2x;
+        v.tris[3 * i + 0] = make_float4(a.x, a.y, a.z, e1x);
+        v.tris[3 * i + 1] = make_float4(e1y, e1z, e2x, e2y);
+        v.tris[3 * i + 2] = make_float4(e2z, nx, ny, nz);
+    }
+    return RT_OK;
+}
+
+int upload_view(rt_ctx* ctx, const HostView& h, DevView& d) {
+    int rc;
+    d.bytes = 0;
+    if ((rc = upload(ctx, &d.nodes, h.nodes, &d.bytes)) || (rc = upload(ctx, &d.leaves, h.leaves, &d.bytes)) ||
+        (rc = upload(ctx, &d.tris, h.tris, &d.bytes)) || (rc = upload(ctx, &d.orig, h.orig, &d.bytes)))
+        return rc;
+    d.root = h.root;
+    d.n_inner = (int)(h.nodes.size() / 4);
+    d.n_leaves = (int)h.leaves.size();
+    return RT_OK;
 }
 
 }  // namespace
@@ -104,7 +208,7 @@ extern "C" int rt_device_count(void) {
     return n;
 }
 
-extern "C" const char* rt_version(void) { return "prt-mi355x 0.1 (gfx950)"; }
+extern "C" const char* rt_version(void) { return "prt-mi355x 0.2 (gfx950)"; }
 
 extern "C" int rt_create(const rt_opts* opts, rt_ctx** out) {
     if (!out) return RT_E_ARG;
@@ -147,66 +251,30 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     if (!sc || !sc->triangles || !sc->bvh || !sc->tri_idx || sc->n_triangles <= 0 || sc->n_nodes <= 0)
         return arg_err(ctx, "rt_upload_scene: empty scene or missing bvh");
     if (sc->n_lights < 0 || (sc->n_lights > 0 && !sc->lights)) return arg_err(ctx, "rt_upload_scene: bad lights");
+    if (sc->accel != RT_ACCEL_AUTO && sc->accel != RT_ACCEL_REFERENCE)
+        return arg_err(ctx, "rt_upload_scene: bad accel");
     HIPC(hipSetDevice(ctx->device));
-    const int n = sc->n_triangles, nn = sc->n_nodes;
-    const rt_bvh_node* B = sc->bvh;
-    // validate tri_idx (a permutation of [0, n))
-    {
-        std::vector<char> seen(n, 0);
-        for (int i = 0; i < n; i++) {
-            int t = sc->tri_idx[i];
-            if (t < 0 || t >= n || seen[t]) return arg_err(ctx, "rt_upload_scene: tri_idx is not a permutation");
-            seen[t] = 1;
-        }
-    }
-    // assign refs: interior -> record index (DFS preorder), leaf -> ~leaf id, empty -> EMPTY_REF
-    std::vector<int> ref(nn, rtd::EMPTY_REF);
-    std::vector<int2> leaves;
-    std::vector<int> inner_order;  // reference node index per record
-    std::vector<int> st{0};
-    std::vector<char> visited(nn, 0);
-    while (!st.empty()) {
-        int i = st.back();
-        st.pop_back();
-        if (i < 0 || i >= nn || visited[i]) return arg_err(ctx, "rt_upload_scene: malformed bvh (child index)");
-        visited[i] = 1;
-        const rt_bvh_node& b = B[i];
-        if (b.tr_len > 0) {
-            if (b.child < 0 || (long long)b.child + b.tr_len > n)
-                return arg_err(ctx, "rt_upload_scene: leaf range outside tri_idx");
-            ref[i] = ~(int)leaves.size();
-            leaves.push_back(make_int2(b.child, b.tr_len));
-        } else if (b.child != 0) {
-            if (b.child < 1 || b.child + 1 >= nn) return arg_err(ctx, "rt_upload_scene: child index out of range");
-            ref[i] = (int)inner_order.size();
-            inner_order.push_back(i);
-            st.push_back(b.child + 1);
-            st.push_back(b.child);  // left visited first (preorder, near-first locality)
-        }
-    }
-    std::vector<float4> nodes(4 * inner_order.size());
-    for (size_t r = 0; r < inner_order.size(); r++) {
-        const rt_bvh_node& p = B[inner_order[r]];
-        const rt_bvh_node& L = B[p.child];
-        const rt_bvh_node& R = B[p.child + 1];
-        nodes[4 * r + 0] = make_float4(L.min.x, L.min.y, L.min.z, L.max.x);
-        nodes[4 * r + 1] = make_float4(L.max.y, L.max.z, R.min.x, R.min.y);
-        nodes[4 * r + 2] = make_float4(R.min.z, R.max.x, R.max.y, R.max.z);
-        nodes[4 * r + 3] = make_float4(i2f(ref[p.child]), i2f(ref[p.child + 1]), 0.0f, 0.0f);
-    }
-    // leaf-ordered triangle planes: v0, e1, e2, n = e1 x e2 (raytracer.c:36-38, same roundings)
-    std::vector<float4> tris(3 * (size_t)n);
-    std::vector<int> orig(n);
-    for (int i = 0; i < n; i++) {
-        const rt_triangle& t = sc->triangles[sc->tri_idx[i]];
-        orig[i] = sc->tri_idx[i];
-        const rt_vec3 &a = t.coords[0], &b = t.coords[1], &c = t.coords[2];
-        const float e1x = b.x - a.x, e1y = b.y - a.y, e1z = b.z - a.z;
-        const float e2x = c.x - a.x, e2y = c.y - a.y, e2z = c.z - a.z;
-        const float nx = e1y * e2z - e1z * e2y, ny = e1z * e2x - e1x * e2z, nz = e1x * e2y - e1y * e2x;
-        tris[3 * i + 0] = make_float4(a.x, a.y, a.z, e1x);
-        tris[3 * i + 1] = make_float4(e1y, e1z, e2x, e2y);
-        tris[3 * i + 2] = make_float4(e2z, nx, ny, nz);
+    const int n = sc->n_triangles;
+    HostView hr, ha;
+    int rc = build_view(ctx, sc->bvh, sc->n_nodes, sc->tri_idx, sc->triangles, n, 0.0f, hr);
+    if (rc) return rc;
+    const bool own_acc = sc->accel == RT_ACCEL_AUTO;
+    if (own_acc) {
+        // the fast walk's BVH: binned SAH over the same triangles (librt_host.so), boxes inflated by
+        // 2^-18 of the scene's coordinate magnitude (>= the reciprocal-FMA test's rounding reach)
+        rt_bvh_node* nodes = nullptr;
+        int nlen = 0;
+        int* idx = nullptr;
+        if (rth_bvh_build(sc->triangles, (size_t)n, RTH_BVH_BINNED_SAH, nullptr, &nodes, &nlen, &idx, nullptr) != RT_OK)
+            return arg_err(ctx, "rt_upload_scene: acceleration BVH build failed");
+        float mx = 16.0f;
+        for (int i = 0; i < n; i++)
+            for (const rt_vec3& c : sc->triangles[i].coords)
+                mx = std::max(mx, std::max(std::fabs(c.x), std::max(std::fabs(c.y), std::fabs(c.z))));
+        rc = build_view(ctx, nodes, nlen, idx, sc->triangles, n, std::ldexp(mx, -18), ha);
+        rth_free(nodes);
+        rth_free(idx);
+        if (rc) return rc;
     }
     // materials: distinct (ks, kd, kr) triples of triangle_t (the reference stores them per triangle)
     std::unordered_map<std::string, int> mat_id;
@@ -236,25 +304,18 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
         lights[2 * j + 1] = make_float4(l.kl.x, l.kl.y, l.kl.z, 0.0f);
     }
     free_scene(ctx);
-    int rc;
-    if ((rc = upload(ctx, &ctx->d_nodes, nodes)) || (rc = upload(ctx, &ctx->d_leaves, leaves)) ||
-        (rc = upload(ctx, &ctx->d_tris, tris)) || (rc = upload(ctx, &ctx->d_orig, orig)) ||
+    if ((rc = upload_view(ctx, hr, ctx->ref)) || (own_acc && (rc = upload_view(ctx, ha, ctx->acc))) ||
         (rc = upload(ctx, &ctx->d_shade, shade)) || (rc = upload(ctx, &ctx->d_mats, mats)) ||
         (rc = upload(ctx, &ctx->d_lights, lights))) {
         free_scene(ctx);
         return rc;
     }
     ctx->n_lights = sc->n_lights;
-    ctx->root = ref[0];
-    if (ctx->root == rtd::EMPTY_REF) return arg_err(ctx, "rt_upload_scene: empty root");
     ctx->n_tris = n;
-    ctx->n_inner = (int)inner_order.size();
-    ctx->n_leaves = (int)leaves.size();
     ctx->amb[0] = sc->amb.x;
     ctx->amb[1] = sc->amb.y;
     ctx->amb[2] = sc->amb.z;
     ctx->has_scene = true;
-    (void)f2i;
     return RT_OK;
 }
 
@@ -270,6 +331,8 @@ void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int pe
         else rtd::k_persist<MAXB, false, false><<<persist_blocks, rtd::BLOCK, 0, s>>>(A);
     }
 }
+
+rtd::DBvh dview(const DevView& v) { return rtd::DBvh{v.nodes, v.leaves, v.tris, v.orig, v.root}; }
 
 }  // namespace
 
@@ -303,15 +366,12 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     }
     rtd::KArgs A;
     std::memset(&A, 0, sizeof A);
-    A.s.nodes = ctx->d_nodes;
-    A.s.leaves = ctx->d_leaves;
-    A.s.tris = ctx->d_tris;
-    A.s.tri_orig = ctx->d_orig;
+    A.s.ref = dview(ctx->ref);
+    A.s.acc = ctx->acc.nodes ? dview(ctx->acc) : A.s.ref;
     A.s.shade = ctx->d_shade;
     A.s.mats = ctx->d_mats;
     A.s.lights = ctx->d_lights;
     A.s.n_lights = ctx->n_lights;
-    A.s.root = ctx->root;
     A.s.amb_x = ctx->amb[0];
     A.s.amb_y = ctx->amb[1];
     A.s.amb_z = ctx->amb[2];
@@ -426,7 +486,8 @@ extern "C" int rt_get_stats(rt_ctx* ctx, rt_stats* st) {
     st->sh_leaf = c[rtd::C_SHL];
     st->sh_tri = c[rtd::C_SHT];
     st->pixels = c[rtd::C_PIX];
-    st->reserved[0] = c[rtd::C_ERR];  // traversal-stack overflows (must be 0)
+    st->fallbacks = c[rtd::C_FALLBACK];
+    st->stack_overflows = c[rtd::C_ERR];
     if (c[rtd::C_ERR]) {
         ctx->err = "traversal stack overflow: BVH deeper than 32 levels";
         return RT_E_STATE;

@@ -8,12 +8,22 @@
 // iteratively: each level's colour c_i and material are kept in registers and the chain is folded
 // from the deepest level outwards, so every float add/mul happens in the reference's order
 // (the GPU reference's forward accumulation, gpu/src/raytracer.cu:61-116, does not: it differs by
-// ~1e-7). Kernels:
+// ~1e-7).
+//
+// Two traversal walks:
+//   strict : the reference BVH in the reference's order with the reference's exact slab divisions
+//            (bvh.c:48-59,269-358), including its IEEE special cases: a zero direction component
+//            makes 0/0 = NaN slabs, and fminf/fmaxf then cull boxes whose face contains the ray.
+//            Bit-exact by construction.
+//   fast   : the acceleration BVH with a reciprocal-FMA slab test on conservatively inflated boxes.
+//            Its result is the reference's except where the reference's answer depends on traversal
+//            order or on the NaN special cases; those rays are detected and re-walked strictly:
+//              - rays with a zero direction component (the NaN-slab cases) walk strictly from the start;
+//              - closest hits that end on an exact tie in t (first-found wins in the reference,
+//                bvh.c:331) are re-walked strictly.
+// Kernels:
 //   k_tiles  : one thread per pixel, 16x16-pixel workgroups (4 waves of 8x8), LDS traversal stack.
-//              STRICT = reference child order + exact slab divisions (bit-exact by construction);
-//              otherwise reciprocal-FMA slab test (conservative, 2-ulp widened).
-//   k_persist: persistent waves pulling 8x8 pixel tiles from an atomic counter (dynamic load
-//              balance across CUs).
+//   k_persist: persistent waves pulling 8x8 pixel tiles from an atomic counter.
 #pragma once
 #include "rt_device.hpp"
 
@@ -21,10 +31,13 @@ namespace rtd {
 
 constexpr int BLOCK = 256;
 constexpr int STACK = 34;  // max stack = max depth (32, bvh.c:84) + 2
-enum { C_PRIM, C_REFL, C_SHAD, C_SKIP, C_HITS, C_CHI, C_CHL, C_CHT, C_SHI, C_SHL, C_SHT, C_PIX, C_ERR, NCOUNT = 16 };
+enum {
+    C_PRIM, C_REFL, C_SHAD, C_SKIP, C_HITS, C_CHI, C_CHL, C_CHT, C_SHI, C_SHL, C_SHT, C_PIX, C_ERR, C_FALLBACK,
+    NCOUNT = 16
+};
 
 struct Ctr {
-    unsigned prim, refl, shad, skip, hits, chi, chl, cht, shi, shl, sht, pix, err;
+    unsigned prim, refl, shad, skip, hits, chi, chl, cht, shi, shl, sht, pix, err, fb;
 };
 
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
@@ -37,43 +50,54 @@ template <bool COUNT>
 __device__ __forceinline__ void flush(const Ctr& c, unsigned long long* g) {
     const bool l0 = (threadIdx.x & 63) == 0;
     unsigned v[NCOUNT] = {c.prim, c.refl, c.shad, c.skip, c.hits, c.chi, c.chl, c.cht,
-                          c.shi, c.shl, c.sht, c.pix, c.err, 0, 0, 0};
+                          c.shi, c.shl, c.sht, c.pix, c.err, c.fb, 0, 0};
 #pragma unroll
-    for (int i = 0; i < 13; i++) {
+    for (int i = 0; i < 14; i++) {
         if (!COUNT && i >= C_CHI && i <= C_SHT) continue;
         unsigned s = wave_sum(v[i]);
         if (l0 && s) atomicAdd(g + i, (unsigned long long)s);
     }
 }
 
-// ---------------------------------------------------------------- traversal
-// Closest hit: bvh_traverse, cpu/src/bvh.c:317-358. Stack of node refs in LDS, [depth][lane] so
-// that the 64 lanes of a wave always hit 64 distinct banks whatever their stack depths.
+__device__ __forceinline__ bool degenerate(v3 d) { return d.x == 0.0f || d.y == 0.0f || d.z == 0.0f; }
+
+// fast-walk pruning: visit a box whose entry is within 4 ulp of the best hit, so that a triangle tied
+// with the best hit is always reached (and the tie detected) despite the reciprocal test's rounding.
+constexpr float PRUNE_SLACK = 1.0000005f;
+
+// ---------------------------------------------------------------- closest hit
+// bvh_traverse, cpu/src/bvh.c:317-358. Stack of node refs in LDS, [depth][lane] so that the 64 lanes
+// of a wave always hit 64 distinct banks whatever their stack depths.
+// Returns the leaf position of the best hit in hp (-1: none); `tie` = the final best was matched by
+// another triangle (fast walk only).
 template <bool STRICT, bool COUNT>
-__device__ __forceinline__ void closest(const DScene& s, v3 o, v3 d, float& best, int& hp, int& nd,
-                                        int* __restrict__ stk, Ctr& c) {
+__device__ __forceinline__ void closest_walk(const DBvh& B, v3 o, v3 d, float& best, int& hp, int& nd, bool& tie,
+                                             int* __restrict__ stk, Ctr& c) {
     RayPre p;
     if (!STRICT) p = ray_pre(o, d);
     int sp = 1;
-    stk[0] = s.root;
+    stk[0] = B.root;
     while (sp > 0) {
         const int ref = stk[(--sp) * BLOCK];
         if (ref < 0) {
-            const int2 lf = s.leaves[~ref];
+            const int2 lf = B.leaves[~ref];
             if (COUNT) c.chl++;
             for (int i = lf.x; i < lf.x + lf.y; ++i) {
                 int k;
-                const float tt = hit_triangle(o, d, s.tris + 3 * i, k);
+                const float tt = hit_triangle(o, d, B.tris + 3 * i, k);
                 if (COUNT) c.cht++;
                 if (tt < best) {
                     best = tt;
                     nd = k;
                     hp = i;
+                    if (!STRICT) tie = false;
+                } else if (!STRICT && tt == best && tt != FMAX) {
+                    tie = true;
                 }
             }
         } else {
             if (COUNT) c.chi++;
-            const float4* N = s.nodes + 4 * ref;
+            const float4* N = B.nodes + 4 * ref;
             const float4 a = N[0], b = N[1], e = N[2], r = N[3];
             int ni = __float_as_int(r.x), fi = __float_as_int(r.y);
             float nt, ft;
@@ -98,28 +122,35 @@ __device__ __forceinline__ void closest(const DScene& s, v3 o, v3 d, float& best
                 c.err++;
                 break;
             }
-            if (ft < best) stk[(sp++) * BLOCK] = fi;
-            if (nt < best) stk[(sp++) * BLOCK] = ni;
+            if (STRICT) {
+                if (ft < best) stk[(sp++) * BLOCK] = fi;
+                if (nt < best) stk[(sp++) * BLOCK] = ni;
+            } else {
+                const float lim = best * PRUNE_SLACK;
+                if (ft <= lim && ft != FMAX) stk[(sp++) * BLOCK] = fi;
+                if (nt <= lim && nt != FMAX) stk[(sp++) * BLOCK] = ni;
+            }
         }
     }
 }
 
 // Any hit toward a light: bvh_light_traverse, cpu/src/bvh.c:269-315 (returns visibility).
+// Occluded iff some triangle hit closer than the light exists: independent of the visiting order.
 template <bool STRICT, bool COUNT>
-__device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c) {
+__device__ __forceinline__ bool visible_walk(const DBvh& B, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c) {
     RayPre p;
     if (!STRICT) p = ray_pre(o, d);
     float best = FMAX;
     int sp = 1;
-    stk[0] = s.root;
+    stk[0] = B.root;
     while (sp > 0) {
         const int ref = stk[(--sp) * BLOCK];
         if (ref < 0) {
-            const int2 lf = s.leaves[~ref];
+            const int2 lf = B.leaves[~ref];
             if (COUNT) c.shl++;
             for (int i = lf.x; i < lf.x + lf.y; ++i) {
                 int k;
-                const float tt = hit_triangle(o, d, s.tris + 3 * i, k);
+                const float tt = hit_triangle(o, d, B.tris + 3 * i, k);
                 if (COUNT) c.sht++;
                 if (tt < best) {
                     best = tt;
@@ -130,7 +161,7 @@ __device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, 
             }
         } else {
             if (COUNT) c.shi++;
-            const float4* N = s.nodes + 4 * ref;
+            const float4* N = B.nodes + 4 * ref;
             const float4 a = N[0], b = N[1], e = N[2], r = N[3];
             int ni = __float_as_int(r.x), fi = __float_as_int(r.y);
             float nt, ft;
@@ -155,11 +186,46 @@ __device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, 
                 c.err++;
                 break;
             }
-            if (ft < best) stk[(sp++) * BLOCK] = fi;
-            if (nt < best) stk[(sp++) * BLOCK] = ni;
+            if (STRICT) {
+                if (ft < best) stk[(sp++) * BLOCK] = fi;
+                if (nt < best) stk[(sp++) * BLOCK] = ni;
+            } else {
+                const float lim = best * PRUNE_SLACK;
+                if (ft <= lim && ft != FMAX) stk[(sp++) * BLOCK] = fi;
+                if (nt <= lim && nt != FMAX) stk[(sp++) * BLOCK] = ni;
+            }
         }
     }
     return true;
+}
+
+// Closest hit with the kernel's policy; returns the ORIGINAL triangle index (-1 = miss).
+template <bool STRICT, bool COUNT>
+__device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best, int& nd, int* __restrict__ stk,
+                                       Ctr& c) {
+    int hp = -1;
+    bool tie = false;
+    best = FMAX;
+    nd = 0;
+    if (!STRICT && !degenerate(d)) {
+        closest_walk<false, COUNT>(s.acc, o, d, best, hp, nd, tie, stk, c);
+        if (!tie) return hp >= 0 ? s.acc.tri_orig[hp] : -1;
+        c.fb++;
+        hp = -1;
+        best = FMAX;
+        nd = 0;
+    } else if (!STRICT) {
+        c.fb++;
+    }
+    closest_walk<true, COUNT>(s.ref, o, d, best, hp, nd, tie, stk, c);
+    return hp >= 0 ? s.ref.tri_orig[hp] : -1;
+}
+
+template <bool STRICT, bool COUNT>
+__device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c) {
+    if (!STRICT && !degenerate(d)) return visible_walk<false, COUNT>(s.acc, o, d, ld2, stk, c);
+    if (!STRICT) c.fb++;
+    return visible_walk<true, COUNT>(s.ref, o, d, ld2, stk, c);
 }
 
 // ---------------------------------------------------------------- one path (raytrace, iterative)
@@ -191,17 +257,16 @@ __device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, in
     int L = 0;
     bool tail = false;
     for (int it = 0; it < A.bounces; ++it) {
-        float best = FMAX;
-        int hp = -1, nd = 0;
+        float best;
+        int nd;
         if (it == 0) c.prim++;
         else c.refl++;
-        closest<STRICT, COUNT>(s, o, d, best, hp, nd, stk, c);
-        const int orig = hp >= 0 ? s.tri_orig[hp] : -1;
+        const int orig = closest<STRICT, COUNT>(s, o, d, best, nd, stk, c);
         if (it == 0) {
             hit0 = orig;
             t0 = best;
         }
-        if (hp < 0) {  // raytracer.c:132-135
+        if (orig < 0) {  // raytracer.c:132-135
             set3<MAXB>(cols, it, mk(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z));
             L = it + 1;
             break;

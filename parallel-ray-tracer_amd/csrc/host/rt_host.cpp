@@ -230,6 +230,8 @@ struct Builder {
             mx = vmax(mx, tris[t].coords[k]);
         }
     }
+    // partition key: centroid[axis]; "centroid[3]" is the next float of triangle_t, ks.r
+    float key(int t, int axis) const { return axis == 3 ? tris[t].ks.x : tris[t].centroid[axis]; }
     void leaf_stats(const rt_bvh_node& p, int depth) {  // bvh.c:87-94
         st.leaves++;
         st.avg_leaf += p.tr_len;
@@ -293,15 +295,17 @@ struct Builder {
                 okA = okB = false;
                 axis = rth_rand(g) % 4;
                 if (axis == 3) {
-                    // center.arr[3] / centroid[3] read past their arrays in the reference;
-                    // on every shipped scene those attempts fail. The second draw is still consumed.
-                    (void)rth_rand(g);
-                    continue;
+                    // rand() % 4 == 3 reads center.arr[3], size.arr[3] and centroid[3] past their arrays
+                    // (bvh.c:229-231,237,247). Restated as the reference's O-strict build (gcc -O2) lays
+                    // them out: center.arr[3] = size.x, size.arr[3] = (min + max).x, centroid[3] = ks.r.
+                    pos = size.x;
+                    pos += ((float)rth_rand(g) / (float)RAND_MAX - 0.5f) * (p->min.x + p->max.x);
+                } else {
+                    pos = comp(center, axis);
+                    pos += ((float)rth_rand(g) / (float)RAND_MAX - 0.5f) * (comp(size, axis));
                 }
-                pos = comp(center, axis);
-                pos += ((float)rth_rand(g) / (float)RAND_MAX - 0.5f) * (comp(size, axis));
                 for (int i = p->child; i < p->child + p->tr_len && (!okA || !okB); i++) {
-                    bool inA = tris[idx[i]].centroid[axis] < pos;
+                    bool inA = key(idx[i], axis) < pos;
                     okA |= inA;
                     okB |= !inA;
                 }
@@ -316,7 +320,7 @@ struct Builder {
         }
         for (int i = p->child; i < p->child + p->tr_len; i++) {  // bvh.c:244-259
             int t = idx[i];
-            bool inA = tris[t].centroid[axis] < pos;
+            bool inA = key(t, axis) < pos;
             rt_bvh_node* c = inA ? L : R;
             grow(c->min, c->max, t);
             c->tr_len += 1;

@@ -49,7 +49,8 @@ class SceneDesc(ctypes.Structure):
     _fields_ = [("triangles", ctypes.POINTER(Triangle)), ("n_triangles", ctypes.c_int),
                 ("bvh", ctypes.POINTER(BvhNode)), ("n_nodes", ctypes.c_int),
                 ("tri_idx", ctypes.POINTER(ctypes.c_int)),
-                ("lights", ctypes.POINTER(Light)), ("n_lights", ctypes.c_int), ("amb", Vec3)]
+                ("lights", ctypes.POINTER(Light)), ("n_lights", ctypes.c_int), ("amb", Vec3),
+                ("accel", ctypes.c_int)]
 
 
 class Frame(ctypes.Structure):
@@ -59,11 +60,11 @@ class Frame(ctypes.Structure):
 
 
 STAT_FIELDS = ["primary", "reflection", "shadow", "shadow_skipped", "hits", "ch_inner", "ch_leaf",
-               "ch_tri", "sh_inner", "sh_leaf", "sh_tri", "pixels"]
+               "ch_tri", "sh_inner", "sh_leaf", "sh_tri", "pixels", "fallbacks", "stack_overflows"]
 
 
 class Stats(ctypes.Structure):
-    _fields_ = [(f, ctypes.c_ulonglong) for f in STAT_FIELDS] + [("reserved", ctypes.c_ulonglong * 4)]
+    _fields_ = [(f, ctypes.c_ulonglong) for f in STAT_FIELDS] + [("reserved", ctypes.c_ulonglong * 2)]
 
 
 _host = None

@@ -13,6 +13,7 @@ from ._lib import BvhNode, Camera, Frame, Light, Opts, SceneDesc, Stats, Triangl
 P = ctypes.POINTER
 
 KERNELS = {"auto": 0, "strict": 1, "fast": 2}
+ACCEL = {"auto": 0, "reference": 1}
 FLAG_COUNTERS = 1
 
 
@@ -58,8 +59,10 @@ class Renderer:
         if rc != 0:
             raise RtError(f"{what}: status {rc}: {_L.rt_last_error(self._ctx).decode()}")
 
-    def upload(self, scene):
-        """load_to_gpu(): scene = prt.host.Scene with a built BVH"""
+    def upload(self, scene, accel="auto"):
+        """load_to_gpu(): scene = prt.host.Scene with a built BVH (the reference's bvh_build output).
+        accel="auto": the library also builds its own binned-SAH BVH for the fast kernel;
+        accel="reference": the fast kernel traverses the given BVH too."""
         if scene.nodes is None:
             raise RtError("upload: build the BVH first")
         tris = np.ascontiguousarray(scene.triangles)
@@ -68,7 +71,8 @@ class Renderer:
         lights = np.ascontiguousarray(scene.lights)
         d = SceneDesc(tris.ctypes.data_as(P(Triangle)), len(tris), nodes.ctypes.data_as(P(BvhNode)), len(nodes),
                       idx.ctypes.data_as(P(ctypes.c_int)),
-                      lights.ctypes.data_as(P(Light)) if len(lights) else None, len(lights), Vec3(*scene.amb))
+                      lights.ctypes.data_as(P(Light)) if len(lights) else None, len(lights), Vec3(*scene.amb),
+                      ACCEL.get(accel, accel))
         self._chk(_L.rt_upload_scene(self._ctx, ctypes.byref(d)), "rt_upload_scene")
         self.scene = scene
         return self

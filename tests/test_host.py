@@ -80,6 +80,14 @@ def test_bvh_h6_matches_oracle():
     np.testing.assert_array_equal(s.tri_idx, idx)
 
 
+@pytest.mark.parametrize("scene", ["dragon", "two_cars"])
+def test_bvh_h3_standins_match_reference(scene):
+    """multi-material scenes exercise the reference's axis-3 read (bvh.c:229-231) as laid out by O-strict"""
+    s = host.Scene.named(scene).build_bvh(3)
+    raw = np.int32(len(s.nodes)).tobytes() + s.nodes.tobytes() + s.tri_idx.astype(np.int32).tobytes()
+    assert hashlib.md5(raw).hexdigest() == G["standin"][scene]["bvh_h3_md5"]
+
+
 def test_bvh_random_mode_matches_reference():
     s = host.Scene.random(10000).build_bvh(3)
     raw = np.int32(len(s.nodes)).tobytes() + s.nodes.tobytes() + s.tri_idx.astype(np.int32).tobytes()

@@ -121,3 +121,19 @@ def test_thread_count_invariance(only):
     a = only.render(96, 54, threads=1)
     b = only.render(96, 54, threads=7)
     assert frame_md5(a) == frame_md5(b)
+
+
+@pytest.mark.parametrize("scene", ["dragon", "sportscar", "two_cars"])
+def test_standin_scenes_match_reference(scene):
+    """stand-in meshes (prt/scenes.py) rendered by the reference itself: BVH dump and frames."""
+    obj, mtl, lts = scene_paths(scene)
+    ent = G["standin"][scene]
+    assert hashlib.md5(open(obj, "rb").read()).hexdigest() == ent["obj_md5"], "stand-in generator drifted"
+    s = OracleScene.load(obj, mtl, lts)
+    assert s.build_bvh(3) == ent["bvh_h3_nodes"]
+    nodes, idx = s.bvh_export()
+    raw = np.int32(len(nodes) // 32).tobytes() + nodes + idx.astype(np.int32).tobytes()
+    assert hashlib.md5(raw).hexdigest() == ent["bvh_h3_md5"]
+    out = s.render(96, 54)
+    assert frame_md5(out) == ent["96x54_md5"]
+    assert frame_md5(s.render(320, 180)) == ent["320x180_md5"]
