@@ -61,7 +61,9 @@ enum {
 enum {
     RT_KERNEL_AUTO = 0,   /* RT_KERNEL_FAST */
     RT_KERNEL_STRICT = 1, /* reference-order traversal, exact slab divisions: bit-exact by construction */
-    RT_KERNEL_FAST = 2    /* persistent wavefront kernel, reciprocal slab test (same results; tests) */
+    RT_KERNEL_FAST = 2,   /* wavefront pipeline: lean traversal kernels over HBM ray queues (rt_wf.hpp) */
+    RT_KERNEL_PATH = 3,   /* persistent waves, one thread per pixel path (k_persist); also serves spp > 1 */
+    RT_KERNEL_WAVE = 4    /* persistent per-lane ray state machine in one kernel (k_wave); A/B only */
 };
 
 /* Rows rendered: y = row_offset + k * row_stride for k in [0, n_rows). Output rows are compact:

@@ -45,7 +45,7 @@ int rth_triangles_random(size_t n, rth_rng* g, rt_triangle** out);
  * heuristic: 0 axis-0 centre, 1 largest-axis centre, 3 random axis/position (cpu default,
  *   options.h:34; consumes g), 6 32-bin SAH with the reference's FLT_MIN box seed (gpu default,
  *   options.cuh:50), RTH_BVH_BINNED_SAH: this library's O(n log n) binned SAH (surface-area cost,
- *   leaf <= 4) for large meshes. Leaves: tr_len <= 2 or depth 32 (bvh.c:84). Output uses the
+ *   leaf <= 8, depth <= 24) for large meshes. Leaves: tr_len <= 2 or depth 32 (bvh.c:84). Output uses the
  *   reference's node layout; nodes has bvh_len entries. */
 enum { RTH_BVH_BINNED_SAH = 16 };
 typedef struct rth_bvh_stats {

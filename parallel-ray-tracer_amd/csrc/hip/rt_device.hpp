@@ -54,8 +54,9 @@ struct KArgs {
     int* hit;
     float* t;
     unsigned long long* counters;  // RT_NCOUNT slots (rt_stats order)
-    unsigned int* work;            // persistent-kernel tile counter
+    unsigned int* work;            // persistent-kernel tile / pixel counter
     int n_tiles, tiles_x;
+    int refill_below;              // k_wave: leave the traversal loop when fewer lanes than this still trace
 };
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

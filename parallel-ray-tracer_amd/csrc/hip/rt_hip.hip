@@ -16,6 +16,10 @@
 #include "rt_hip.h"
 #include "rt_host.h"
 #include "rt_kernels.hpp"
+#include "rt_wave.hpp"
+#include "rt_wf.hpp"
+
+#include <cstdlib>
 
 namespace {
 
@@ -60,6 +64,14 @@ struct rt_ctx {
     size_t last_pixels = 0;
     unsigned long long* d_counters = nullptr;  // rtd::NCOUNT
     unsigned int* d_work = nullptr;
+    // wavefront pipeline buffers (rt_wf.hpp), sized for wf_pix pixels x wf_lights lights
+    void* wf_mem = nullptr;
+    size_t wf_pix = 0;
+    int wf_lights = 0;
+    float4 *wf_cq[2] = {nullptr, nullptr}, *wf_sq = nullptr, *wf_hrec = nullptr, *wf_lev = nullptr;
+    unsigned char* wf_vis = nullptr;
+    int *wf_fq = nullptr, *wf_plen = nullptr;
+    unsigned* wf_q = nullptr;
     static constexpr int NEV = 64;  // ring of per-launch event pairs (rt_kernel_times)
     hipEvent_t ev0s[NEV] = {}, ev1s[NEV] = {};
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // the last launch's pair
@@ -321,18 +333,138 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
 
 namespace {
 
+// resident workgroups per CU of a persistent kernel (occupancy API, capped at 8)
+template <class K>
+int resident(K kernel, int device) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, rtd::BLOCK, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    return std::min(per_cu, 8) * cus;
+}
+
 template <int MAXB>
-void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int persist_blocks, hipStream_t s) {
+void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int device, hipStream_t s) {
     if (kernel == RT_KERNEL_STRICT) {
         if (count) rtd::k_tiles<MAXB, true, true><<<grid_tiles, rtd::BLOCK, 0, s>>>(A);
         else rtd::k_tiles<MAXB, true, false><<<grid_tiles, rtd::BLOCK, 0, s>>>(A);
+    } else if (kernel == RT_KERNEL_PATH) {
+        // one wave per 8x8 tile, never more workgroups than tiles / 4
+        auto k = count ? rtd::k_persist<MAXB, false, true> : rtd::k_persist<MAXB, false, false>;
+        int blocks = std::max(1, std::min(resident(k, device), (A.n_tiles + 3) / 4));
+        k<<<blocks, rtd::BLOCK, 0, s>>>(A);
     } else {
-        if (count) rtd::k_persist<MAXB, false, true><<<persist_blocks, rtd::BLOCK, 0, s>>>(A);
-        else rtd::k_persist<MAXB, false, false><<<persist_blocks, rtd::BLOCK, 0, s>>>(A);
+        const char* ev = std::getenv("PRT_WAVE_VARIANT");  // "4": the 128-VGPR build (A/B knob)
+        const int variant = ev ? std::atoi(ev) : 0;
+        auto k = count ? rtd::k_wave<MAXB, true> : rtd::k_wave<MAXB, false>;
+        if (variant == 4) k = count ? rtd::k_wave4<MAXB, true> : rtd::k_wave4<MAXB, false>;
+        int blocks = std::max(1, std::min(resident(k, device), (A.n_tiles + 3) / 4));
+        k<<<blocks, rtd::BLOCK, 0, s>>>(A);
     }
 }
 
 rtd::DBvh dview(const DevView& v) { return rtd::DBvh{v.nodes, v.leaves, v.tris, v.orig, v.root}; }
+
+// one allocation for every wavefront buffer, carved at 256-B boundaries
+int wf_reserve(rt_ctx* ctx, size_t npix, int lights) {
+    const int L = std::max(lights, 1);
+    if (ctx->wf_mem && ctx->wf_pix >= npix && ctx->wf_lights >= L) return RT_OK;
+    if (ctx->wf_mem) HIPC(hipFree(ctx->wf_mem));
+    ctx->wf_mem = nullptr;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t sz[] = {al(npix * 32), al(npix * 32), al(npix * L * 32), al(npix * 16), al(npix * rtd::WF_MAXB * 16),
+                         al(npix * L), al(npix * L * 4), al(npix * 4), al(rtd::Q_N * 4)};
+    size_t total = 0;
+    for (size_t b : sz) total += b;
+    HIPC(hipMalloc(&ctx->wf_mem, total));
+    char* p = (char*)ctx->wf_mem;
+    ctx->wf_cq[0] = (float4*)p;
+    p += sz[0];
+    ctx->wf_cq[1] = (float4*)p;
+    p += sz[1];
+    ctx->wf_sq = (float4*)p;
+    p += sz[2];
+    ctx->wf_hrec = (float4*)p;
+    p += sz[3];
+    ctx->wf_lev = (float4*)p;
+    p += sz[4];
+    ctx->wf_vis = (unsigned char*)p;
+    p += sz[5];
+    ctx->wf_fq = (int*)p;
+    p += sz[6];
+    ctx->wf_plen = (int*)p;
+    p += sz[7];
+    ctx->wf_q = (unsigned*)p;
+    ctx->wf_pix = npix;
+    ctx->wf_lights = L;
+    return RT_OK;
+}
+
+template <class K>
+int blocks_resident(K kernel, int device, int cap) {
+    return std::max(1, std::min(resident(kernel, device), cap));
+}
+
+// the wavefront pipeline: ~6 launches per bounce level on the context stream, counts stay on the device
+int launch_wf(rt_ctx* ctx, const rtd::KArgs& K, bool count) {
+    const size_t npix = (size_t)K.W * K.n_rows;
+    int rc = wf_reserve(ctx, npix, K.s.n_lights);
+    if (rc) return rc;
+    rtd::WfArgs A;
+    std::memset(&A, 0, sizeof A);
+    A.s = K.s;
+    for (int i = 0; i < 3; i++) {
+        A.pos[i] = K.pos[i];
+        A.ul[i] = K.ul[i];
+        A.ix[i] = K.ix[i];
+        A.iy[i] = K.iy[i];
+    }
+    A.W = K.W;
+    A.n_rows = K.n_rows;
+    A.row_offset = K.row_offset;
+    A.row_stride = K.row_stride;
+    A.tiles_x = K.tiles_x;
+    A.n_tiles = K.n_tiles;
+    A.bounces = K.bounces;
+    A.cq[0] = ctx->wf_cq[0];
+    A.cq[1] = ctx->wf_cq[1];
+    A.sq = ctx->wf_sq;
+    A.hrec = ctx->wf_hrec;
+    A.vis = ctx->wf_vis;
+    A.fq = ctx->wf_fq;
+    A.lev = ctx->wf_lev;
+    A.plen = ctx->wf_plen;
+    A.rgb = K.rgb;
+    A.hit = K.hit;
+    A.t = K.t;
+    A.q = ctx->wf_q;
+    A.counters = K.counters;
+    A.refill_below = K.refill_below;
+    hipStream_t s = ctx->stream;
+    const int dev = ctx->device;
+    const int B = rtd::WF_BLOCK;
+    const int grid_px = (int)std::max<size_t>(1, std::min<size_t>((npix + B - 1) / B, 2048));
+    const int grid_id = (int)std::max<size_t>(1, std::min<size_t>(((size_t)K.n_tiles * 64 + B - 1) / B, 2048));
+    auto tc = count ? rtd::k_wf_trace<false, true> : rtd::k_wf_trace<false, false>;
+    auto ts = count ? rtd::k_wf_trace<true, true> : rtd::k_wf_trace<true, false>;
+    const int gtc = blocks_resident(tc, dev, (int)((npix + 255) / 256));
+    const int gts = blocks_resident(ts, dev, (int)((npix * std::max(1, K.s.n_lights) + 255) / 256));
+    HIPC(hipMemsetAsync(ctx->wf_q, 0, rtd::Q_N * sizeof(unsigned), s));
+    rtd::k_wf_primary<<<grid_id, B, 0, s>>>(A);
+    for (int lv = 0; lv < K.bounces; lv++) {
+        A.level = lv;
+        A.cur = lv & 1;
+        tc<<<gtc, B, 0, s>>>(A);
+        rtd::k_wf_fallback<false><<<64, B, 0, s>>>(A);
+        rtd::k_wf_shade<<<grid_px, B, 0, s>>>(A);
+        ts<<<gts, B, 0, s>>>(A);
+        rtd::k_wf_fallback<true><<<64, B, 0, s>>>(A);
+        rtd::k_wf_accum<<<grid_px, B, 0, s>>>(A);
+    }
+    rtd::k_wf_fold<<<grid_px, B, 0, s>>>(A);
+    return RT_OK;
+}
 
 }  // namespace
 
@@ -350,7 +482,7 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     int g = 1;
     while (g * g < f->spp) g++;
     if (f->spp < 1 || g * g != f->spp || g > 16) return arg_err(ctx, "rt_render: spp must be a square 1..256");
-    if (f->kernel < RT_KERNEL_AUTO || f->kernel > RT_KERNEL_FAST) return arg_err(ctx, "rt_render: bad kernel");
+    if (f->kernel < RT_KERNEL_AUTO || f->kernel > RT_KERNEL_WAVE) return arg_err(ctx, "rt_render: bad kernel");
     HIPC(hipSetDevice(ctx->device));
     const size_t pixels = (size_t)f->width * f->n_rows;
     float* rgb = out ? out->rgb : nullptr;
@@ -397,22 +529,28 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     A.work = ctx->d_work;
     A.tiles_x = (f->width + 7) / 8;
     A.n_tiles = A.tiles_x * ((f->n_rows + 7) / 8);
-    const int kernel = f->kernel == RT_KERNEL_AUTO ? RT_KERNEL_FAST : f->kernel;
+    int kernel = f->kernel == RT_KERNEL_AUTO ? RT_KERNEL_FAST : f->kernel;
+    // the wavefront pipeline and k_wave render 1 spp; spp > 1 goes to the per-pixel path kernel
+    if ((kernel == RT_KERNEL_FAST || kernel == RT_KERNEL_WAVE) && f->spp > 1) kernel = RT_KERNEL_PATH;
+    if (f->bounces > rtd::WF_MAXB && kernel == RT_KERNEL_FAST) kernel = RT_KERNEL_PATH;
+    A.refill_below = kernel == RT_KERNEL_FAST ? 48 : 32;  // tuning knob, PRT_REFILL_BELOW overrides (0..64)
+    if (const char* e = std::getenv("PRT_REFILL_BELOW")) A.refill_below = std::max(0, std::min(64, std::atoi(e)));
     const bool count = (ctx->flags & RT_FLAG_COUNTERS) != 0;
     dim3 grid((f->width + 15) / 16, (f->n_rows + 15) / 16);
-    int dev_cus = 256;
-    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    int persist_blocks = dev_cus * 4;  // 4 x 256-thread workgroups per CU (LDS stack 34 KiB each)
-    if (persist_blocks * 4 > A.n_tiles) persist_blocks = (A.n_tiles + 3) / 4;
-    if (persist_blocks < 1) persist_blocks = 1;
     HIPC(hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT, ctx->stream));
     HIPC(hipMemsetAsync(ctx->d_work, 0, 256, ctx->stream));
     const int slot = (int)(ctx->launches % rt_ctx::NEV);
     ctx->ev0 = ctx->ev0s[slot];
     ctx->ev1 = ctx->ev1s[slot];
     HIPC(hipEventRecord(ctx->ev0, ctx->stream));
-    if (f->bounces <= 4) launch<4>(A, kernel, count, grid, persist_blocks, ctx->stream);
-    else launch<8>(A, kernel, count, grid, persist_blocks, ctx->stream);
+    if (kernel == RT_KERNEL_FAST) {
+        const int rc = launch_wf(ctx, A, count);
+        if (rc) return rc;
+    } else if (f->bounces <= 4) {
+        launch<4>(A, kernel, count, grid, ctx->device, ctx->stream);
+    } else {
+        launch<8>(A, kernel, count, grid, ctx->device, ctx->stream);
+    }
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(ctx->ev1, ctx->stream));
     ctx->launches++;
@@ -502,6 +640,7 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     free_scene(ctx);
+    if (ctx->wf_mem) (void)hipFree(ctx->wf_mem);
     if (ctx->d_rgb_own) (void)hipFree(ctx->d_rgb_own);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->d_work) (void)hipFree(ctx->d_work);

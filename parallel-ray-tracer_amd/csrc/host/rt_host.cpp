@@ -343,12 +343,14 @@ struct Builder {
         if (dx < 0 || dy < 0 || dz < 0) return 0.0f;
         return 2.0f * (dx * dy + dy * dz + dz * dx);
     }
+    // depth cap 24: the fast kernels stack only deferred far children, at most depth entries (26 slots)
+    static constexpr int SAH_MAX_DEPTH = 24;
     std::vector<float> cen;  // centroid x,y,z per triangle (copied from triangle_t.centroid)
 
     void sah_split(int ni, int depth) {
         rt_bvh_node* p = &bvh[ni];
         const int first = p->child, cnt = p->tr_len;
-        if (cnt <= 2 || depth == 32 || len + 2 > 2 * n) {
+        if (cnt <= 2 || depth == SAH_MAX_DEPTH || len + 2 > 2 * n) {
             leaf_stats(*p, depth);
             return;
         }

@@ -124,13 +124,13 @@ def _check_tree(nodes, idx, tris):
 @pytest.mark.parametrize("scene", ["car_boxed", "dragon"])
 def test_binned_sah_is_a_valid_bvh(scene):
     s = host.Scene.named(scene).build_bvh("binned_sah")
-    assert _check_tree(s.nodes, s.tri_idx, s.triangles) <= 32
+    assert _check_tree(s.nodes, s.tri_idx, s.triangles) <= 24  # the fast kernels' stack bound
     assert s.bvh_stats["max_leaf"] <= 8
 
 
 def test_binned_sah_random_mode_depth_cap():
     s = host.Scene.random(20000).build_bvh("binned_sah")
-    assert _check_tree(s.nodes, s.tri_idx, s.triangles) <= 32
+    assert _check_tree(s.nodes, s.tri_idx, s.triangles) <= 24
 
 
 @pytest.mark.parametrize("W,H", [(1920, 1080), (640, 360), (160, 90), (7, 3)])

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""A/B timing of kernel variants in ONE process (interleaved rounds, §5.4 rule 24 of the HIP guide).
+usage: python tools/ab.py [--scene dragon] [--W 1920 --H 1080] [--rounds 5] [--frames 5] variant...
+variant = "<kernel>[:ENV=VAL,ENV=VAL]", e.g. fast fast:PRT_REFILL_BELOW=16 path strict
+Prints median/min kernel ms per variant and Mrays/s (rays from the kernel counters)."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "parallel-ray-tracer_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="dragon")
+    ap.add_argument("--W", type=int, default=1920)
+    ap.add_argument("--H", type=int, default=1080)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--frames", type=int, default=5)
+    ap.add_argument("variants", nargs="+")
+    a = ap.parse_args()
+    import torch
+    from prt import device, host
+    s = host.Scene.named(a.scene).build_bvh(3)
+    r = device.Renderer(0)
+    r.upload(s)
+    cam = host.camera(a.W, a.H)
+    rgb = torch.empty((a.H, a.W, 3), dtype=torch.float32, device="cuda")
+    res = {v: [] for v in a.variants}
+    rays = {}
+    pixels = {}
+
+    def setenv(v):
+        parts = v.split(":")
+        for k in ("PRT_REFILL_BELOW", "PRT_WAVE_VARIANT"):
+            os.environ.pop(k, None)
+        if len(parts) > 1:
+            for kv in parts[1].split(","):
+                k, val = kv.split("=")
+                os.environ[k] = val
+        return parts[0]
+
+    for rnd in range(a.rounds + 1):
+        for v in a.variants:
+            kern = setenv(v)
+            for _ in range(a.frames):
+                r.render(cam, a.W, a.H, kernel=kern, rgb=rgb)
+            ts = r.kernel_times(a.frames)
+            if rnd > 0:  # round 0 = warm-up
+                res[v] += ts
+            st = r.stats()
+            rays[v] = st["rays"]
+            pixels[v] = st["pixels"]
+    out = {}
+    for v in a.variants:
+        t = sorted(res[v])
+        med = t[len(t) // 2]
+        out[v] = {"median_ms": med, "min_ms": t[0], "Mrays_s": rays[v] / med / 1e3, "rays": rays[v]}
+        print(f"{v:40s} median {med:8.3f} ms  min {t[0]:8.3f} ms  {rays[v] / med / 1e3:9.1f} Mrays/s  rays {rays[v]} px {pixels[v]}")
+    print(json.dumps({"scene": a.scene, "W": a.W, "H": a.H, "results": out}))
+
+
+if __name__ == "__main__":
+    main()

@@ -26,6 +26,8 @@ for s in "${@:-smoke pytest bench}"; do
       bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
       benchq) run bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
       prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+      ab)     run ab 600 python tools/ab.py --rounds 4 --frames 5 path fast fast:PRT_REFILL_BELOW=8 fast:PRT_REFILL_BELOW=16 fast:PRT_REFILL_BELOW=48 fast:PRT_REFILL_BELOW=0 ;;
+      abcar)  run abcar 600 python tools/ab.py --scene car_boxed --rounds 3 --frames 5 path fast fast:PRT_WAVE_VARIANT=4 strict ;;
       *) echo "unknown step $step"; exit 2 ;;
     esac
   done
