@@ -409,7 +409,11 @@ int blocks_resident(K kernel, int device, int cap) {
 // the wavefront pipeline: ~6 launches per bounce level on the context stream, counts stay on the device
 int launch_wf(rt_ctx* ctx, const rtd::KArgs& K, bool count) {
     const size_t npix = (size_t)K.W * K.n_rows;
-    int rc = wf_reserve(ctx, npix, K.s.n_lights);
+    // queue entries are 8x8-tile-padded pixel ids (k_wf_primary writes n_tiles * 64 entries)
+    const size_t nent = (size_t)K.n_tiles * 64;
+    if (nent < npix || K.tiles_x * 8 < K.W || (size_t)K.n_tiles * 8 < (size_t)K.n_rows * K.tiles_x)
+        return arg_err(ctx, "launch_wf: tile grid does not cover the frame");
+    int rc = wf_reserve(ctx, nent, K.s.n_lights);
     if (rc) return rc;
     rtd::WfArgs A;
     std::memset(&A, 0, sizeof A);
@@ -441,6 +445,13 @@ int launch_wf(rt_ctx* ctx, const rtd::KArgs& K, bool count) {
     A.q = ctx->wf_q;
     A.counters = K.counters;
     A.refill_below = K.refill_below;
+    auto knob = [](const char* name, int dflt) {  // A/B tuning knobs (tools/ab.py)
+        const char* e = std::getenv(name);
+        return e ? std::atoi(e) : dflt;
+    };
+    A.chunk_min = std::max(1, knob("PRT_WF_CHUNK_MIN", 64));
+    A.chunk_max = std::max(A.chunk_min, knob("PRT_WF_CHUNK_MAX", 2048));
+    const int bpc = knob("PRT_WF_BPC", 0);  // workgroups per CU for the trace kernels (0 = occupancy API)
     hipStream_t s = ctx->stream;
     const int dev = ctx->device;
     const int B = rtd::WF_BLOCK;
@@ -448,8 +459,13 @@ int launch_wf(rt_ctx* ctx, const rtd::KArgs& K, bool count) {
     const int grid_id = (int)std::max<size_t>(1, std::min<size_t>(((size_t)K.n_tiles * 64 + B - 1) / B, 2048));
     auto tc = count ? rtd::k_wf_trace<false, true> : rtd::k_wf_trace<false, false>;
     auto ts = count ? rtd::k_wf_trace<true, true> : rtd::k_wf_trace<true, false>;
-    const int gtc = blocks_resident(tc, dev, (int)((npix + 255) / 256));
-    const int gts = blocks_resident(ts, dev, (int)((npix * std::max(1, K.s.n_lights) + 255) / 256));
+    int gtc = blocks_resident(tc, dev, (int)((nent + 255) / 256));
+    int gts = blocks_resident(ts, dev, (int)((nent * std::max(1, K.s.n_lights) + 255) / 256));
+    if (bpc > 0) {
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        gtc = gts = bpc * cus;
+    }
     HIPC(hipMemsetAsync(ctx->wf_q, 0, rtd::Q_N * sizeof(unsigned), s));
     rtd::k_wf_primary<<<grid_id, B, 0, s>>>(A);
     for (int lv = 0; lv < K.bounces; lv++) {
@@ -532,7 +548,7 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     int kernel = f->kernel == RT_KERNEL_AUTO ? RT_KERNEL_FAST : f->kernel;
     // the wavefront pipeline and k_wave render 1 spp; spp > 1 goes to the per-pixel path kernel
     if ((kernel == RT_KERNEL_FAST || kernel == RT_KERNEL_WAVE) && f->spp > 1) kernel = RT_KERNEL_PATH;
-    if (f->bounces > rtd::WF_MAXB && kernel == RT_KERNEL_FAST) kernel = RT_KERNEL_PATH;
+    if ((f->bounces > rtd::WF_MAXB || ctx->n_lights > 32) && kernel == RT_KERNEL_FAST) kernel = RT_KERNEL_PATH;
     A.refill_below = kernel == RT_KERNEL_FAST ? 48 : 32;  // tuning knob, PRT_REFILL_BELOW overrides (0..64)
     if (const char* e = std::getenv("PRT_REFILL_BELOW")) A.refill_below = std::max(0, std::min(64, std::atoi(e)));
     const bool count = (ctx->flags & RT_FLAG_COUNTERS) != 0;

@@ -46,6 +46,7 @@ struct WfArgs {
     unsigned* q;            // Q_N counters
     unsigned long long* counters;
     int refill_below;
+    int chunk_min, chunk_max;  // guided self-scheduling window bounds (entries per claim)
 };
 
 __device__ __forceinline__ void ray_store(float4* q, unsigned e, v3 o, v3 d, int tag, float w) {
@@ -65,30 +66,56 @@ __device__ __forceinline__ unsigned wave_append(unsigned* cnt, bool want) {
 }
 
 // ---------------------------------------------------------------- primary rays
+// Positional (no atomics): entry id = 8x8-tile-major pixel id, so a wave's 64 lanes trace one tile.
+// Ids that fall outside a partial edge tile carry pixel -1 and are skipped by every stage.
 __global__ __launch_bounds__(WF_BLOCK) void k_wf_primary(WfArgs A) {
     const unsigned n_ids = (unsigned)A.n_tiles * 64u;
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.q[Q_C0] = n_ids;
+    KArgs K;  // primary_dir reads only the camera fields
+    for (int i = 0; i < 3; i++) {
+        K.pos[i] = A.pos[i];
+        K.ul[i] = A.ul[i];
+        K.ix[i] = A.ix[i];
+        K.iy[i] = A.iy[i];
+    }
     Ctr c = {};
-    for (unsigned id = blockIdx.x * WF_BLOCK + threadIdx.x; id - (threadIdx.x & 63) < n_ids;
-         id += gridDim.x * WF_BLOCK) {
+    for (unsigned id = blockIdx.x * WF_BLOCK + threadIdx.x; id < n_ids; id += gridDim.x * WF_BLOCK) {
         const int tile = (int)(id >> 6), w = (int)(id & 63u);
         const int x = (tile % A.tiles_x) * 8 + (w & 7), k = (tile / A.tiles_x) * 8 + (w >> 3);
-        const bool ok = id < n_ids && x < A.W && k < A.n_rows;
-        const unsigned e = wave_append(&A.q[Q_C0], ok);
-        if (ok) {
-            const int y = A.row_offset + k * A.row_stride;
-            KArgs K;  // primary_dir reads only the camera fields
-            for (int i = 0; i < 3; i++) {
-                K.pos[i] = A.pos[i];
-                K.ul[i] = A.ul[i];
-                K.ix[i] = A.ix[i];
-                K.iy[i] = A.iy[i];
-            }
-            ray_store(A.cq[0], e, mk(A.pos[0], A.pos[1], A.pos[2]), primary_dir(K, (float)x, (float)y), k * A.W + x,
-                      0.0f);
-            c.prim++;
-        }
+        const bool ok = x < A.W && k < A.n_rows;
+        const int y = A.row_offset + k * A.row_stride;
+        ray_store(A.cq[0], id, mk(A.pos[0], A.pos[1], A.pos[2]), primary_dir(K, (float)x, (float)y),
+                  ok ? k * A.W + x : -1, 0.0f);
+        if (ok) c.prim++;
     }
     flush<false>(c, A.counters);
+}
+
+// Block-aggregated append: every thread of the (256-thread) workgroup calls it with its item count;
+// ONE global atomic per workgroup (a single queue counter saturates at ~88 dequeues/us,
+// MI355X_MICROARCH.md "dequeue"). Returns the thread's first slot.
+__device__ __forceinline__ unsigned block_alloc(unsigned cnt, unsigned* gcnt, unsigned* s /* __shared__ [5] */) {
+    const unsigned lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    unsigned x = cnt;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned y = __shfl_up(x, (unsigned)o, 64);
+        if (lane >= (unsigned)o) x += y;
+    }
+    if (lane == 63) s[w] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t0 = s[0], t1 = s[1], t2 = s[2], t3 = s[3], tot = t0 + t1 + t2 + t3;
+        const unsigned base = tot ? atomicAdd(gcnt, tot) : 0u;
+        s[0] = base;
+        s[1] = base + t0;
+        s[2] = base + t0 + t1;
+        s[3] = base + t0 + t1 + t2;
+    }
+    __syncthreads();
+    const unsigned r = s[w] + x - cnt;
+    __syncthreads();
+    return r;
 }
 
 // ---------------------------------------------------------------- traversal (fast walk)
@@ -103,46 +130,67 @@ __global__ __launch_bounds__(WF_BLOCK) void k_wf_trace(WfArgs A) {
     unsigned* work = &A.q[Q_WORK];
     if (blockIdx.x == 0 && threadIdx.x == 0) A.q[Q_FWORK] = 0;  // for the fallback kernel that follows
     Ctr c = {};
-    bool act = false, exhausted = false, tie = false;
+    bool act = false, tie = false;
     unsigned e = 0;
     int slot = 0, cur = 0, sp = 0, hp = -1, nd = 0;
     float best = FMAX, ld2 = 0.0f;
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0);
     RayPre p = {};
+    // Guided self-scheduling: the wave claims a window of queue entries with ONE atomic, sized to the
+    // remaining work (rem / (2 * waves), 64..2048 entries), and refills its idle lanes from the window
+    // without further atomics. Wave-uniform state.
+    const unsigned lane = threadIdx.x & 63u;
+    const unsigned nwaves = gridDim.x * (WF_BLOCK / 64);
+    unsigned wnext = 0, wend = 0;
+    bool drained = false;
     for (;;) {
-        // ---- refill idle lanes (one returning atomic per wave)
+        // ---- refill idle lanes from the wave's window
         for (;;) {
-            const unsigned long long need = __ballot(!act && !exhausted);
-            if (!need) break;
-            const int leader = __ffsll((long long)need) - 1;
-            unsigned base = 0;
-            if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(work, (unsigned)__popcll(need));
-            base = __shfl(base, leader, 64);
-            if (!act && !exhausted) {
-                e = base + (unsigned)__popcll(need & ((1ull << (threadIdx.x & 63)) - 1ull));
-                if (e >= n) {
-                    exhausted = true;
+            const unsigned long long need = __ballot(!act);
+            if (!need || drained) break;
+            if (wnext >= wend) {
+                unsigned start = 0, chunk = 0;
+                if (lane == 0) {
+                    const unsigned taken = __atomic_load_n(work, __ATOMIC_RELAXED);
+                    const unsigned rem = taken < n ? n - taken : 0u;
+                    chunk = min((unsigned)A.chunk_max, max((unsigned)A.chunk_min, rem / (2u * nwaves)));
+                    start = atomicAdd(work, chunk);
+                }
+                start = __shfl(start, 0, 64);
+                chunk = __shfl(chunk, 0, 64);
+                if (start >= n) {
+                    drained = true;
+                    break;
+                }
+                wnext = start;
+                wend = min(start + chunk, n);
+            }
+            const unsigned take = min((unsigned)__popcll(need), wend - wnext);
+            const unsigned rank = (unsigned)__popcll(need & ((1ull << lane) - 1ull));
+            if (!act && rank < take) {
+                e = wnext + rank;
+                const float4 a = q[2 * e], b = q[2 * e + 1];
+                o = mk(a.x, a.y, a.z);
+                d = mk(b.x, b.y, b.z);
+                slot = __float_as_int(a.w);
+                ld2 = b.w;
+                if (!SHADOW && slot < 0) {
+                    // padding entry of a partial edge tile: nothing to trace
+                } else if (degenerate(d)) {  // NaN-slab semantics: strict walk (fallback kernel)
+                    A.fq[atomicAdd(&A.q[Q_F], 1u)] = (int)e;
+                    c.fb++;
                 } else {
-                    const float4 a = q[2 * e], b = q[2 * e + 1];
-                    o = mk(a.x, a.y, a.z);
-                    d = mk(b.x, b.y, b.z);
-                    slot = __float_as_int(a.w);
-                    ld2 = b.w;
-                    if (degenerate(d)) {  // NaN-slab semantics: strict walk (fallback kernel)
-                        A.fq[atomicAdd(&A.q[Q_F], 1u)] = (int)e;
-                        c.fb++;
-                    } else {
-                        p = ray_pre(o, d);
-                        best = FMAX;
-                        hp = -1;
-                        nd = 0;
-                        tie = false;
-                        sp = 0;
-                        cur = B.root;
-                        act = true;
-                    }
+                    p = ray_pre(o, d);
+                    best = FMAX;
+                    hp = -1;
+                    nd = 0;
+                    tie = false;
+                    sp = 0;
+                    cur = B.root;
+                    act = true;
                 }
             }
+            wnext += take;
         }
         if (!__ballot(act)) break;  // queue drained, every lane idle
         // ---- traverse until too few lanes remain busy
@@ -239,7 +287,7 @@ __global__ __launch_bounds__(WF_BLOCK) void k_wf_trace(WfArgs A) {
             }
             const unsigned long long tr = __ballot(act);
             if (!tr) break;
-            if (__popcll(tr) < (unsigned)A.refill_below && __ballot(!exhausted)) break;
+            if (__popcll(tr) < (unsigned)A.refill_below && !drained) break;
         }
     }
     flush<COUNT>(c, A.counters);
@@ -313,18 +361,18 @@ __global__ __launch_bounds__(WF_BLOCK) void k_wf_shade(WfArgs A) {
         A.q[Q_WORK] = 0;
         A.q[Q_F] = 0;
     }
+    __shared__ unsigned s_alloc[4];
     Ctr c = {};
     const unsigned stride = gridDim.x * WF_BLOCK;
-    for (unsigned e0 = blockIdx.x * WF_BLOCK + (threadIdx.x & ~63u); e0 < n; e0 += stride) {
-        const unsigned e = e0 + (threadIdx.x & 63u);
-        const bool valid = e < n;
+    for (unsigned e0 = blockIdx.x * WF_BLOCK; e0 < n; e0 += stride) {  // uniform per workgroup
+        const unsigned e = e0 + threadIdx.x;
         bool hit = false, refl = false;
-        v3 ip = mk(0, 0, 0), r = mk(0, 0, 0);
-        int pix = 0, og = -1;
-        if (valid) {
+        v3 ip = mk(0, 0, 0), r = mk(0, 0, 0), nrm = mk(0, 0, 0), v = mk(0, 0, 0), ks = v, kd = v;
+        int pix = -1, og = -1;
+        if (e < n) pix = __float_as_int(A.cq[A.cur][2 * e].w);
+        if (pix >= 0) {
             const float4 a = A.cq[A.cur][2 * e], b = A.cq[A.cur][2 * e + 1], h = A.hrec[e];
             const v3 o = mk(a.x, a.y, a.z), d = mk(b.x, b.y, b.z);
-            pix = __float_as_int(a.w);
             og = __float_as_int(h.y);
             const float best = h.x;
             const int nd = __float_as_int(h.z);
@@ -342,9 +390,11 @@ __global__ __launch_bounds__(WF_BLOCK) void k_wf_shade(WfArgs A) {
                 ip = add(o, mul(d, best));
                 const float4 sh0 = s.shade[2 * og];
                 const int m = __float_as_int(sh0.w);
-                const v3 nrm = xyz(s.shade[2 * og + nd]);
-                const v3 ks = xyz(s.mats[3 * m]), kd = xyz(s.mats[3 * m + 1]), kr = xyz(s.mats[3 * m + 2]);
-                const v3 v = mul(d, -1.0f);
+                nrm = xyz(s.shade[2 * og + nd]);
+                ks = xyz(s.mats[3 * m]);
+                kd = xyz(s.mats[3 * m + 1]);
+                const v3 kr = xyz(s.mats[3 * m + 2]);
+                v = mul(d, -1.0f);
                 lv->w = __int_as_float(m);
                 const v3 dd = mul(v, -1.0f);  // raytracer.c:163-166
                 const v3 ns = mul(nrm, 2.0f * __builtin_fabsf(dot(dd, nrm)));
@@ -353,30 +403,28 @@ __global__ __launch_bounds__(WF_BLOCK) void k_wf_shade(WfArgs A) {
                 refl = rec && A.level + 1 < A.bounces;
                 if (!refl) A.plen[pix] = (A.level + 1) | (rec ? (1 << 16) : 0);
                 for (int j = 0; j < L; j++) A.vis[(size_t)e * L + j] = 0;
-                (void)ks;
-                (void)kd;
             }
         }
-        // shadow rays, one light at a time so that the wave's appends stay aggregated
-        for (int j = 0; j < L; j++) {
-            bool emit = false;
-            LightTerm T;
-            if (hit) {
-                const int nd = __float_as_int(A.hrec[e].z);
-                const int m = __float_as_int(s.shade[2 * og].w);
-                T = light_term(s, j, ip, xyz(s.shade[2 * og + nd]), mul(mk(A.cq[A.cur][2 * e + 1].x,
-                               A.cq[A.cur][2 * e + 1].y, A.cq[A.cur][2 * e + 1].z), -1.0f),
-                               xyz(s.mats[3 * m]), xyz(s.mats[3 * m + 1]));
-                emit = T.front;
-                if (emit) c.shad++;
-                else c.skip++;
+        // shadow rays past the back-face test (raytracer.c:66-67), then their queue slots
+        unsigned emask = 0;
+        if (hit)
+            for (int j = 0; j < L; j++) {
+                if (light_term(s, j, ip, nrm, v, ks, kd).front) {
+                    emask |= 1u << j;
+                    c.shad++;
+                } else {
+                    c.skip++;
+                }
             }
-            const unsigned slot = wave_append(&A.q[Q_S], emit);
-            if (emit) ray_store(A.sq, slot, ip, T.l, (int)(e * L + j), T.ld2);
-        }
-        const unsigned slot = wave_append(&A.q[nxt], refl);
+        unsigned slot = block_alloc((unsigned)__popc(emask), &A.q[Q_S], s_alloc);
+        for (int j = 0; emask >> j; j++)
+            if ((emask >> j) & 1u) {
+                const LightTerm T = light_term(s, j, ip, nrm, v, ks, kd);
+                ray_store(A.sq, slot++, ip, T.l, (int)(e * L + j), T.ld2);
+            }
+        const unsigned rslot = block_alloc(refl ? 1u : 0u, &A.q[nxt], s_alloc);
         if (refl) {
-            ray_store(A.cq[nxt], slot, ip, r, pix, 0.0f);
+            ray_store(A.cq[nxt], rslot, ip, r, pix, 0.0f);
             c.refl++;
         }
     }
@@ -393,12 +441,15 @@ __global__ __launch_bounds__(WF_BLOCK) void k_wf_accum(WfArgs A) {
         A.q[Q_F] = 0;
     }
     for (unsigned e = blockIdx.x * WF_BLOCK + threadIdx.x; e < n; e += gridDim.x * WF_BLOCK) {
+        const float4 a = A.cq[A.cur][2 * e];
+        const int pix = __float_as_int(a.w);
+        if (pix < 0) continue;  // padding entry of a partial edge tile
         const float4 h = A.hrec[e];
         const int og = __float_as_int(h.y);
         if (og < 0) continue;
-        const float4 a = A.cq[A.cur][2 * e], b = A.cq[A.cur][2 * e + 1];
+        const float4 b = A.cq[A.cur][2 * e + 1];
         const v3 o = mk(a.x, a.y, a.z), d = mk(b.x, b.y, b.z);
-        const int pix = __float_as_int(a.w), nd = __float_as_int(h.z);
+        const int nd = __float_as_int(h.z);
         const v3 ip = add(o, mul(d, h.x));
         const int m = __float_as_int(s.shade[2 * og].w);
         const v3 nrm = xyz(s.shade[2 * og + nd]);

@@ -35,7 +35,7 @@ def main():
 
     def setenv(v):
         parts = v.split(":")
-        for k in ("PRT_REFILL_BELOW", "PRT_WAVE_VARIANT"):
+        for k in ("PRT_REFILL_BELOW", "PRT_WAVE_VARIANT", "PRT_WF_CHUNK_MIN", "PRT_WF_CHUNK_MAX", "PRT_WF_BPC"):
             os.environ.pop(k, None)
         if len(parts) > 1:
             for kv in parts[1].split(","):

@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Traversal work per kernel on one frame (RT_FLAG_COUNTERS): node visits / triangle tests per ray."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "parallel-ray-tracer_amd"))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+from prt import device, host  # noqa: E402
+
+scene = sys.argv[1] if len(sys.argv) > 1 else "dragon"
+W, H = 1920, 1080
+s = host.Scene.named(scene).build_bvh(3)
+out = {}
+for k in sys.argv[2:] or ["path", "fast", "strict"]:
+    r = device.Renderer(0, counters=True)
+    r.upload(s)
+    rgb = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    r.render(host.camera(W, H), W, H, kernel=k, rgb=rgb)
+    st = r.stats()
+    cl = st["primary"] + st["reflection"]
+    st["ch_inner_per_ray"] = st["ch_inner"] / cl
+    st["ch_tri_per_ray"] = st["ch_tri"] / cl
+    st["sh_inner_per_ray"] = st["sh_inner"] / max(1, st["shadow"])
+    st["sh_tri_per_ray"] = st["sh_tri"] / max(1, st["shadow"])
+    out[k] = st
+    print(k, {a: round(b, 2) if isinstance(b, float) else b for a, b in st.items()})
+    r.close()
+print(json.dumps(out))
