@@ -12,7 +12,8 @@
  * contexts may be driven from distinct host threads.
  *
  * The per-pixel hot path (ray generation, BVH traversal, ray-triangle intersection, Lambert/Blinn
- * shading with shadow rays, the BOUNCES reflection loop, clamp) runs in ONE HIP kernel per frame.
+ * shading with shadow rays, the BOUNCES reflection loop, clamp) runs in ONE HIP kernel per frame
+ * (RT_KERNEL_WAVEFRONT, an A/B alternative, splits it into ~6 launches per bounce).
  */
 #ifndef RT_HIP_H
 #define RT_HIP_H
@@ -61,8 +62,8 @@ enum {
 enum {
     RT_KERNEL_AUTO = 0,   /* RT_KERNEL_FAST */
     RT_KERNEL_STRICT = 1, /* reference-order traversal, exact slab divisions: bit-exact by construction */
-    RT_KERNEL_FAST = 2,   /* wavefront pipeline: lean traversal kernels over HBM ray queues (rt_wf.hpp) */
-    RT_KERNEL_PATH = 3,   /* persistent waves, one thread per pixel path (k_persist); also serves spp > 1 */
+    RT_KERNEL_FAST = 2,   /* persistent waves, one 8x8 tile per wave, one lane per pixel path (k_persist) */
+    RT_KERNEL_WAVEFRONT = 3, /* wavefront pipeline: traversal kernels over HBM ray queues (rt_wf.hpp); A/B only */
     RT_KERNEL_WAVE = 4    /* persistent per-lane ray state machine in one kernel (k_wave); A/B only */
 };
 

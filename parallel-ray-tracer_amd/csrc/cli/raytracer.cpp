@@ -2,7 +2,7 @@
 //
 //   raytracer [threads] [ntris] [--scene NAME] [--assets DIR] [--width W] [--height H]
 //             [--bounces B] [--iterations K] [--warmup W] [--bvh-heuristic H] [--seed S]
-//             [--gpus N] [--spp S] [--kernel fast|strict] [--out FILE.bmp]
+//             [--gpus N] [--spp S] [--kernel fast|strict|wavefront|wave] [--out FILE.bmp]
 //
 // Positional arguments and defaults are the reference's (options.h: 1920x1080, car_boxed, BOUNCES 4,
 // ITERATIONS 1, BVH_HEURISTIC 3, SEED 1; main.c:97-131: `threads` in 1..63, `ntris` = random mode).
@@ -142,7 +142,14 @@ int main(int argc, char** argv) {
             return EXIT_FAILURE;
         }
     }
-    int kern = a.kernel == "strict" ? RT_KERNEL_STRICT : RT_KERNEL_FAST;
+    int kern = a.kernel == "strict" ? RT_KERNEL_STRICT
+               : a.kernel == "wavefront" ? RT_KERNEL_WAVEFRONT
+               : a.kernel == "wave" ? RT_KERNEL_WAVE
+               : a.kernel == "fast" ? RT_KERNEL_FAST : -1;
+    if (kern < 0) {
+        std::fprintf(stderr, "unknown --kernel %s\n", a.kernel.c_str());
+        return EXIT_FAILURE;
+    }
     std::vector<float> frame((size_t)a.W * a.H * 3);
     std::vector<std::vector<float>> part(G);
     unsigned long long rays = 0;

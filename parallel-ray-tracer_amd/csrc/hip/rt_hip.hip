@@ -349,9 +349,11 @@ void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int de
     if (kernel == RT_KERNEL_STRICT) {
         if (count) rtd::k_tiles<MAXB, true, true><<<grid_tiles, rtd::BLOCK, 0, s>>>(A);
         else rtd::k_tiles<MAXB, true, false><<<grid_tiles, rtd::BLOCK, 0, s>>>(A);
-    } else if (kernel == RT_KERNEL_PATH) {
+    } else if (kernel == RT_KERNEL_FAST) {
         // one wave per 8x8 tile, never more workgroups than tiles / 4
         auto k = count ? rtd::k_persist<MAXB, false, true> : rtd::k_persist<MAXB, false, false>;
+        if (const char* e = std::getenv("PRT_PERSIST_REG"); e && std::atoi(e) == 0)  // A/B: stack-only walk
+            k = count ? rtd::k_persist<MAXB, false, true, false> : rtd::k_persist<MAXB, false, false, false>;
         int blocks = std::max(1, std::min(resident(k, device), (A.n_tiles + 3) / 4));
         k<<<blocks, rtd::BLOCK, 0, s>>>(A);
     } else {
@@ -547,9 +549,9 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     A.n_tiles = A.tiles_x * ((f->n_rows + 7) / 8);
     int kernel = f->kernel == RT_KERNEL_AUTO ? RT_KERNEL_FAST : f->kernel;
     // the wavefront pipeline and k_wave render 1 spp; spp > 1 goes to the per-pixel path kernel
-    if ((kernel == RT_KERNEL_FAST || kernel == RT_KERNEL_WAVE) && f->spp > 1) kernel = RT_KERNEL_PATH;
-    if ((f->bounces > rtd::WF_MAXB || ctx->n_lights > 32) && kernel == RT_KERNEL_FAST) kernel = RT_KERNEL_PATH;
-    A.refill_below = kernel == RT_KERNEL_FAST ? 48 : 32;  // tuning knob, PRT_REFILL_BELOW overrides (0..64)
+    if ((kernel == RT_KERNEL_WAVEFRONT || kernel == RT_KERNEL_WAVE) && f->spp > 1) kernel = RT_KERNEL_FAST;
+    if ((f->bounces > rtd::WF_MAXB || ctx->n_lights > 32) && kernel == RT_KERNEL_WAVEFRONT) kernel = RT_KERNEL_FAST;
+    A.refill_below = kernel == RT_KERNEL_WAVEFRONT ? 48 : 32;  // tuning knob, PRT_REFILL_BELOW overrides (0..64)
     if (const char* e = std::getenv("PRT_REFILL_BELOW")) A.refill_below = std::max(0, std::min(64, std::atoi(e)));
     const bool count = (ctx->flags & RT_FLAG_COUNTERS) != 0;
     dim3 grid((f->width + 15) / 16, (f->n_rows + 15) / 16);
@@ -559,7 +561,7 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     ctx->ev0 = ctx->ev0s[slot];
     ctx->ev1 = ctx->ev1s[slot];
     HIPC(hipEventRecord(ctx->ev0, ctx->stream));
-    if (kernel == RT_KERNEL_FAST) {
+    if (kernel == RT_KERNEL_WAVEFRONT) {
         const int rc = launch_wf(ctx, A, count);
         if (rc) return rc;
     } else if (f->bounces <= 4) {

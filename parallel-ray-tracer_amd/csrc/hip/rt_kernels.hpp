@@ -65,22 +65,66 @@ __device__ __forceinline__ bool degenerate(v3 d) { return d.x == 0.0f || d.y == 
 // with the best hit is always reached (and the tie detected) despite the reciprocal test's rounding.
 constexpr float PRUNE_SLACK = 1.0000005f;
 
+// ---------------------------------------------------------------- one interior node
+// Entry distances of both children of record `ref`, nearer child first (empty child / miss: FMAX).
+template <bool STRICT>
+__device__ __forceinline__ void children(const DBvh& B, int ref, v3 o, v3 d, const RayPre& p, int& ni, float& nt,
+                                         int& fi, float& ft) {
+    const float4* N = B.nodes + 4 * ref;
+    const float4 a = N[0], b = N[1], e = N[2], r = N[3];
+    ni = __float_as_int(r.x);
+    fi = __float_as_int(r.y);
+    if (STRICT) {
+        nt = box_exact(mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), o, d);
+        ft = box_exact(mk(b.z, b.w, e.x), mk(e.y, e.z, e.w), o, d);
+    } else {
+        nt = box_fast(a.x, a.y, a.z, a.w, b.x, b.y, p);
+        ft = box_fast(b.z, b.w, e.x, e.y, e.z, e.w, p);
+    }
+    if (ni == EMPTY_REF) nt = FMAX;
+    if (fi == EMPTY_REF) ft = FMAX;
+    if (ft < nt) {
+        const int ti = ni;
+        const float tt = nt;
+        ni = fi;
+        nt = ft;
+        fi = ti;
+        ft = tt;
+    }
+}
+
+// Is a child whose box is entered at t worth visiting? Strict: the reference's test (bvh.c:343-352).
+template <bool STRICT>
+__device__ __forceinline__ bool visit(float t, float best) {
+    if (STRICT) return t < best;
+    return t <= best * PRUNE_SLACK && t != FMAX;
+}
+
 // ---------------------------------------------------------------- closest hit
 // bvh_traverse, cpu/src/bvh.c:317-358. Stack of node refs in LDS, [depth][lane] so that the 64 lanes
 // of a wave always hit 64 distinct banks whatever their stack depths.
+// REG: the node to visit next is kept in a register and only the farther child goes through the LDS
+// stack (the reference pushes far then near and pops near at once: the same visiting sequence, one
+// LDS round trip less on the dependent chain of most steps).
 // Returns the leaf position of the best hit in hp (-1: none); `tie` = the final best was matched by
 // another triangle (fast walk only).
-template <bool STRICT, bool COUNT>
+template <bool STRICT, bool COUNT, bool REG = true>
 __device__ __forceinline__ void closest_walk(const DBvh& B, v3 o, v3 d, float& best, int& hp, int& nd, bool& tie,
                                              int* __restrict__ stk, Ctr& c) {
-    RayPre p;
+    RayPre p = {};
     if (!STRICT) p = ray_pre(o, d);
-    int sp = 1;
-    stk[0] = B.root;
-    while (sp > 0) {
-        const int ref = stk[(--sp) * BLOCK];
-        if (ref < 0) {
-            const int2 lf = B.leaves[~ref];
+    int sp = 0, cur = B.root;
+    if (!REG) {
+        stk[0] = B.root;
+        sp = 1;
+    }
+    for (;;) {
+        if (!REG) {
+            if (sp == 0) break;
+            cur = stk[(--sp) * BLOCK];
+        }
+        if (cur < 0) {
+            const int2 lf = B.leaves[~cur];
             if (COUNT) c.chl++;
             for (int i = lf.x; i < lf.x + lf.y; ++i) {
                 int k;
@@ -97,56 +141,56 @@ __device__ __forceinline__ void closest_walk(const DBvh& B, v3 o, v3 d, float& b
             }
         } else {
             if (COUNT) c.chi++;
-            const float4* N = B.nodes + 4 * ref;
-            const float4 a = N[0], b = N[1], e = N[2], r = N[3];
-            int ni = __float_as_int(r.x), fi = __float_as_int(r.y);
+            int ni, fi;
             float nt, ft;
-            if (STRICT) {
-                nt = box_exact(mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), o, d);
-                ft = box_exact(mk(b.z, b.w, e.x), mk(e.y, e.z, e.w), o, d);
-            } else {
-                nt = box_fast(a.x, a.y, a.z, a.w, b.x, b.y, p);
-                ft = box_fast(b.z, b.w, e.x, e.y, e.z, e.w, p);
-            }
-            if (ni == EMPTY_REF) nt = FMAX;
-            if (fi == EMPTY_REF) ft = FMAX;
-            if (ft < nt) {
-                const int ti = ni;
-                const float tt = nt;
-                ni = fi;
-                nt = ft;
-                fi = ti;
-                ft = tt;
-            }
+            children<STRICT>(B, cur, o, d, p, ni, nt, fi, ft);
+            const bool vn = visit<STRICT>(nt, best), vf = visit<STRICT>(ft, best);
             if (sp + 2 > STACK) {  // cannot happen for depth <= 32 BVHs; reported, never silent
                 c.err++;
                 break;
             }
-            if (STRICT) {
-                if (ft < best) stk[(sp++) * BLOCK] = fi;
-                if (nt < best) stk[(sp++) * BLOCK] = ni;
+            if (REG) {
+                if (vn) {
+                    if (vf) stk[(sp++) * BLOCK] = fi;
+                    cur = ni;
+                    continue;
+                }
+                if (vf) {
+                    cur = fi;
+                    continue;
+                }
             } else {
-                const float lim = best * PRUNE_SLACK;
-                if (ft <= lim && ft != FMAX) stk[(sp++) * BLOCK] = fi;
-                if (nt <= lim && nt != FMAX) stk[(sp++) * BLOCK] = ni;
+                if (vf) stk[(sp++) * BLOCK] = fi;
+                if (vn) stk[(sp++) * BLOCK] = ni;
+                continue;
             }
+        }
+        if (REG) {
+            if (sp == 0) break;
+            cur = stk[(--sp) * BLOCK];
         }
     }
 }
 
 // Any hit toward a light: bvh_light_traverse, cpu/src/bvh.c:269-315 (returns visibility).
 // Occluded iff some triangle hit closer than the light exists: independent of the visiting order.
-template <bool STRICT, bool COUNT>
+template <bool STRICT, bool COUNT, bool REG = true>
 __device__ __forceinline__ bool visible_walk(const DBvh& B, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c) {
-    RayPre p;
+    RayPre p = {};
     if (!STRICT) p = ray_pre(o, d);
     float best = FMAX;
-    int sp = 1;
-    stk[0] = B.root;
-    while (sp > 0) {
-        const int ref = stk[(--sp) * BLOCK];
-        if (ref < 0) {
-            const int2 lf = B.leaves[~ref];
+    int sp = 0, cur = B.root;
+    if (!REG) {
+        stk[0] = B.root;
+        sp = 1;
+    }
+    for (;;) {
+        if (!REG) {
+            if (sp == 0) break;
+            cur = stk[(--sp) * BLOCK];
+        }
+        if (cur < 0) {
+            const int2 lf = B.leaves[~cur];
             if (COUNT) c.shl++;
             for (int i = lf.x; i < lf.x + lf.y; ++i) {
                 int k;
@@ -161,46 +205,40 @@ __device__ __forceinline__ bool visible_walk(const DBvh& B, v3 o, v3 d, float ld
             }
         } else {
             if (COUNT) c.shi++;
-            const float4* N = B.nodes + 4 * ref;
-            const float4 a = N[0], b = N[1], e = N[2], r = N[3];
-            int ni = __float_as_int(r.x), fi = __float_as_int(r.y);
+            int ni, fi;
             float nt, ft;
-            if (STRICT) {
-                nt = box_exact(mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), o, d);
-                ft = box_exact(mk(b.z, b.w, e.x), mk(e.y, e.z, e.w), o, d);
-            } else {
-                nt = box_fast(a.x, a.y, a.z, a.w, b.x, b.y, p);
-                ft = box_fast(b.z, b.w, e.x, e.y, e.z, e.w, p);
-            }
-            if (ni == EMPTY_REF) nt = FMAX;
-            if (fi == EMPTY_REF) ft = FMAX;
-            if (ft < nt) {
-                const int ti = ni;
-                const float tt = nt;
-                ni = fi;
-                nt = ft;
-                fi = ti;
-                ft = tt;
-            }
+            children<STRICT>(B, cur, o, d, p, ni, nt, fi, ft);
+            const bool vn = visit<STRICT>(nt, best), vf = visit<STRICT>(ft, best);
             if (sp + 2 > STACK) {
                 c.err++;
                 break;
             }
-            if (STRICT) {
-                if (ft < best) stk[(sp++) * BLOCK] = fi;
-                if (nt < best) stk[(sp++) * BLOCK] = ni;
+            if (REG) {
+                if (vn) {
+                    if (vf) stk[(sp++) * BLOCK] = fi;
+                    cur = ni;
+                    continue;
+                }
+                if (vf) {
+                    cur = fi;
+                    continue;
+                }
             } else {
-                const float lim = best * PRUNE_SLACK;
-                if (ft <= lim && ft != FMAX) stk[(sp++) * BLOCK] = fi;
-                if (nt <= lim && nt != FMAX) stk[(sp++) * BLOCK] = ni;
+                if (vf) stk[(sp++) * BLOCK] = fi;
+                if (vn) stk[(sp++) * BLOCK] = ni;
+                continue;
             }
+        }
+        if (REG) {
+            if (sp == 0) break;
+            cur = stk[(--sp) * BLOCK];
         }
     }
     return true;
 }
 
 // Closest hit with the kernel's policy; returns the ORIGINAL triangle index (-1 = miss).
-template <bool STRICT, bool COUNT>
+template <bool STRICT, bool COUNT, bool REG = true>
 __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best, int& nd, int* __restrict__ stk,
                                        Ctr& c) {
     int hp = -1;
@@ -208,7 +246,7 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
     best = FMAX;
     nd = 0;
     if (!STRICT && !degenerate(d)) {
-        closest_walk<false, COUNT>(s.acc, o, d, best, hp, nd, tie, stk, c);
+        closest_walk<false, COUNT, REG>(s.acc, o, d, best, hp, nd, tie, stk, c);
         if (!tie) return hp >= 0 ? s.acc.tri_orig[hp] : -1;
         c.fb++;
         hp = -1;
@@ -217,15 +255,15 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
     } else if (!STRICT) {
         c.fb++;
     }
-    closest_walk<true, COUNT>(s.ref, o, d, best, hp, nd, tie, stk, c);
+    closest_walk<true, COUNT, REG>(s.ref, o, d, best, hp, nd, tie, stk, c);
     return hp >= 0 ? s.ref.tri_orig[hp] : -1;
 }
 
-template <bool STRICT, bool COUNT>
+template <bool STRICT, bool COUNT, bool REG = true>
 __device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c) {
-    if (!STRICT && !degenerate(d)) return visible_walk<false, COUNT>(s.acc, o, d, ld2, stk, c);
+    if (!STRICT && !degenerate(d)) return visible_walk<false, COUNT, REG>(s.acc, o, d, ld2, stk, c);
     if (!STRICT) c.fb++;
-    return visible_walk<true, COUNT>(s.ref, o, d, ld2, stk, c);
+    return visible_walk<true, COUNT, REG>(s.ref, o, d, ld2, stk, c);
 }
 
 // ---------------------------------------------------------------- one path (raytrace, iterative)
@@ -242,7 +280,7 @@ __device__ __forceinline__ void seti(int (&a)[MAXB], int i, int v) {
         if (k == i) a[k] = v;
 }
 
-template <int MAXB, bool STRICT, bool COUNT>
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true>
 __device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0) {
     const DScene& s = A.s;
     v3 o = mk(A.pos[0], A.pos[1], A.pos[2]);
@@ -261,7 +299,7 @@ __device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, in
         int nd;
         if (it == 0) c.prim++;
         else c.refl++;
-        const int orig = closest<STRICT, COUNT>(s, o, d, best, nd, stk, c);
+        const int orig = closest<STRICT, COUNT, REG>(s, o, d, best, nd, stk, c);
         if (it == 0) {
             hit0 = orig;
             t0 = best;
@@ -298,7 +336,7 @@ __device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, in
                 c.skip++;
             } else {
                 c.shad++;
-                V = visible<STRICT, COUNT>(s, ip, l, ld2, stk, c) ? 1 : 0;
+                V = visible<STRICT, COUNT, REG>(s, ip, l, ld2, stk, c) ? 1 : 0;
             }
             const float fV = (float)V;
             col.x = col.x + fV * kl.x * cr.x / mg;
@@ -356,7 +394,7 @@ __device__ __forceinline__ v3 primary_dir(const KArgs& A, float fx, float fy) {
     return d;
 }
 
-template <int MAXB, bool STRICT, bool COUNT>
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true>
 __device__ __forceinline__ void render_pixel(const KArgs& A, int x, int k, int* __restrict__ stk, Ctr& c) {
     const int y = A.row_offset + k * A.row_stride;
     const size_t o = (size_t)k * A.W + x;
@@ -364,7 +402,7 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, int x, int k, int* 
     float t0 = FMAX;
     v3 col;
     if (A.spp <= 1) {
-        col = clamp01(trace_path<MAXB, STRICT, COUNT>(A, primary_dir(A, (float)x, (float)y), stk, c, hit0, t0));
+        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG>(A, primary_dir(A, (float)x, (float)y), stk, c, hit0, t0));
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples
         const int g = A.spp_grid;
         v3 acc = mk(0.0f, 0.0f, 0.0f);
@@ -374,7 +412,7 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, int x, int k, int* 
                 const float fy = (float)y + ((float)sj + 0.5f) / (float)g;
                 int h;
                 float tt;
-                const v3 cs = clamp01(trace_path<MAXB, STRICT, COUNT>(A, primary_dir(A, fx, fy), stk, c, h, tt));
+                const v3 cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG>(A, primary_dir(A, fx, fy), stk, c, h, tt));
                 acc = add(acc, cs);
                 if (si == 0 && sj == 0) {
                     hit0 = h;
@@ -411,7 +449,7 @@ __global__ __launch_bounds__(BLOCK) void k_tiles(KArgs A) {
 // (one returning atomic per wave per tile; microarch row "dequeue"). Tiles are dealt in row-major
 // order of 8x8 blocks so that concurrently running waves trace neighbouring pixels (shared L1/L2
 // lines for the upper BVH levels).
-template <int MAXB, bool STRICT, bool COUNT>
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true>
 __global__ __launch_bounds__(BLOCK) void k_persist(KArgs A) {
     __shared__ int lds[STACK * BLOCK];
     int* stk = lds + threadIdx.x;
@@ -424,7 +462,7 @@ __global__ __launch_bounds__(BLOCK) void k_persist(KArgs A) {
         if (tile >= (unsigned)A.n_tiles) break;
         const int tx = (int)(tile % (unsigned)A.tiles_x), ty = (int)(tile / (unsigned)A.tiles_x);
         const int x = tx * 8 + (lane & 7), k = ty * 8 + (lane >> 3);
-        if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT>(A, x, k, stk, c);
+        if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT, REG>(A, x, k, stk, c);
     }
     flush<COUNT>(c, A.counters);
 }

@@ -1,4 +1,4 @@
-// rt_wf.hpp — the wavefront pipeline (RT_KERNEL_FAST): the per-pixel recursion split into stages that
+// rt_wf.hpp — the wavefront pipeline (RT_KERNEL_WAVEFRONT): the per-pixel recursion split into stages that
 // communicate through dense ray queues in HBM, so the traversal kernels stay lean.
 //
 // Why: one fused per-pixel kernel keeps the whole path state alive across every traversal (~150

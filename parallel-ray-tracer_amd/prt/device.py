@@ -12,7 +12,7 @@ from ._lib import BvhNode, Camera, Frame, Light, Opts, SceneDesc, Stats, Triangl
 
 P = ctypes.POINTER
 
-KERNELS = {"auto": 0, "strict": 1, "fast": 2, "path": 3, "wave": 4}
+KERNELS = {"auto": 0, "strict": 1, "fast": 2, "wavefront": 3, "wave": 4}
 ACCEL = {"auto": 0, "reference": 1}
 FLAG_COUNTERS = 1
 

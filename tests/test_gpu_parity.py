@@ -16,6 +16,8 @@ from prt import host
 
 pytestmark = pytest.mark.gpu
 RGB_TOL = 1e-5
+# every kernel the C-ABI exposes: STRICT, FAST (production), and the A/B variants WAVEFRONT and WAVE
+KERNELS = ["strict", "fast", "wavefront", "wave"]
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 G = json.load(open(os.path.join(GOLD, "golden.json")))
 
@@ -56,7 +58,7 @@ def same_bits(a, b):
     return np.array_equal(np.asarray(a, np.float32).view(np.int32), np.asarray(b, np.float32).view(np.int32))
 
 
-@pytest.mark.parametrize("kernel", ["strict", "fast"])
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("scene", ["car_boxed", "car_only"])
 @pytest.mark.parametrize("W,H", [(64, 36), (160, 90)])
 def test_small_frames_vs_reference_fixture(dev, scenes, kernel, scene, W, H):
@@ -67,7 +69,7 @@ def test_small_frames_vs_reference_fixture(dev, scenes, kernel, scene, W, H):
     assert same_bits(out["rgb"], ref["rgb"]), np.abs(out["rgb"] - ref["rgb"]).max()
 
 
-@pytest.mark.parametrize("kernel", ["strict", "fast"])
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("scene", ["car_boxed", "car_only"])
 def test_1080p_vs_reference_sample(dev, scenes, kernel, scene):
     out = render(dev, scenes[scene], 1920, 1080, kernel, counters=True)
@@ -86,12 +88,27 @@ def test_1080p_vs_reference_sample(dev, scenes, kernel, scene):
     assert st["pixels"] == 1920 * 1080
 
 
-def test_row_subset_equals_full_frame(dev, scenes):
-    full = render(dev, scenes["car_boxed"], 320, 180, "fast")
-    part = render(dev, scenes["car_boxed"], 320, 180, "fast", rows=(5, 8, 22))
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_row_subset_equals_full_frame(dev, scenes, kernel):
+    full = render(dev, scenes["car_boxed"], 320, 180, kernel)
+    part = render(dev, scenes["car_boxed"], 320, 180, kernel, rows=(5, 8, 22))
     rows = [5 + 8 * k for k in range(22)]
     assert same_bits(part["rgb"], full["rgb"][rows])
     np.testing.assert_array_equal(part["hit"], full["hit"][rows])
+
+
+def test_ragged_and_tiny_frames(dev, scenes):
+    """frames that are not multiples of the 8x8 tile, down to one pixel, against the oracle"""
+    from tests.oracle_bind import OracleScene
+    from tests.scenes import scene_paths
+    o = OracleScene.load(*scene_paths("car_only"))
+    o.build_bvh(3)
+    for W, H in ((1, 1), (7, 3), (13, 9), (65, 17)):
+        ref = o.render(W, H)
+        for k in KERNELS:
+            out = render(dev, scenes["car_only"], W, H, k)
+            np.testing.assert_array_equal(out["hit"], ref["hit"], err_msg=f"{k} {W}x{H}")
+            assert same_bits(out["rgb"], ref["rgb"]), (k, W, H)
 
 
 def test_fast_kernel_traversing_a_sah_bvh_only(dev):
@@ -107,7 +124,7 @@ def test_fast_kernel_traversing_a_sah_bvh_only(dev):
 def test_random_mode(dev):
     s = host.Scene.random(10000).build_bvh(3)
     ref = np.load(os.path.join(GOLD, "random10k_160x90_strict.npz"))
-    for k in ("strict", "fast"):
+    for k in KERNELS:
         out = render(dev, s, 160, 90, k)
         np.testing.assert_array_equal(out["hit"], ref["hit"])
         assert same_bits(out["rgb"], ref["rgb"])
@@ -119,14 +136,15 @@ def test_oracle_counts_and_bounces(dev, scenes):
     from tests.scenes import scene_paths
     o = OracleScene.load(*scene_paths("car_boxed"))
     o.build_bvh(3)
-    for b in (1, 2, 4, 6):
+    for b in (1, 2, 4, 6, 8):
         o.set_bounces(b)
         ref = o.render(128, 72)
-        out = render(dev, scenes["car_boxed"], 128, 72, "fast", bounces=b, counters=True)
-        assert same_bits(out["rgb"], ref["rgb"]), b
-        c, st = ref["counters"], out["stats"]
-        for k in ("primary", "reflection", "shadow", "shadow_skipped", "hits"):
-            assert st[k] == c[k], (b, k)
+        for kern in KERNELS:
+            out = render(dev, scenes["car_boxed"], 128, 72, kern, bounces=b, counters=True)
+            assert same_bits(out["rgb"], ref["rgb"]), (b, kern)
+            c, st = ref["counters"], out["stats"]
+            for k in ("primary", "reflection", "shadow", "shadow_skipped", "hits"):
+                assert st[k] == c[k], (b, kern, k)
 
 
 def test_strict_traversal_counters_match_reference_order(dev, scenes):
@@ -160,7 +178,7 @@ def test_standin_scenes_vs_reference_fixture(dev, name):
     import hashlib
     s = host.Scene.named(name).build_bvh(3)
     ref = np.load(os.path.join(GOLD, f"{name}_96x54_strict.npz"))
-    for k in ("strict", "fast"):
+    for k in KERNELS:
         out = render(dev, s, 96, 54, k)
         np.testing.assert_array_equal(out["hit"], ref["hit"], err_msg=k)
         assert same_bits(out["t"], ref["t"]), k

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B timing of kernel variants in ONE process (interleaved rounds, §5.4 rule 24 of the HIP guide).
 usage: python tools/ab.py [--scene dragon] [--W 1920 --H 1080] [--rounds 5] [--frames 5] variant...
-variant = "<kernel>[:ENV=VAL,ENV=VAL]", e.g. fast fast:PRT_REFILL_BELOW=16 path strict
+variant = "<kernel>[:ENV=VAL,ENV=VAL]", e.g. fast wavefront wavefront:PRT_REFILL_BELOW=16 strict
 Prints median/min kernel ms per variant and Mrays/s (rays from the kernel counters)."""
 import argparse
 import json

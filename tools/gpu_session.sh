@@ -26,12 +26,15 @@ for s in "${@:-smoke pytest bench}"; do
       bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
       benchq) run bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
       prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
-      ab)     run ab 600 python tools/ab.py --rounds 4 --frames 5 path fast fast:PRT_REFILL_BELOW=16 fast:PRT_REFILL_BELOW=32 fast:PRT_REFILL_BELOW=56 fast:PRT_REFILL_BELOW=0 ;;
-      abcar)  run abcar 600 python tools/ab.py --scene car_boxed --rounds 3 --frames 5 path fast ;;
-      profwf) run profwf 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profwf -o run --output-format csv -- python3 tools/ab.py --rounds 1 --frames 3 fast ;;
-      abwf)   run abwf 600 python tools/ab.py --rounds 3 --frames 3 path fast fast:PRT_WF_CHUNK_MAX=64 fast:PRT_WF_CHUNK_MAX=128 fast:PRT_WF_BPC=2 fast:PRT_WF_BPC=4 fast:PRT_WF_BPC=4,PRT_WF_CHUNK_MAX=64 fast:PRT_REFILL_BELOW=32,PRT_WF_CHUNK_MAX=64 ;;
-      ctrs)   run ctrs 600 python tools/counters.py dragon path fast strict ;;
-      pmcwf)  run pmcwf 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES -d gpurun_out/pmcwf -o run --output-format csv -- python3 tools/ab.py --rounds 1 --frames 2 fast path ;;
+      ab)     run ab 600 python tools/ab.py --rounds 4 --frames 5 fast wavefront wavefront:PRT_REFILL_BELOW=16 wavefront:PRT_REFILL_BELOW=32 wavefront:PRT_REFILL_BELOW=56 wavefront:PRT_REFILL_BELOW=0 ;;
+      abcar)  run abcar 600 python tools/ab.py --scene car_boxed --rounds 3 --frames 5 fast wavefront ;;
+      profwf) run profwf 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profwf -o run --output-format csv -- python3 tools/ab.py --rounds 1 --frames 3 wavefront ;;
+      abwf)   run abwf 600 python tools/ab.py --rounds 3 --frames 3 fast wavefront wavefront:PRT_WF_CHUNK_MAX=64 wavefront:PRT_WF_CHUNK_MAX=128 wavefront:PRT_WF_BPC=2 wavefront:PRT_WF_BPC=4 wavefront:PRT_WF_BPC=4,PRT_WF_CHUNK_MAX=64 wavefront:PRT_REFILL_BELOW=32,PRT_WF_CHUNK_MAX=64 ;;
+      ctrs)   run ctrs 600 python tools/counters.py dragon fast wavefront strict ;;
+      pmcwf)  run pmcwf 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES -d gpurun_out/pmcwf -o run --output-format csv -- python3 tools/ab.py --rounds 1  --frames 2 wavefront fast ;;
+      pmcl2)  run pmcl2 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum -d gpurun_out/pmcl2 -o run --output-format csv -- python3 tools/ab.py --rounds 1  --frames 2 wavefront fast ;;
+      pmcfetch) run pmcfetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcfetch -o run --output-format csv -- python3 tools/ab.py --rounds 1  --frames 2 wavefront fast ;;
+      pmclat) run pmclat 600 rocprofv3 --pmc TCP_TCC_READ_REQ_LATENCY_sum TCP_TCR_TCP_STALL_CYCLES_sum -d gpurun_out/pmclat -o run --output-format csv -- python3 tools/ab.py --rounds 1  --frames 2 wavefront fast ;;
       *) echo "unknown step $step"; exit 2 ;;
     esac
   done
