@@ -23,9 +23,11 @@ host: $(LIB)/librt_host.so
 hip: $(LIB)/librt_hip.so
 cli: $(BIN)/raytracer
 
-$(LIB)/librt_host.so: $(CSRC)/host/rt_host.cpp include/rt_host.h include/rt_types.h
+HOST_SRCS := $(CSRC)/host/rt_host.cpp $(CSRC)/host/rt_wide.cpp
+
+$(LIB)/librt_host.so: $(HOST_SRCS) include/rt_host.h include/rt_types.h
 	@mkdir -p $(LIB)
-	g++ $(HOST_FLAGS) -shared -o $@ $(CSRC)/host/rt_host.cpp
+	g++ $(HOST_FLAGS) -shared -o $@ $(HOST_SRCS)
 
 HIP_SRCS := $(CSRC)/hip/rt_hip.hip
 HIP_HDRS := $(wildcard $(CSRC)/hip/*.hpp) include/rt_hip.h include/rt_types.h

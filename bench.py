@@ -31,13 +31,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 def alg_bytes(st, pixels, n_lights):
     """Algorithmic bytes of one launch from the kernel's traversal counters:
-    64 B per interior visit (child-pair node), 8 B per leaf visit (leaf table), 48 B per triangle
+    BVH records read (node_bytes, counted on the device: 80 B per wide-node visit of the fast walk,
+    64 B per child-pair node + 8 B per leaf record of the strict fallback walk), 48 B per triangle
     test (v0, e1, e2, n), per closest hit 4 + 32 + 48 B (tri_orig, normals + material id, material),
-    32 B per light per hit, 20 B per pixel written (rgb + hit + t)."""
-    inner = st["ch_inner"] + st["sh_inner"]
-    leaf = st["ch_leaf"] + st["sh_leaf"]
+    32 B per light per hit, 12 B per pixel written (rgb)."""
     tri = st["ch_tri"] + st["sh_tri"]
-    return 64 * inner + 8 * leaf + 48 * tri + (84 + 32 * n_lights) * st["hits"] + 12 * pixels
+    nodes = st.get("node_bytes") or (64 * (st["ch_inner"] + st["sh_inner"]) + 8 * (st["ch_leaf"] + st["sh_leaf"]))
+    return nodes + 48 * tri + (84 + 32 * n_lights) * st["hits"] + 12 * pixels
 
 
 def cpu_baseline(scene_files, W, H, gpu_rays_for_rows, args):

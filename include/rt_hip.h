@@ -97,7 +97,8 @@ typedef struct rt_stats {
     unsigned long long pixels;         /* pixels written                                    */
     unsigned long long fallbacks;      /* fast-kernel rays re-walked strictly (zero direction component or exact tie) */
     unsigned long long stack_overflows; /* must be 0 (rt_get_stats fails otherwise)          */
-    unsigned long long reserved[2];
+    unsigned long long node_bytes;     /* BVH node / leaf record bytes read (RT_FLAG_COUNTERS; fused kernels) */
+    unsigned long long reserved[1];
 } rt_stats;
 
 int rt_device_count(void);

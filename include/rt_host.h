@@ -55,6 +55,18 @@ typedef struct rth_bvh_stats {
 int rth_bvh_build(const rt_triangle* tris, size_t n, int heuristic, rth_rng* g, rt_bvh_node** nodes,
                   int* bvh_len, int** tri_idx, rth_bvh_stats* stats);
 
+/* ---- 8-wide quantised BVH: the fast walk's device layout (rt_device.hpp DWide), built
+ * from any reference-layout binary BVH (bvh + tri_idx as rth_bvh_build returns them). Interior nodes
+ * hold up to 8 children; child boxes are grown by `inflate` and quantised outward to 8 bits per
+ * plane; leaves hold <= 4 triangles. Replaces no reference function: it is the acceleration structure
+ * behind RT_ACCEL_AUTO. nodes: 20 x uint32 per node, root = node 0; tri_order: wide-leaf position
+ * -> triangle index (a permutation of 0..n_tris-1). Buffers are released with rth_free(). */
+typedef struct rth_wbvh_info {
+    int n_nodes, n_tris, depth, max_children;
+} rth_wbvh_info;
+int rth_wbvh_build(const rt_bvh_node* bvh, int n_nodes, const int* tri_idx, const rt_triangle* tris, int n_tris,
+                   float inflate, uint32_t** nodes, int** tri_order, rth_wbvh_info* info);
+
 /* ---- camera: cam_init + cam.rot.x + cam_calculate_screen_coords + inc_x/inc_y
  * (cpu/src/cam.c:5-48, main.c:105-106, main.c:243-250) for a width x height frame:
  * pos (0,-9,3), fov pi/3.2, rot.x = -pi/12. */

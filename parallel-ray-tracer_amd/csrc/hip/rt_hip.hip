@@ -50,6 +50,10 @@ struct rt_ctx {
     std::string err;
     // device scene
     DevView ref, acc;  // acc.nodes == nullptr: acc aliases ref
+    // 8-wide quantised view of acc (rt_wide.cpp); wide_nodes == nullptr: none
+    float4 *wide_nodes = nullptr, *wide_tris = nullptr;
+    int* wide_orig = nullptr;
+    int wide_n = 0, wide_depth = 0;
     float4* d_shade = nullptr;
     float4* d_mats = nullptr;
     float4* d_lights = nullptr;
@@ -105,6 +109,11 @@ void free_view(DevView& v) {
 void free_scene(rt_ctx* ctx) {
     free_view(ctx->ref);
     free_view(ctx->acc);
+    for (void* p : {(void*)ctx->wide_nodes, (void*)ctx->wide_tris, (void*)ctx->wide_orig})
+        if (p) (void)hipFree(p);
+    ctx->wide_nodes = ctx->wide_tris = nullptr;
+    ctx->wide_orig = nullptr;
+    ctx->wide_n = ctx->wide_depth = 0;
     for (void* p : {(void*)ctx->d_shade, (void*)ctx->d_mats, (void*)ctx->d_lights})
         if (p) (void)hipFree(p);
     ctx->d_shade = nullptr;
@@ -126,6 +135,23 @@ inline float i2f(int i) {
     float f;
     std::memcpy(&f, &i, 4);
     return f;
+}
+
+// leaf-ordered triangle planes: v0, e1, e2, n = e1 x e2 (raytracer.c:36-38, same roundings)
+void tri_records(const rt_triangle* T, const int* order, int n, std::vector<float4>& tris, std::vector<int>& orig) {
+    tris.resize(3 * (size_t)n);
+    orig.resize(n);
+    for (int i = 0; i < n; i++) {
+        const rt_triangle& t = T[order[i]];
+        orig[i] = order[i];
+        const rt_vec3 &a = t.coords[0], &b = t.coords[1], &c = t.coords[2];
+        const float e1x = b.x - a.x, e1y = b.y - a.y, e1z = b.z - a.z;
+        const float e2x = c.x - a.x, e2y = c.y - a.y, e2z = c.z - a.z;
+        const float nx = e1y * e2z - e1z * e2y, ny = e1z * e2x - e1x * e2z, nz = e1x * e2y - e1y * e2x;
+        tris[3 * i + 0] = make_float4(a.x, a.y, a.z, e1x);
+        tris[3 * i + 1] = make_float4(e1y, e1z, e2x, e2y);
+        tris[3 * i + 2] = make_float4(e2z, nx, ny, nz);
+    }
 }
 
 // Reference-layout BVH (bvh_t[], tri_idx) -> device view. `inflate` > 0 grows every child box by that
@@ -183,20 +209,7 @@ int build_view(rt_ctx* ctx, const rt_bvh_node* B, int nn, const int* tri_idx, co
         v.nodes[4 * r + 2] = make_float4(R.min.z, R.max.x, R.max.y, R.max.z);
         v.nodes[4 * r + 3] = make_float4(i2f(ref[p.child]), i2f(ref[p.child + 1]), 0.0f, 0.0f);
     }
-    // leaf-ordered triangle planes: v0, e1, e2, n = e1 x e2 (raytracer.c:36-38, same roundings)
-    v.tris.resize(3 * (size_t)n);
-    v.orig.resize(n);
-    for (int i = 0; i < n; i++) {
-        const rt_triangle& t = T[tri_idx[i]];
-        v.orig[i] = tri_idx[i];
-        const rt_vec3 &a = t.coords[0], &b = t.coords[1], &c = t.coords[2];
-        const float e1x = b.x - a.x, e1y = b.y - a.y, e1z = b.z - a.z;
-        const float e2x = c.x - a.x, e2y = c.y - a.y, e2z = c.z - a.z;
-        const float nx = e1y * e2z - e1z * e2y, ny = e1z * e2x - e1x * e2z, nz = e1x * e2y - e1y * e2x;
-        v.tris[3 * i + 0] = make_float4(a.x, a.y, a.z, e1x);
-        v.tris[3 * i + 1] = make_float4(e1y, e1z, e2x, e2y);
-        v.tris[3 * i + 2] = make_float4(e2z, nx, ny, nz);
-    }
+    tri_records(T, tri_idx, n, v.tris, v.orig);
     return RT_OK;
 }
 
@@ -268,6 +281,9 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     HIPC(hipSetDevice(ctx->device));
     const int n = sc->n_triangles;
     HostView hr, ha;
+    std::vector<float4> wide_nodes, wide_tris;
+    std::vector<int> wide_orig;
+    int wide_depth = 0;
     int rc = build_view(ctx, sc->bvh, sc->n_nodes, sc->tri_idx, sc->triangles, n, 0.0f, hr);
     if (rc) return rc;
     const bool own_acc = sc->accel == RT_ACCEL_AUTO;
@@ -283,7 +299,21 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
         for (int i = 0; i < n; i++)
             for (const rt_vec3& c : sc->triangles[i].coords)
                 mx = std::max(mx, std::max(std::fabs(c.x), std::max(std::fabs(c.y), std::fabs(c.z))));
-        rc = build_view(ctx, nodes, nlen, idx, sc->triangles, n, std::ldexp(mx, -18), ha);
+        const float inflate = std::ldexp(mx, -18);
+        rc = build_view(ctx, nodes, nlen, idx, sc->triangles, n, inflate, ha);
+        // ... and its 8-wide quantised form (same inflation, planes rounded outward)
+        uint32_t* words = nullptr;
+        int* order = nullptr;
+        rth_wbvh_info wi{};
+        if (!rc && rth_wbvh_build(nodes, nlen, idx, sc->triangles, n, inflate, &words, &order, &wi) == RT_OK &&
+            wi.depth <= rtd::WSTACK) {
+            wide_nodes.resize(5 * (size_t)wi.n_nodes);
+            std::memcpy(wide_nodes.data(), words, sizeof(uint32_t) * 20 * (size_t)wi.n_nodes);
+            tri_records(sc->triangles, order, n, wide_tris, wide_orig);
+            wide_depth = wi.depth;
+        }
+        rth_free(words);
+        rth_free(order);
         rth_free(nodes);
         rth_free(idx);
         if (rc) return rc;
@@ -318,10 +348,15 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     free_scene(ctx);
     if ((rc = upload_view(ctx, hr, ctx->ref)) || (own_acc && (rc = upload_view(ctx, ha, ctx->acc))) ||
         (rc = upload(ctx, &ctx->d_shade, shade)) || (rc = upload(ctx, &ctx->d_mats, mats)) ||
-        (rc = upload(ctx, &ctx->d_lights, lights))) {
+        (rc = upload(ctx, &ctx->d_lights, lights)) ||
+        (!wide_nodes.empty() && ((rc = upload(ctx, &ctx->wide_nodes, wide_nodes)) ||
+                                 (rc = upload(ctx, &ctx->wide_tris, wide_tris)) ||
+                                 (rc = upload(ctx, &ctx->wide_orig, wide_orig))))) {
         free_scene(ctx);
         return rc;
     }
+    ctx->wide_n = (int)(wide_nodes.size() / 5);
+    ctx->wide_depth = wide_depth;
     ctx->n_lights = sc->n_lights;
     ctx->n_tris = n;
     ctx->amb[0] = sc->amb.x;
@@ -518,6 +553,8 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     std::memset(&A, 0, sizeof A);
     A.s.ref = dview(ctx->ref);
     A.s.acc = ctx->acc.nodes ? dview(ctx->acc) : A.s.ref;
+    A.s.wide = rtd::DWide{ctx->wide_nodes, ctx->wide_tris, ctx->wide_orig};
+    if (const char* e = std::getenv("PRT_WIDE"); e && std::atoi(e) == 0) A.s.wide.nodes = nullptr;  // A/B knob
     A.s.shade = ctx->d_shade;
     A.s.mats = ctx->d_mats;
     A.s.lights = ctx->d_lights;
@@ -644,6 +681,7 @@ extern "C" int rt_get_stats(rt_ctx* ctx, rt_stats* st) {
     st->pixels = c[rtd::C_PIX];
     st->fallbacks = c[rtd::C_FALLBACK];
     st->stack_overflows = c[rtd::C_ERR];
+    st->node_bytes = 8 * c[rtd::C_NB];
     if (c[rtd::C_ERR]) {
         ctx->err = "traversal stack overflow: BVH deeper than 32 levels";
         return RT_E_STATE;

@@ -33,11 +33,12 @@ constexpr int BLOCK = 256;
 constexpr int STACK = 34;  // max stack = max depth (32, bvh.c:84) + 2
 enum {
     C_PRIM, C_REFL, C_SHAD, C_SKIP, C_HITS, C_CHI, C_CHL, C_CHT, C_SHI, C_SHL, C_SHT, C_PIX, C_ERR, C_FALLBACK,
+    C_NB,  // node/leaf record bytes read, in 8-B units (RT_FLAG_COUNTERS)
     NCOUNT = 16
 };
 
 struct Ctr {
-    unsigned prim, refl, shad, skip, hits, chi, chl, cht, shi, shl, sht, pix, err, fb;
+    unsigned prim, refl, shad, skip, hits, chi, chl, cht, shi, shl, sht, pix, err, fb, nb;
 };
 
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
@@ -50,10 +51,10 @@ template <bool COUNT>
 __device__ __forceinline__ void flush(const Ctr& c, unsigned long long* g) {
     const bool l0 = (threadIdx.x & 63) == 0;
     unsigned v[NCOUNT] = {c.prim, c.refl, c.shad, c.skip, c.hits, c.chi, c.chl, c.cht,
-                          c.shi, c.shl, c.sht, c.pix, c.err, c.fb, 0, 0};
+                          c.shi, c.shl, c.sht, c.pix, c.err, c.fb, c.nb, 0};
 #pragma unroll
-    for (int i = 0; i < 14; i++) {
-        if (!COUNT && i >= C_CHI && i <= C_SHT) continue;
+    for (int i = 0; i < 15; i++) {
+        if (!COUNT && ((i >= C_CHI && i <= C_SHT) || i == C_NB)) continue;
         unsigned s = wave_sum(v[i]);
         if (l0 && s) atomicAdd(g + i, (unsigned long long)s);
     }
@@ -125,7 +126,10 @@ __device__ __forceinline__ void closest_walk(const DBvh& B, v3 o, v3 d, float& b
         }
         if (cur < 0) {
             const int2 lf = B.leaves[~cur];
-            if (COUNT) c.chl++;
+            if (COUNT) {
+                c.chl++;
+                c.nb += 1;
+            }
             for (int i = lf.x; i < lf.x + lf.y; ++i) {
                 int k;
                 const float tt = hit_triangle(o, d, B.tris + 3 * i, k);
@@ -140,7 +144,10 @@ __device__ __forceinline__ void closest_walk(const DBvh& B, v3 o, v3 d, float& b
                 }
             }
         } else {
-            if (COUNT) c.chi++;
+            if (COUNT) {
+                c.chi++;
+                c.nb += 8;
+            }
             int ni, fi;
             float nt, ft;
             children<STRICT>(B, cur, o, d, p, ni, nt, fi, ft);
@@ -191,7 +198,10 @@ __device__ __forceinline__ bool visible_walk(const DBvh& B, v3 o, v3 d, float ld
         }
         if (cur < 0) {
             const int2 lf = B.leaves[~cur];
-            if (COUNT) c.shl++;
+            if (COUNT) {
+                c.shl++;
+                c.nb += 1;
+            }
             for (int i = lf.x; i < lf.x + lf.y; ++i) {
                 int k;
                 const float tt = hit_triangle(o, d, B.tris + 3 * i, k);
@@ -204,7 +214,10 @@ __device__ __forceinline__ bool visible_walk(const DBvh& B, v3 o, v3 d, float ld
                 }
             }
         } else {
-            if (COUNT) c.shi++;
+            if (COUNT) {
+                c.shi++;
+                c.nb += 8;
+            }
             int ni, fi;
             float nt, ft;
             children<STRICT>(B, cur, o, d, p, ni, nt, fi, ft);
@@ -237,6 +250,171 @@ __device__ __forceinline__ bool visible_walk(const DBvh& B, v3 o, v3 d, float ld
     return true;
 }
 
+// ---------------------------------------------------------------- 8-wide quantised walk (fast)
+// Node-group traversal (after Ylitie et al., "Efficient Incoherent Ray Traversal on GPUs Through
+// Compressed Wide BVHs", HPG 2017): one visit tests all 8 child boxes, tests the triangles of every
+// hit leaf slot at once, and keeps the hit interior children as ONE stack entry (child base, imask,
+// hit bits) popped child by child in the order k ^ octant(ray) (near first, no sort).
+// Same result semantics as closest_walk<false>: min t over all triangles, boxes pruned at
+// best * PRUNE_SLACK so that exact ties are always met and reported.
+constexpr int WSTACK = 16;  // node-group entries (2 ints) in the STACK-int LDS column; builder depth <= 16
+
+__device__ __forceinline__ float ubyte(unsigned w, int b) { return (float)((w >> (8 * b)) & 0xFFu); }
+
+// Tests the 8 children of wide node `node`: nh = hit interior slots as bits (s ^ oct), th = triangle
+// bits (relative to tbase) of every hit leaf slot.
+template <bool COUNT>
+__device__ __forceinline__ void wide_node(const DWide& W, int node, const RayPre& p, unsigned oct, float lim,
+                                          unsigned& nh, unsigned& th, int& cbase, int& tbase, unsigned& imask,
+                                          unsigned& nleaf) {
+    const float4* N = W.nodes + 5 * node;
+    const float4 f0 = N[0], f1 = N[1], f2 = N[2], f3 = N[3], f4 = N[4];
+    const unsigned e = __float_as_uint(f0.w);
+    const float sx = __uint_as_float((e & 0xFFu) << 23), sy = __uint_as_float(((e >> 8) & 0xFFu) << 23),
+                sz = __uint_as_float(((e >> 16) & 0xFFu) << 23);
+    imask = e >> 24;
+    cbase = __float_as_int(f1.x);
+    tbase = __float_as_int(f1.y);
+    const unsigned m[2] = {__float_as_uint(f1.z), __float_as_uint(f1.w)};
+    // near / far plane bytes per axis from the direction signs (== min / max of the two slab ends)
+    const bool bx = (oct & 1u) != 0, by = (oct & 2u) != 0, bz = (oct & 4u) != 0;
+    const unsigned lx[2] = {__float_as_uint(f2.x), __float_as_uint(f2.y)}, ly[2] = {__float_as_uint(f2.z), __float_as_uint(f2.w)},
+                   lz[2] = {__float_as_uint(f3.x), __float_as_uint(f3.y)}, hx[2] = {__float_as_uint(f3.z), __float_as_uint(f3.w)},
+                   hy[2] = {__float_as_uint(f4.x), __float_as_uint(f4.y)}, hz[2] = {__float_as_uint(f4.z), __float_as_uint(f4.w)};
+    nh = 0;
+    th = 0;
+    nleaf = 0;
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+        const int h = s >> 2, b = s & 3;
+        const float nxp = __builtin_fmaf(sx, ubyte(bx ? hx[h] : lx[h], b), f0.x);
+        const float fxp = __builtin_fmaf(sx, ubyte(bx ? lx[h] : hx[h], b), f0.x);
+        const float nyp = __builtin_fmaf(sy, ubyte(by ? hy[h] : ly[h], b), f0.y);
+        const float fyp = __builtin_fmaf(sy, ubyte(by ? ly[h] : hy[h], b), f0.y);
+        const float nzp = __builtin_fmaf(sz, ubyte(bz ? hz[h] : lz[h], b), f0.z);
+        const float fzp = __builtin_fmaf(sz, ubyte(bz ? lz[h] : hz[h], b), f0.z);
+        const float tmin = fmaxf(fmaxf(__builtin_fmaf(nxp, p.ix, -p.ox), __builtin_fmaf(nyp, p.iy, -p.oy)),
+                                 __builtin_fmaf(nzp, p.iz, -p.oz));
+        const float tmax = fminf(fminf(__builtin_fmaf(fxp, p.ix, -p.ox), __builtin_fmaf(fyp, p.iy, -p.oy)),
+                                 __builtin_fmaf(fzp, p.iz, -p.oz)) * 1.00000024f;
+        const bool hit = tmax >= tmin && tmax > 0.0f && tmin <= lim;
+        const unsigned meta = (m[h] >> (8 * b)) & 0xFFu;
+        if (hit) {
+            if ((imask >> s) & 1u) {
+                nh |= 1u << (s ^ oct);
+            } else if (meta) {
+                th |= ((1u << (meta >> 5)) - 1u) << (meta & 31u);
+                nleaf++;
+            }
+        }
+    }
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& best, int& hp, int& nd, bool& tie,
+                                             int* __restrict__ stk, Ctr& c) {
+    const RayPre p = ray_pre(o, d);
+    const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
+    int node = 0, sp = 0;
+    for (;;) {
+        unsigned nh, th, imask, nl;
+        int cb, tb;
+        wide_node<COUNT>(W, node, p, oct, best * PRUNE_SLACK, nh, th, cb, tb, imask, nl);
+        if (COUNT) {
+            c.chi++;
+            c.chl += nl;
+            c.nb += 10;
+        }
+        while (th) {
+            const int i = tb + __builtin_ctz(th);
+            th &= th - 1u;
+            int k;
+            const float tt = hit_triangle(o, d, W.tris + 3 * i, k);
+            if (COUNT) c.cht++;
+            if (tt < best) {
+                best = tt;
+                nd = k;
+                hp = i;
+                tie = false;
+            } else if (tt == best && tt != FMAX) {
+                tie = true;
+            }
+        }
+        if (!nh) {
+            if (sp == 0) break;
+            --sp;
+            cb = stk[(2 * sp) * BLOCK];
+            const unsigned bits = (unsigned)stk[(2 * sp + 1) * BLOCK];
+            imask = bits >> 8;
+            nh = bits & 0xFFu;
+        }
+        const unsigned slot = (unsigned)__builtin_ctz(nh) ^ oct;
+        nh &= nh - 1u;
+        if (nh) {
+            if (sp >= WSTACK) {  // deeper than the builder allows: reported, never silent
+                c.err++;
+                break;
+            }
+            stk[(2 * sp) * BLOCK] = cb;
+            stk[(2 * sp + 1) * BLOCK] = (int)((imask << 8) | nh);
+            ++sp;
+        }
+        node = cb + __popc(imask & ((1u << slot) - 1u));
+    }
+}
+
+template <bool COUNT>
+__device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c) {
+    const RayPre p = ray_pre(o, d);
+    const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
+    float best = FMAX;
+    int node = 0, sp = 0;
+    for (;;) {
+        unsigned nh, th, imask, nl;
+        int cb, tb;
+        wide_node<COUNT>(W, node, p, oct, best * PRUNE_SLACK, nh, th, cb, tb, imask, nl);
+        if (COUNT) {
+            c.shi++;
+            c.shl += nl;
+            c.nb += 10;
+        }
+        while (th) {
+            const int i = tb + __builtin_ctz(th);
+            th &= th - 1u;
+            int k;
+            const float tt = hit_triangle(o, d, W.tris + 3 * i, k);
+            if (COUNT) c.sht++;
+            if (tt < best) {
+                best = tt;
+                const v3 ip = add(o, mul(d, best));
+                const v3 oi = sub(o, ip);
+                if (ld2 > dot(oi, oi)) return false;
+            }
+        }
+        if (!nh) {
+            if (sp == 0) break;
+            --sp;
+            cb = stk[(2 * sp) * BLOCK];
+            const unsigned bits = (unsigned)stk[(2 * sp + 1) * BLOCK];
+            imask = bits >> 8;
+            nh = bits & 0xFFu;
+        }
+        const unsigned slot = (unsigned)__builtin_ctz(nh) ^ oct;
+        nh &= nh - 1u;
+        if (nh) {
+            if (sp >= WSTACK) {
+                c.err++;
+                break;
+            }
+            stk[(2 * sp) * BLOCK] = cb;
+            stk[(2 * sp + 1) * BLOCK] = (int)((imask << 8) | nh);
+            ++sp;
+        }
+        node = cb + __popc(imask & ((1u << slot) - 1u));
+    }
+    return true;
+}
+
 // Closest hit with the kernel's policy; returns the ORIGINAL triangle index (-1 = miss).
 template <bool STRICT, bool COUNT, bool REG = true>
 __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best, int& nd, int* __restrict__ stk,
@@ -246,8 +424,13 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
     best = FMAX;
     nd = 0;
     if (!STRICT && !degenerate(d)) {
-        closest_walk<false, COUNT, REG>(s.acc, o, d, best, hp, nd, tie, stk, c);
-        if (!tie) return hp >= 0 ? s.acc.tri_orig[hp] : -1;
+        if (s.wide.nodes) {
+            closest_wide<COUNT>(s.wide, o, d, best, hp, nd, tie, stk, c);
+            if (!tie) return hp >= 0 ? s.wide.tri_orig[hp] : -1;
+        } else {
+            closest_walk<false, COUNT, REG>(s.acc, o, d, best, hp, nd, tie, stk, c);
+            if (!tie) return hp >= 0 ? s.acc.tri_orig[hp] : -1;
+        }
         c.fb++;
         hp = -1;
         best = FMAX;
@@ -261,7 +444,10 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
 
 template <bool STRICT, bool COUNT, bool REG = true>
 __device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c) {
-    if (!STRICT && !degenerate(d)) return visible_walk<false, COUNT, REG>(s.acc, o, d, ld2, stk, c);
+    if (!STRICT && !degenerate(d)) {
+        if (s.wide.nodes) return visible_wide<COUNT>(s.wide, o, d, ld2, stk, c);
+        return visible_walk<false, COUNT, REG>(s.acc, o, d, ld2, stk, c);
+    }
     if (!STRICT) c.fb++;
     return visible_walk<true, COUNT, REG>(s.ref, o, d, ld2, stk, c);
 }

@@ -1,0 +1,343 @@
+// rt_wide.cpp — the fast walk's 8-wide quantised BVH (device layout: rt_device.hpp, DWide).
+//
+// Built from any reference-layout binary BVH (bvh_t[] + tri_idx, cpu/src/bvh.c:360-388), normally
+// this library's binned SAH. The binary tree is collapsed top-down: a wide node starts from the two
+// children of a binary node and repeatedly opens its largest-area interior child until it has 8
+// children (Wald et al. / Ylitie et al. style collapse). Leaves are cut to <= 4 triangles so that a
+// wide node's leaf triangles fit a 32-bit mask (8 slots x 4).
+//
+// Conservativeness: each child box is first grown by `inflate` (the same margin the binary fast walk
+// uses, >= the reciprocal-FMA slab test's rounding reach), then quantised OUTWARD to 8 bits per
+// plane on a per-node power-of-two grid. Every plane is checked with the device's own decode,
+// fmaf(scale, q, p) (scale * q is exact, so this is p + scale * q rounded once), and moved outward
+// until the decoded box contains the grown box.
+//
+// Slot order: children sit in the slot of the octant they occupy relative to the node centre
+// (bit 0 = +x, bit 1 = +y, bit 2 = +z), so that a ray visiting slots in the order k ^ octant(ray)
+// for k = 0..7 meets them roughly front to back without sorting.
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "rt_host.h"
+
+namespace {
+
+struct Box {
+    float lo[3], hi[3];
+};
+
+Box empty_box() {
+    Box b;
+    for (int a = 0; a < 3; a++) {
+        b.lo[a] = INFINITY;
+        b.hi[a] = -INFINITY;
+    }
+    return b;
+}
+
+void grow(Box& b, const Box& o) {
+    for (int a = 0; a < 3; a++) {
+        b.lo[a] = std::min(b.lo[a], o.lo[a]);
+        b.hi[a] = std::max(b.hi[a], o.hi[a]);
+    }
+}
+
+float area(const Box& b) {
+    const float dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+    return 2.0f * (dx * dy + dy * dz + dz * dx);
+}
+
+constexpr int LEAF_MAX = 4;
+constexpr int WIDTH = 8;
+
+struct BNode {
+    Box b;
+    int l = -1, r = -1;      // interior: children (BNode indices); leaf: l == -1
+    int first = 0, cnt = 0;  // leaf: range of `idx`
+};
+
+struct WBuilder {
+    const rt_triangle* T = nullptr;
+    int n = 0;
+    std::vector<int> idx;
+    std::vector<BNode> bn;
+    float inflate = 0.0f;
+
+    Box tri_box(int t) const {
+        Box b = empty_box();
+        for (const rt_vec3& c : T[t].coords) {
+            const float v[3] = {c.x, c.y, c.z};
+            for (int a = 0; a < 3; a++) {
+                b.lo[a] = std::min(b.lo[a], v[a]);
+                b.hi[a] = std::max(b.hi[a], v[a]);
+            }
+        }
+        return b;
+    }
+
+    // a leaf range, cut by object median on the widest centroid axis until <= LEAF_MAX triangles
+    int leaf(int first, int cnt) {
+        if (cnt <= LEAF_MAX) {
+            BNode x;
+            x.first = first;
+            x.cnt = cnt;
+            x.b = empty_box();
+            for (int i = first; i < first + cnt; i++) grow(x.b, tri_box(idx[i]));
+            bn.push_back(x);
+            return (int)bn.size() - 1;
+        }
+        float cl[3] = {INFINITY, INFINITY, INFINITY}, ch[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int i = first; i < first + cnt; i++)
+            for (int a = 0; a < 3; a++) {
+                cl[a] = std::min(cl[a], T[idx[i]].centroid[a]);
+                ch[a] = std::max(ch[a], T[idx[i]].centroid[a]);
+            }
+        int ax = 0;
+        for (int a = 1; a < 3; a++)
+            if (ch[a] - cl[a] > ch[ax] - cl[ax]) ax = a;
+        std::stable_sort(idx.begin() + first, idx.begin() + first + cnt,
+                         [&](int u, int v) { return T[u].centroid[ax] < T[v].centroid[ax]; });
+        const int h = cnt / 2;
+        const int l = leaf(first, h), r = leaf(first + h, cnt - h);
+        return inner(l, r);
+    }
+
+    int inner(int l, int r) {
+        BNode x;
+        x.l = l;
+        x.r = r;
+        x.b = bn[l].b;
+        grow(x.b, bn[r].b);
+        bn.push_back(x);
+        return (int)bn.size() - 1;
+    }
+
+    // reference-layout node i -> BNode index (-1: empty subtree)
+    int make(const rt_bvh_node* B, int nn, int i, int depth, bool& bad) {
+        if (i < 0 || i >= nn || depth > 64) {
+            bad = true;
+            return -1;
+        }
+        const rt_bvh_node& p = B[i];
+        if (p.tr_len > 0) {
+            if (p.child < 0 || (long long)p.child + p.tr_len > n) {
+                bad = true;
+                return -1;
+            }
+            return leaf(p.child, p.tr_len);
+        }
+        if (p.child == 0) return -1;
+        const int l = make(B, nn, p.child, depth + 1, bad);
+        const int r = make(B, nn, p.child + 1, depth + 1, bad);
+        if (l < 0) return r;
+        if (r < 0) return l;
+        return inner(l, r);
+    }
+};
+
+inline float fma_decode(float scale, int q, float p) { return std::fmaf(scale, (float)q, p); }
+
+inline uint32_t f2u(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+}
+
+// Quantise one axis of up to 8 child boxes (already grown) on the grid p + 2^e * q, q in 0..255.
+// Returns the biased exponent byte (e + 127); qlo/qhi receive the planes.
+int quantise_axis(const float* lo, const float* hi, int k, float& p, int* qlo, int* qhi) {
+    p = INFINITY;
+    float top = -INFINITY;
+    for (int c = 0; c < k; c++) {
+        p = std::min(p, lo[c]);
+        top = std::max(top, hi[c]);
+    }
+    const double ext = (double)top - (double)p;
+    int e = ext > 0 ? (int)std::ceil(std::log2(ext / 255.0)) : -126;
+    e = std::max(-126, std::min(e, 120));
+    for (;; e++) {
+        const float scale = std::ldexp(1.0f, e);
+        bool ok = true;
+        for (int c = 0; c < k && ok; c++) {
+            int a = (int)std::floor(((double)lo[c] - (double)p) / scale);
+            a = std::max(0, std::min(a, 255));
+            while (a > 0 && fma_decode(scale, a, p) > lo[c]) a--;
+            int b = (int)std::ceil(((double)hi[c] - (double)p) / scale);
+            b = std::max(0, b);
+            while (b <= 255 && fma_decode(scale, b, p) < hi[c]) b++;
+            if (b > 255 || fma_decode(scale, a, p) > lo[c]) ok = false;
+            qlo[c] = a;
+            qhi[c] = b;
+        }
+        if (ok || e >= 126) return e + 127;
+    }
+}
+
+}  // namespace
+
+extern "C" int rth_wbvh_build(const rt_bvh_node* bvh, int n_nodes, const int* tri_idx, const rt_triangle* tris,
+                              int n_tris, float inflate, uint32_t** nodes_out, int** tri_order_out,
+                              rth_wbvh_info* info) {
+    if (!bvh || n_nodes <= 0 || !tri_idx || !tris || n_tris <= 0 || !nodes_out || !tri_order_out ||
+        !(inflate >= 0.0f))
+        return RT_E_ARG;
+    WBuilder w;
+    w.T = tris;
+    w.n = n_tris;
+    w.inflate = inflate;
+    w.idx.assign(tri_idx, tri_idx + n_tris);
+    for (int t : w.idx)
+        if (t < 0 || t >= n_tris) return RT_E_ARG;
+    w.bn.reserve(2 * (size_t)n_tris + 2);
+    bool bad = false;
+    const int root = w.make(bvh, n_nodes, 0, 0, bad);
+    if (bad || root < 0) return RT_E_ARG;
+
+    // breadth-first: interior children of a wide node get consecutive indices
+    struct Item {
+        int b, depth;
+    };
+    std::vector<Item> queue{{root, 1}};
+    std::vector<uint32_t> words;
+    std::vector<int> order;
+    order.reserve(n_tris);
+    int depth = 0, max_kids = 0;
+    for (size_t qi = 0; qi < queue.size(); qi++) {
+        const Item it = queue[qi];
+        depth = std::max(depth, it.depth);
+        const BNode& B = w.bn[it.b];
+        // children: open the largest-area interior child until WIDTH
+        std::vector<int> kids;
+        if (B.l < 0) {
+            kids.push_back(it.b);  // a leaf root
+        } else {
+            kids = {B.l, B.r};
+            while ((int)kids.size() < WIDTH) {
+                int best = -1;
+                float ba = -1.0f;
+                for (int c = 0; c < (int)kids.size(); c++)
+                    if (w.bn[kids[c]].l >= 0 && area(w.bn[kids[c]].b) > ba) {
+                        ba = area(w.bn[kids[c]].b);
+                        best = c;
+                    }
+                if (best < 0) break;
+                const int o = kids[best];
+                kids[best] = w.bn[o].l;
+                kids.push_back(w.bn[o].r);
+            }
+        }
+        const int k = (int)kids.size();
+        max_kids = std::max(max_kids, k);
+        // octant slots: greedy on cost = -dot(centre offset, slot direction)
+        Box all = empty_box();
+        for (int c : kids) grow(all, w.bn[c].b);
+        float pc[3];
+        for (int a = 0; a < 3; a++) pc[a] = 0.5f * (all.lo[a] + all.hi[a]);
+        int kid_in[WIDTH];
+        for (int s = 0; s < WIDTH; s++) kid_in[s] = -1;
+        std::vector<char> done(k, 0);
+        for (int round = 0; round < k; round++) {
+            float bc = INFINITY;
+            int bk = -1, bs = -1;
+            for (int c = 0; c < k; c++) {
+                if (done[c]) continue;
+                const Box& cb = w.bn[kids[c]].b;
+                for (int s = 0; s < WIDTH; s++) {
+                    if (kid_in[s] >= 0) continue;
+                    float cost = 0.0f;
+                    for (int a = 0; a < 3; a++) {
+                        const float off = 0.5f * (cb.lo[a] + cb.hi[a]) - pc[a];
+                        cost -= ((s >> a) & 1) ? off : -off;
+                    }
+                    if (cost < bc) {
+                        bc = cost;
+                        bk = c;
+                        bs = s;
+                    }
+                }
+            }
+            done[bk] = 1;
+            kid_in[bs] = bk;
+        }
+        // quantise (grown boxes) per axis over the occupied slots
+        float lo[3][WIDTH], hi[3][WIDTH];
+        int qlo[3][WIDTH], qhi[3][WIDTH];
+        int ks = 0;
+        int slot_list[WIDTH];
+        for (int s = 0; s < WIDTH; s++)
+            if (kid_in[s] >= 0) {
+                const Box& cb = w.bn[kids[kid_in[s]]].b;
+                for (int a = 0; a < 3; a++) {
+                    lo[a][ks] = cb.lo[a] - inflate;
+                    hi[a][ks] = cb.hi[a] + inflate;
+                }
+                slot_list[ks++] = s;
+            }
+        float p[3];
+        int eb[3];
+        for (int a = 0; a < 3; a++) eb[a] = quantise_axis(lo[a], hi[a], ks, p[a], qlo[a], qhi[a]);
+        // node words
+        const size_t base = words.size();
+        words.resize(base + 20, 0);
+        uint32_t* W = &words[base];
+        W[0] = f2u(p[0]);
+        W[1] = f2u(p[1]);
+        W[2] = f2u(p[2]);
+        uint32_t imask = 0;
+        for (int s = 0; s < WIDTH; s++)
+            if (kid_in[s] >= 0 && w.bn[kids[kid_in[s]]].l >= 0) imask |= 1u << s;
+        W[3] = (uint32_t)eb[0] | ((uint32_t)eb[1] << 8) | ((uint32_t)eb[2] << 16) | (imask << 24);
+        const int child_base = (int)queue.size();
+        const int tri_base = (int)order.size();
+        W[4] = (uint32_t)child_base;
+        W[5] = (uint32_t)tri_base;
+        uint8_t meta[WIDTH] = {0};
+        uint8_t q8[6][WIDTH];
+        for (int s = 0; s < WIDTH; s++) {  // empty slots: an inverted box (never selected: meta 0, imask 0)
+            for (int a = 0; a < 3; a++) {
+                q8[a][s] = 255;
+                q8[3 + a][s] = 0;
+            }
+        }
+        for (int j = 0; j < ks; j++) {
+            const int s = slot_list[j];
+            for (int a = 0; a < 3; a++) {
+                q8[a][s] = (uint8_t)qlo[a][j];
+                q8[3 + a][s] = (uint8_t)qhi[a][j];
+            }
+            const BNode& c = w.bn[kids[kid_in[s]]];
+            if (c.l >= 0) {
+                queue.push_back({kids[kid_in[s]], it.depth + 1});
+            } else {
+                const int off = (int)order.size() - tri_base;
+                meta[s] = (uint8_t)((c.cnt << 5) | off);
+                for (int i = c.first; i < c.first + c.cnt; i++) order.push_back(w.idx[i]);
+            }
+        }
+        std::memcpy(&W[6], meta, 8);
+        // qlo_x qlo_y | qlo_z qhi_x | qhi_y qhi_z  (8 bytes each)
+        for (int pl = 0; pl < 6; pl++) std::memcpy(&W[8 + 2 * pl], q8[pl], 8);
+    }
+    if ((int)order.size() != n_tris) return RT_E_ARG;  // a triangle referenced twice or never
+    uint32_t* nodes = (uint32_t*)std::malloc(sizeof(uint32_t) * words.size());
+    int* ord = (int*)std::malloc(sizeof(int) * order.size());
+    if (!nodes || !ord) {
+        std::free(nodes);
+        std::free(ord);
+        return RT_E_NOMEM;
+    }
+    std::memcpy(nodes, words.data(), sizeof(uint32_t) * words.size());
+    std::memcpy(ord, order.data(), sizeof(int) * order.size());
+    *nodes_out = nodes;
+    *tri_order_out = ord;
+    if (info) {
+        info->n_nodes = (int)(words.size() / 20);
+        info->n_tris = (int)order.size();
+        info->depth = depth;
+        info->max_children = max_kids;
+    }
+    return RT_OK;
+}

@@ -9,6 +9,7 @@ import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(PKG_DIR, "lib")
+LIB_DIR = os.environ.get("PRT_LIB_DIR") or LIB_DIR  # A/B of two builds (tools/ab.py); default: in-tree
 
 
 class Vec3(ctypes.Structure):
@@ -60,11 +61,16 @@ class Frame(ctypes.Structure):
 
 
 STAT_FIELDS = ["primary", "reflection", "shadow", "shadow_skipped", "hits", "ch_inner", "ch_leaf",
-               "ch_tri", "sh_inner", "sh_leaf", "sh_tri", "pixels", "fallbacks", "stack_overflows"]
+               "ch_tri", "sh_inner", "sh_leaf", "sh_tri", "pixels", "fallbacks", "stack_overflows", "node_bytes"]
+
+
+class WbvhInfo(ctypes.Structure):
+    _fields_ = [("n_nodes", ctypes.c_int), ("n_tris", ctypes.c_int), ("depth", ctypes.c_int),
+                ("max_children", ctypes.c_int)]
 
 
 class Stats(ctypes.Structure):
-    _fields_ = [(f, ctypes.c_ulonglong) for f in STAT_FIELDS] + [("reserved", ctypes.c_ulonglong * 2)]
+    _fields_ = [(f, ctypes.c_ulonglong) for f in STAT_FIELDS] + [("reserved", ctypes.c_ulonglong * 1)]
 
 
 _host = None
@@ -90,6 +96,9 @@ def host():
         L.rth_triangles_random.argtypes = [ctypes.c_size_t, P(Rng), P(P(Triangle))]
         L.rth_bvh_build.argtypes = [P(Triangle), ctypes.c_size_t, ctypes.c_int, P(Rng), P(P(BvhNode)),
                                     P(ctypes.c_int), P(P(ctypes.c_int)), P(BvhStats)]
+        if hasattr(L, "rth_wbvh_build"):  # absent from older builds (A/B via PRT_LIB_DIR)
+            L.rth_wbvh_build.argtypes = [P(BvhNode), ctypes.c_int, P(ctypes.c_int), P(Triangle), ctypes.c_int,
+                                         ctypes.c_float, P(P(ctypes.c_uint32)), P(P(ctypes.c_int)), P(WbvhInfo)]
         L.rth_camera.argtypes = [ctypes.c_int, ctypes.c_int, P(Camera)]
         L.rth_bmp_write.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
         L.rth_bmp_encode.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]

@@ -94,6 +94,43 @@ def bvh_build(tris, heuristic=3, rng=None):
     return nodes_np, idx_np, stats
 
 
+def wbvh_build(nodes, tri_idx, tris, inflate=0.0):
+    """the fast walk's 8-wide quantised BVH (rth_wbvh_build, rt_wide.cpp) from a reference-layout BVH
+    -> (words uint32 [n_nodes, 20], tri_order int32 [n], info dict)"""
+    L = _lib.host()
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    tri_idx = np.ascontiguousarray(tri_idx, dtype=np.int32)
+    tris = np.ascontiguousarray(tris, dtype=TRI_DTYPE)
+    words = P(ctypes.c_uint32)()
+    order = P(ctypes.c_int)()
+    info = _lib.WbvhInfo()
+    _check(L.rth_wbvh_build(nodes.ctypes.data_as(P(_lib.BvhNode)), len(nodes), tri_idx.ctypes.data_as(P(ctypes.c_int)),
+                            tris.ctypes.data_as(P(Triangle)), len(tris), float(inflate), ctypes.byref(words),
+                            ctypes.byref(order), ctypes.byref(info)), "wbvh_build")
+    w = _take(words, 20 * info.n_nodes, np.dtype(np.uint32)).reshape(-1, 20)
+    o = _take(order, info.n_tris, np.dtype(np.int32))
+    return w, o, {"n_nodes": info.n_nodes, "depth": info.depth, "max_children": info.max_children}
+
+
+def wbvh_decode(words):
+    """decoded view of wide nodes: p [N,3] f32, scale [N,3] f32, imask [N], child_base [N], tri_base [N],
+    meta [N,8] u8, qlo/qhi [N,3,8] u8 and the decoded child boxes lo/hi [N,8,3] (fmaf(scale, q, p))"""
+    w = np.ascontiguousarray(words, dtype=np.uint32)
+    p = w[:, 0:3].view(np.float32)
+    e = np.stack([(w[:, 3] >> (8 * a)) & 0xFF for a in range(3)], 1).astype(np.int64)
+    scale = np.ldexp(np.float32(1), (e - 127).astype(np.int32)).astype(np.float32)
+    imask = (w[:, 3] >> 24) & 0xFF
+    meta = w[:, 6:8].copy().view(np.uint8).reshape(-1, 8)
+    q = w[:, 8:20].copy().view(np.uint8).reshape(-1, 6, 8)
+    qlo, qhi = q[:, 0:3], q[:, 3:6]
+    # fmaf(scale, q, p) == p + scale * q rounded once (the product is exact): evaluate in f64, round to f32
+    lo = (p[:, :, None].astype(np.float64) + scale[:, :, None].astype(np.float64) * qlo).astype(np.float32)
+    hi = (p[:, :, None].astype(np.float64) + scale[:, :, None].astype(np.float64) * qhi).astype(np.float32)
+    return {"p": p, "scale": scale, "imask": imask, "child_base": w[:, 4].astype(np.int64),
+            "tri_base": w[:, 5].astype(np.int64), "meta": meta, "qlo": qlo, "qhi": qhi,
+            "lo": lo.transpose(0, 2, 1), "hi": hi.transpose(0, 2, 1)}
+
+
 def camera(width, height):
     """cam_init + cam_calculate_screen_coords + inc_x/inc_y (cpu/src/cam.c, main.c:105-106,243-250)"""
     c = Camera()

@@ -161,3 +161,83 @@ def test_bmp_matches_reference_writer(tmp_path):
 def test_empty_scene_bvh_is_an_error():
     with pytest.raises(RuntimeError):
         host.bvh_build(np.zeros(0, host.TRI_DTYPE), 3, host.Rand(1))
+
+
+def _check_wbvh(s, inflate):
+    """every triangle reachable exactly once; every decoded child box contains its subtree's triangles
+    grown by `inflate` (the conservativeness the fast walk relies on); leaf slots hold 1..4 triangles
+    inside the node's 32-triangle window; children of a node are consecutive records"""
+    words, order, info = host.wbvh_build(s.nodes, s.tri_idx, s.triangles, inflate)
+    D = host.wbvh_decode(words)
+    n = len(s.triangles)
+    assert sorted(order.tolist()) == list(range(n))
+    v = s.triangles["coords"].astype(np.float32)  # [n, 3, 3]
+    tlo, thi = v.min(1), v.max(1)
+    N = len(words)
+    seen_node = np.zeros(N, int)
+    seen_tri = np.zeros(n, int)
+    stack = [(0, 1)]
+    maxd = 0
+    while stack:
+        k, d = stack.pop()
+        seen_node[k] += 1
+        maxd = max(maxd, d)
+        internal = [s_ for s_ in range(8) if (D["imask"][k] >> s_) & 1]
+        for s_ in range(8):
+            m = int(D["meta"][k, s_])
+            lo, hi = D["lo"][k, s_], D["hi"][k, s_]
+            if s_ in internal:
+                c = int(D["child_base"][k]) + sum(1 for j in internal if j < s_)
+                stack.append((c, d + 1))
+                sub = _wbvh_subtree_tris(D, c, order)
+            elif m:
+                cnt, off = m >> 5, m & 31
+                assert 1 <= cnt <= 4 and off + cnt <= 32
+                sub = order[int(D["tri_base"][k]) + off: int(D["tri_base"][k]) + off + cnt]
+                seen_tri[sub] += 1
+            else:
+                continue
+            assert (lo <= tlo[sub] - inflate).all() and (hi >= thi[sub] + inflate).all(), (k, s_)
+    assert (seen_node == 1).all() and (seen_tri == 1).all()
+    assert maxd == info["depth"]
+    return info
+
+
+def _wbvh_subtree_tris(D, k, order, memo={}):
+    key = (id(D), k)
+    if key in memo:
+        return memo[key]
+    out = []
+    internal = [s_ for s_ in range(8) if (D["imask"][k] >> s_) & 1]
+    for s_ in range(8):
+        m = int(D["meta"][k, s_])
+        if s_ in internal:
+            c = int(D["child_base"][k]) + sum(1 for j in internal if j < s_)
+            out.append(_wbvh_subtree_tris(D, c, order))
+        elif m:
+            off, cnt = m & 31, m >> 5
+            out.append(order[int(D["tri_base"][k]) + off: int(D["tri_base"][k]) + off + cnt])
+    memo[key] = np.concatenate(out) if out else np.zeros(0, np.int32)
+    return memo[key]
+
+
+@pytest.mark.parametrize("scene", ["car_boxed", "dragon"])
+def test_wide_bvh_is_conservative_and_complete(scene):
+    s = host.Scene.named(scene).build_bvh("binned_sah")
+    mx = max(16.0, float(np.abs(s.triangles["coords"]).max()))
+    info = _check_wbvh(s, np.ldexp(np.float32(mx), -18))
+    assert info["depth"] <= 16 and info["max_children"] <= 8  # the fast walk's LDS stack bound
+
+
+def test_wide_bvh_from_reference_layout_and_random_mode():
+    """any reference-layout tree works, incl. the reference's own h3 BVH with leaves > 4 triangles"""
+    s = host.Scene.named("car_only").build_bvh(3)
+    assert s.bvh_stats["max_leaf"] > 4
+    _check_wbvh(s, 0.0)
+    _check_wbvh(host.Scene.random(5000).build_bvh("binned_sah"), 1e-4)
+
+
+def test_wide_bvh_single_triangle():
+    s = host.Scene.random(1).build_bvh("binned_sah")
+    words, order, info = host.wbvh_build(s.nodes, s.tri_idx, s.triangles, 0.0)
+    assert info["n_nodes"] == 1 and order.tolist() == [0]

@@ -35,8 +35,8 @@ def main():
 
     def setenv(v):
         parts = v.split(":")
-        for k in ("PRT_REFILL_BELOW", "PRT_WAVE_VARIANT", "PRT_WF_CHUNK_MIN", "PRT_WF_CHUNK_MAX", "PRT_WF_BPC"):
-            os.environ.pop(k, None)
+        for k in [k for k in os.environ if k.startswith("PRT_") and k != "PRT_SCENE_CACHE"]:
+            os.environ.pop(k)
         if len(parts) > 1:
             for kv in parts[1].split(","):
                 k, val = kv.split("=")

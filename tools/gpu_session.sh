@@ -35,6 +35,15 @@ for s in "${@:-smoke pytest bench}"; do
       pmcl2)  run pmcl2 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum -d gpurun_out/pmcl2 -o run --output-format csv -- python3 tools/ab.py --rounds 1  --frames 2 wavefront fast ;;
       pmcfetch) run pmcfetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcfetch -o run --output-format csv -- python3 tools/ab.py --rounds 1  --frames 2 wavefront fast ;;
       pmclat) run pmclat 600 rocprofv3 --pmc TCP_TCC_READ_REQ_LATENCY_sum TCP_TCR_TCP_STALL_CYCLES_sum -d gpurun_out/pmclat -o run --output-format csv -- python3 tools/ab.py --rounds 1  --frames 2 wavefront fast ;;
+      abreg)  run abreg 600 python tools/ab.py --rounds 4 --frames 5 fast fast:PRT_PERSIST_REG=0 ;;
+      abregcar) run abregcar 600 python tools/ab.py --scene car_boxed --rounds 4 --frames 5 fast fast:PRT_PERSIST_REG=0 ;;
+      abold)  for i in 1 2; do
+                  run abnew$i 300 python tools/ab.py --rounds 3 --frames 5 fast fast:PRT_WIDE=0
+                  PRT_LIB_DIR=build/old/lib run abold$i 300 python tools/ab.py --rounds 3 --frames 5 wavefront
+              done ;;
+      abwide) run abwide 300 python tools/ab.py --rounds 4 --frames 5 fast fast:PRT_WIDE=0
+              run abwidecar 300 python tools/ab.py --scene car_boxed --rounds 4 --frames 5 fast fast:PRT_WIDE=0 ;;
+      ctrswide) run ctrswide 300 python tools/counters.py dragon fast ;;
       *) echo "unknown step $step"; exit 2 ;;
     esac
   done
