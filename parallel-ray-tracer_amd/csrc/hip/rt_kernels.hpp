@@ -66,6 +66,16 @@ __device__ __forceinline__ bool degenerate(v3 d) { return d.x == 0.0f || d.y == 
 // with the best hit is always reached (and the tie detected) despite the reciprocal test's rounding.
 constexpr float PRUNE_SLACK = 1.0000005f;
 
+// Shadow rays (fast walks): a triangle can occlude only if ld2 > |o - (o + d t)|^2 (bvh.c:283-290), which
+// holds for no t beyond this bound, so boxes entered past it are pruned from the start. Margins: |d| = 1
+// within 2 ulp (l is normalised, raytracer.c:153), and the rounding of ip = o + d t and o - ip is at most
+// a few ulp of max|o| absolute; 1e-3 relative + 1e-5 max|o| exceed both by > 50x. The result ("some
+// triangle nearer than the light") does not depend on which farther boxes are visited.
+__device__ __forceinline__ float shadow_reach(v3 o, float ld2) {
+    const float om = fmaxf(fmaxf(__builtin_fabsf(o.x), __builtin_fabsf(o.y)), __builtin_fabsf(o.z));
+    return __builtin_sqrtf(ld2) * 1.001f + om * 1e-5f;
+}
+
 // ---------------------------------------------------------------- one interior node
 // Entry distances of both children of record `ref`, nearer child first (empty child / miss: FMAX).
 template <bool STRICT>
@@ -185,7 +195,8 @@ template <bool STRICT, bool COUNT, bool REG = true>
 __device__ __forceinline__ bool visible_walk(const DBvh& B, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c) {
     RayPre p = {};
     if (!STRICT) p = ray_pre(o, d);
-    float best = FMAX;
+    // fast walk: prune at the light (visit(t, best) tests t <= best * PRUNE_SLACK); strict: the reference's walk
+    float best = STRICT ? FMAX : shadow_reach(o, ld2);
     int sp = 0, cur = B.root;
     if (!REG) {
         stk[0] = B.root;
@@ -368,11 +379,12 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
     const RayPre p = ray_pre(o, d);
     const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
     float best = FMAX;
+    const float reach = shadow_reach(o, ld2);
     int node = 0, sp = 0;
     for (;;) {
         unsigned nh, th, imask, nl;
         int cb, tb;
-        wide_node<COUNT>(W, node, p, oct, best * PRUNE_SLACK, nh, th, cb, tb, imask, nl);
+        wide_node<COUNT>(W, node, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nl);
         if (COUNT) {
             c.shi++;
             c.shl += nl;

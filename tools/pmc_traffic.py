@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run into profiles/: kernel-trace stats (markdown) and the PMC HBM traffic
+of the bench's production kernel (profiles/pmc_traffic.json, read by bench.py for roofline.traffic).
+
+traffic per launch = 2 x FETCH_SIZE + WRITE_SIZE (kB -> bytes): MI355X_MICROARCH.md §HBM — on gfx950
+FETCH_SIZE reports half the bytes of 16-B-per-lane reads (the kernel's node/triangle loads are float4
+per lane); WRITE_SIZE reads exactly for 16-B stores. Counters come from separate --pmc passes.
+usage: tools/pmc_traffic.py gpurun_out/prof_<tag> <round-tag> [bench key]
+"""
+import csv
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROD = "k_persist<4, false, false, true>"
+
+
+def rows(path):
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+def per_kernel(path, counter):
+    out = {}
+    for r in rows(path):
+        if r["Counter_Name"] == counter:
+            out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+    return out
+
+
+def find(d, sub):
+    for k, v in d.items():
+        if sub in k:
+            return k, v
+    return None, None
+
+
+def main():
+    prof, tag = sys.argv[1], sys.argv[2]
+    key = sys.argv[3] if len(sys.argv) > 3 else "dragon_1920x1080_fast_random"
+    pdir = os.path.join(ROOT, "profiles")
+    os.makedirs(pdir, exist_ok=True)
+    # kernel trace stats
+    stats = rows(os.path.join(prof, "trace", "run_kernel_stats.csv"))
+    lines = [f"# rocprofv3 --kernel-trace --stats ({tag})", "",
+             f"command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline`",
+             "", "| kernel | calls | total ms | avg ms | min ms | max ms | % |", "|---|---|---|---|---|---|---|"]
+    for r in stats:
+        lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
+                     f"{float(r['AverageNs']) / 1e6:.4f} | {float(r['MinNs']) / 1e6:.4f} | "
+                     f"{float(r['MaxNs']) / 1e6:.4f} | {float(r['Percentage']):.2f} |")
+    fetch = per_kernel(os.path.join(prof, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(prof, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    kf, vf = find(fetch, PROD)
+    kw, vw = find(write, PROD)
+    res = None
+    if vf and vw:
+        f_kb, w_kb = statistics.median(vf), statistics.median(vw)
+        hbm = 2 * f_kb * 1024 + w_kb * 1024
+        _, avg = find({r["Name"]: float(r["AverageNs"]) for r in stats}, PROD)
+        res = {"kernel": kf, "launches": len(vf), "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
+               "hbm_bytes_per_launch": hbm, "trace_avg_ms": avg / 1e6 if avg else None,
+               "hbm_gbs_at_trace_avg": hbm / (avg / 1e9) / 1e9 if avg else None,
+               "rule": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md §HBM, gfx950 FETCH_SIZE halving)",
+               "source": f"profiles/{tag}_kernel_stats.md, gpurun_out/{os.path.basename(prof)}", "round": tag}
+        lines += ["", f"## HBM traffic of `{PROD}` (PMC, separate passes)", "",
+                  f"- FETCH_SIZE median {f_kb:.0f} kB/launch, WRITE_SIZE median {w_kb:.0f} kB/launch",
+                  f"- traffic = 2 x FETCH + WRITE = {hbm / 1e6:.1f} MB/launch"
+                  + (f" = {res['hbm_gbs_at_trace_avg']:.1f} GB/s at the trace average" if avg else "")]
+        tj_path = os.path.join(pdir, "pmc_traffic.json")
+        tj = json.load(open(tj_path)) if os.path.exists(tj_path) else {}
+        tj[key] = res
+        json.dump(tj, open(tj_path, "w"), indent=1)
+    # other PMC passes, if present: per-kernel medians
+    for sub in ("pmc_sq", "pmc_l2", "pmc_valu"):
+        p = os.path.join(prof, sub, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        agg = {}
+        for r in rows(p):
+            if PROD in r["Kernel_Name"]:
+                agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+        if agg:
+            lines += ["", f"### {sub} (`{PROD}`, median per launch)", ""]
+            lines += [f"- {k}: {statistics.median(v):.4g}" for k, v in sorted(agg.items())]
+    with open(os.path.join(pdir, f"{tag}_kernel_stats.md"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+    if res:
+        print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
