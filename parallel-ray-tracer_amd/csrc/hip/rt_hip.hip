@@ -289,7 +289,7 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     const bool own_acc = sc->accel == RT_ACCEL_AUTO;
     if (own_acc) {
         // the fast walk's BVH: binned SAH over the same triangles (librt_host.so), boxes inflated by
-        // 2^-18 of the scene's coordinate magnitude (>= the reciprocal-FMA test's rounding reach)
+        // 2^-16 of the scene's coordinate magnitude (>= 20x the slab tests' rounding reach)
         rt_bvh_node* nodes = nullptr;
         int nlen = 0;
         int* idx = nullptr;
@@ -299,7 +299,7 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
         for (int i = 0; i < n; i++)
             for (const rt_vec3& c : sc->triangles[i].coords)
                 mx = std::max(mx, std::max(std::fabs(c.x), std::max(std::fabs(c.y), std::fabs(c.z))));
-        const float inflate = std::ldexp(mx, -18);
+        const float inflate = std::ldexp(mx, -16);
         rc = build_view(ctx, nodes, nlen, idx, sc->triangles, n, inflate, ha);
         // ... and its 8-wide quantised form (same inflation, planes rounded outward)
         uint32_t* words = nullptr;
@@ -389,6 +389,8 @@ void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int de
         auto k = count ? rtd::k_persist<MAXB, false, true> : rtd::k_persist<MAXB, false, false>;
         if (const char* e = std::getenv("PRT_PERSIST_REG"); e && std::atoi(e) == 0)  // A/B: stack-only walk
             k = count ? rtd::k_persist<MAXB, false, true, false> : rtd::k_persist<MAXB, false, false, false>;
+        if (const char* e = std::getenv("PRT_PERSIST_OCC"); e && std::atoi(e) == 4)  // A/B: <= 128 VGPRs
+            k = count ? rtd::k_persist<MAXB, false, true, true, 4> : rtd::k_persist<MAXB, false, false, true, 4>;
         int blocks = std::max(1, std::min(resident(k, device), (A.n_tiles + 3) / 4));
         k<<<blocks, rtd::BLOCK, 0, s>>>(A);
     } else {

@@ -287,6 +287,13 @@ __device__ __forceinline__ void wide_node(const DWide& W, int node, const RayPre
     cbase = __float_as_int(f1.x);
     tbase = __float_as_int(f1.y);
     const unsigned m[2] = {__float_as_uint(f1.z), __float_as_uint(f1.w)};
+    // The ray in the node's grid: plane q of axis x is entered at t = fma(q, 2^ex / d.x, (p.x - o.x) / d.x),
+    // computed as fma(q, kx, ax) with kx = 2^ex * (1/d.x) (exact: power-of-two scale) and
+    // ax = fma(p.x, 1/d.x, -o.x/d.x): one FMA per plane. Its rounding reach (a few ulp of max|coord| / |d|)
+    // is covered >= 20x by the boxes' inflation (2^-16 max|coord|, rt_hip.hip).
+    const float ax = __builtin_fmaf(f0.x, p.ix, -p.ox), ay = __builtin_fmaf(f0.y, p.iy, -p.oy),
+                az = __builtin_fmaf(f0.z, p.iz, -p.oz);
+    const float kx = sx * p.ix, ky = sy * p.iy, kz = sz * p.iz;
     // near / far plane bytes per axis from the direction signs (== min / max of the two slab ends)
     const bool bx = (oct & 1u) != 0, by = (oct & 2u) != 0, bz = (oct & 4u) != 0;
     const unsigned lx[2] = {__float_as_uint(f2.x), __float_as_uint(f2.y)}, ly[2] = {__float_as_uint(f2.z), __float_as_uint(f2.w)},
@@ -298,16 +305,14 @@ __device__ __forceinline__ void wide_node(const DWide& W, int node, const RayPre
 #pragma unroll
     for (int s = 0; s < 8; s++) {
         const int h = s >> 2, b = s & 3;
-        const float nxp = __builtin_fmaf(sx, ubyte(bx ? hx[h] : lx[h], b), f0.x);
-        const float fxp = __builtin_fmaf(sx, ubyte(bx ? lx[h] : hx[h], b), f0.x);
-        const float nyp = __builtin_fmaf(sy, ubyte(by ? hy[h] : ly[h], b), f0.y);
-        const float fyp = __builtin_fmaf(sy, ubyte(by ? ly[h] : hy[h], b), f0.y);
-        const float nzp = __builtin_fmaf(sz, ubyte(bz ? hz[h] : lz[h], b), f0.z);
-        const float fzp = __builtin_fmaf(sz, ubyte(bz ? lz[h] : hz[h], b), f0.z);
-        const float tmin = fmaxf(fmaxf(__builtin_fmaf(nxp, p.ix, -p.ox), __builtin_fmaf(nyp, p.iy, -p.oy)),
-                                 __builtin_fmaf(nzp, p.iz, -p.oz));
-        const float tmax = fminf(fminf(__builtin_fmaf(fxp, p.ix, -p.ox), __builtin_fmaf(fyp, p.iy, -p.oy)),
-                                 __builtin_fmaf(fzp, p.iz, -p.oz)) * 1.00000024f;
+        const float tnx = __builtin_fmaf(ubyte(bx ? hx[h] : lx[h], b), kx, ax);
+        const float tfx = __builtin_fmaf(ubyte(bx ? lx[h] : hx[h], b), kx, ax);
+        const float tny = __builtin_fmaf(ubyte(by ? hy[h] : ly[h], b), ky, ay);
+        const float tfy = __builtin_fmaf(ubyte(by ? ly[h] : hy[h], b), ky, ay);
+        const float tnz = __builtin_fmaf(ubyte(bz ? hz[h] : lz[h], b), kz, az);
+        const float tfz = __builtin_fmaf(ubyte(bz ? lz[h] : hz[h], b), kz, az);
+        const float tmin = fmaxf(fmaxf(tnx, tny), tnz);
+        const float tmax = fminf(fminf(tfx, tfy), tfz) * 1.00000024f;
         const bool hit = tmax >= tmin && tmax > 0.0f && tmin <= lim;
         const unsigned meta = (m[h] >> (8 * b)) & 0xFFu;
         if (hit) {
@@ -647,8 +652,11 @@ __global__ __launch_bounds__(BLOCK) void k_tiles(KArgs A) {
 // (one returning atomic per wave per tile; microarch row "dequeue"). Tiles are dealt in row-major
 // order of 8x8 blocks so that concurrently running waves trace neighbouring pixels (shared L1/L2
 // lines for the upper BVH levels).
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true>
-__global__ __launch_bounds__(BLOCK) void k_persist(KArgs A) {
+// OCC: waves per SIMD the register allocation must allow (0 = compiler's choice); 4 caps VGPRs at 128
+// (the LDS stack allows 4 workgroups per CU).
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int OCC = 0>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(OCC > 0 ? OCC : 1)))
+void k_persist(KArgs A) {
     __shared__ int lds[STACK * BLOCK];
     int* stk = lds + threadIdx.x;
     const int lane = threadIdx.x & 63;

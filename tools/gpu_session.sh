@@ -44,6 +44,12 @@ for s in "${@:-smoke pytest bench}"; do
       abwide) run abwide 300 python tools/ab.py --rounds 4 --frames 5 fast fast:PRT_WIDE=0
               run abwidecar 300 python tools/ab.py --scene car_boxed --rounds 4 --frames 5 fast fast:PRT_WIDE=0 ;;
       ctrswide) run ctrswide 300 python tools/counters.py dragon fast ;;
+      abocc)  run abocc 300 python tools/ab.py --rounds 4 --frames 5 fast fast:PRT_PERSIST_OCC=4
+              run abocccar 300 python tools/ab.py --scene car_boxed --rounds 4 --frames 5 fast fast:PRT_PERSIST_OCC=4 ;;
+      abhead) for i in 1 2 3; do
+                  run abnew$i 300 python tools/ab.py --rounds 3 --frames 5 fast
+                  PRT_LIB_DIR=build/old/lib run abold$i 300 python tools/ab.py --rounds 3 --frames 5 fast
+              done ;;
       *) echo "unknown step $step"; exit 2 ;;
     esac
   done
