@@ -98,7 +98,8 @@ typedef struct rt_stats {
     unsigned long long fallbacks;      /* fast-kernel rays re-walked strictly (zero direction component or exact tie) */
     unsigned long long stack_overflows; /* must be 0 (rt_get_stats fails otherwise)          */
     unsigned long long node_bytes;     /* BVH node / leaf record bytes read (RT_FLAG_COUNTERS; fused kernels) */
-    unsigned long long reserved[1];
+    unsigned long long wave_steps;     /* wave-level wide-node steps (RT_FLAG_COUNTERS): SIMD efficiency =
+                                          (ch_inner + sh_inner of the wide walk) / (64 * wave_steps) */
 } rt_stats;
 
 int rt_device_count(void);

@@ -72,6 +72,8 @@ struct KArgs {
     unsigned int* work;            // persistent-kernel tile / pixel counter
     int n_tiles, tiles_x;
     int refill_below;              // k_wave: leave the traversal loop when fewer lanes than this still trace
+    unsigned long long* tile_trace;  // diagnostics (PRT_TILE_TRACE): per-tile timeline (rt_kernels.hpp)
+    const int* tile_order;           // nullable: k-th dealt tile = tile_order[k] (default: row-major)
 };
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

@@ -67,6 +67,8 @@ struct rt_ctx {
     int* last_hit = nullptr;
     size_t last_pixels = 0;
     unsigned long long* d_counters = nullptr;  // rtd::NCOUNT
+    int* d_order = nullptr;                    // tile dealing order (PRT_TILE_ORDER), for order_tx x order_ty tiles
+    int order_tx = 0, order_ty = 0;
     unsigned int* d_work = nullptr;
     // wavefront pipeline buffers (rt_wf.hpp), sized for wf_pix pixels x wf_lights lights
     void* wf_mem = nullptr;
@@ -391,6 +393,14 @@ void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int de
             k = count ? rtd::k_persist<MAXB, false, true, false> : rtd::k_persist<MAXB, false, false, false>;
         if (const char* e = std::getenv("PRT_PERSIST_OCC"); e && std::atoi(e) == 4)  // A/B: <= 128 VGPRs
             k = count ? rtd::k_persist<MAXB, false, true, true, 4> : rtd::k_persist<MAXB, false, false, true, 4>;
+        if (A.tile_trace)  // diagnostics (PRT_TILE_TRACE)
+            k = count ? rtd::k_persist<MAXB, false, true, true, 3, true> : rtd::k_persist<MAXB, false, false, true, 3, true>;
+        if (const char* e = std::getenv("PRT_REGEN"); e && std::atoi(e) == 1 && A.spp <= 1) {  // A/B: path regeneration
+            auto kr = count ? rtd::k_regen<MAXB, true> : rtd::k_regen<MAXB, false>;
+            int blocks = std::max(1, std::min(resident(kr, device), (A.n_tiles + 3) / 4));
+            kr<<<blocks, rtd::BLOCK, 0, s>>>(A);
+            return;
+        }
         int blocks = std::max(1, std::min(resident(k, device), (A.n_tiles + 3) / 4));
         k<<<blocks, rtd::BLOCK, 0, s>>>(A);
     } else {
@@ -600,6 +610,40 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     ctx->ev0 = ctx->ev0s[slot];
     ctx->ev1 = ctx->ev1s[slot];
     HIPC(hipEventRecord(ctx->ev0, ctx->stream));
+    // diagnostics: PRT_TILE_TRACE=<file> writes 4 x uint64 per tile of a k_persist frame (rt_kernels.hpp)
+    // (s_memrealtime, 100 MHz); synchronous, never used by tests or the bench
+    const char* trace_path = std::getenv("PRT_TILE_TRACE");
+    unsigned long long* d_trace = nullptr;
+    if (trace_path && kernel == RT_KERNEL_FAST) {
+        HIPC(hipMalloc((void**)&d_trace, sizeof(unsigned long long) * 4 * (size_t)A.n_tiles));
+        HIPC(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * 4 * (size_t)A.n_tiles, ctx->stream));
+        A.tile_trace = d_trace;
+    }
+    // Tile dealing order of the persistent kernel: centre-out (default). The frame ends when the slowest
+    // tile does (PRT_TILE_TRACE: 8x8 tiles range from 2 us to ~1.9 ms; expensive ones are deep reflection
+    // chains, usually on the object in view); dealing from the centre starts them first (bench frame
+    // -7 %). PRT_TILE_ORDER=rows: row-major (A/B knob).
+    const char* order_env = std::getenv("PRT_TILE_ORDER");
+    if (kernel == RT_KERNEL_FAST && !(order_env && std::strcmp(order_env, "rows") == 0)) {
+        const int ty = A.n_tiles / A.tiles_x;
+        if (!ctx->d_order || ctx->order_tx != A.tiles_x || ctx->order_ty != ty) {
+            std::vector<int> ord(A.n_tiles);
+            for (int i = 0; i < A.n_tiles; i++) ord[i] = i;
+            const float cx = 0.5f * A.tiles_x, cy = 0.5f * ty;
+            std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+                const float ax = a % A.tiles_x + 0.5f - cx, ay = a / A.tiles_x + 0.5f - cy;
+                const float bx = b % A.tiles_x + 0.5f - cx, by = b / A.tiles_x + 0.5f - cy;
+                return ax * ax + ay * ay < bx * bx + by * by;
+            });
+            if (ctx->d_order) HIPC(hipFree(ctx->d_order));
+            ctx->d_order = nullptr;
+            HIPC(hipMalloc((void**)&ctx->d_order, sizeof(int) * ord.size()));
+            HIPC(hipMemcpy(ctx->d_order, ord.data(), sizeof(int) * ord.size(), hipMemcpyHostToDevice));
+            ctx->order_tx = A.tiles_x;
+            ctx->order_ty = ty;
+        }
+        A.tile_order = ctx->d_order;
+    }
     if (kernel == RT_KERNEL_WAVEFRONT) {
         const int rc = launch_wf(ctx, A, count);
         if (rc) return rc;
@@ -610,6 +654,16 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     }
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(ctx->ev1, ctx->stream));
+    if (d_trace) {
+        std::vector<unsigned long long> h(4 * (size_t)A.n_tiles);
+        HIPC(hipStreamSynchronize(ctx->stream));
+        HIPC(hipMemcpy(h.data(), d_trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+        HIPC(hipFree(d_trace));
+        if (FILE* f = std::fopen(trace_path, "wb")) {
+            std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+            std::fclose(f);
+        }
+    }
     ctx->launches++;
     ctx->last_rgb = rgb;
     ctx->last_hit = A.hit;
@@ -684,6 +738,7 @@ extern "C" int rt_get_stats(rt_ctx* ctx, rt_stats* st) {
     st->fallbacks = c[rtd::C_FALLBACK];
     st->stack_overflows = c[rtd::C_ERR];
     st->node_bytes = 8 * c[rtd::C_NB];
+    st->wave_steps = c[rtd::C_WS];
     if (c[rtd::C_ERR]) {
         ctx->err = "traversal stack overflow: BVH deeper than 32 levels";
         return RT_E_STATE;
@@ -701,6 +756,7 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     if (ctx->wf_mem) (void)hipFree(ctx->wf_mem);
     if (ctx->d_rgb_own) (void)hipFree(ctx->d_rgb_own);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->d_order) (void)hipFree(ctx->d_order);
     if (ctx->d_work) (void)hipFree(ctx->d_work);
     for (int i = 0; i < rt_ctx::NEV; i++) {
         if (ctx->ev0s[i]) (void)hipEventDestroy(ctx->ev0s[i]);

@@ -34,11 +34,12 @@ constexpr int STACK = 34;  // max stack = max depth (32, bvh.c:84) + 2
 enum {
     C_PRIM, C_REFL, C_SHAD, C_SKIP, C_HITS, C_CHI, C_CHL, C_CHT, C_SHI, C_SHL, C_SHT, C_PIX, C_ERR, C_FALLBACK,
     C_NB,  // node/leaf record bytes read, in 8-B units (RT_FLAG_COUNTERS)
+    C_WS,  // wave-level wide-node steps (RT_FLAG_COUNTERS): lane visits / (64 x this) = SIMD efficiency
     NCOUNT = 16
 };
 
 struct Ctr {
-    unsigned prim, refl, shad, skip, hits, chi, chl, cht, shi, shl, sht, pix, err, fb, nb;
+    unsigned prim, refl, shad, skip, hits, chi, chl, cht, shi, shl, sht, pix, err, fb, nb, ws;
 };
 
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
@@ -51,10 +52,10 @@ template <bool COUNT>
 __device__ __forceinline__ void flush(const Ctr& c, unsigned long long* g) {
     const bool l0 = (threadIdx.x & 63) == 0;
     unsigned v[NCOUNT] = {c.prim, c.refl, c.shad, c.skip, c.hits, c.chi, c.chl, c.cht,
-                          c.shi, c.shl, c.sht, c.pix, c.err, c.fb, c.nb, 0};
+                          c.shi, c.shl, c.sht, c.pix, c.err, c.fb, c.nb, c.ws};
 #pragma unroll
-    for (int i = 0; i < 15; i++) {
-        if (!COUNT && ((i >= C_CHI && i <= C_SHT) || i == C_NB)) continue;
+    for (int i = 0; i < 16; i++) {
+        if (!COUNT && ((i >= C_CHI && i <= C_SHT) || i >= C_NB)) continue;
         unsigned s = wave_sum(v[i]);
         if (l0 && s) atomicAdd(g + i, (unsigned long long)s);
     }
@@ -270,6 +271,12 @@ __device__ __forceinline__ bool visible_walk(const DBvh& B, v3 o, v3 d, float ld
 // best * PRUNE_SLACK so that exact ties are always met and reported.
 constexpr int WSTACK = 16;  // node-group entries (2 ints) in the STACK-int LDS column; builder depth <= 16
 
+// 1 in the lowest active lane of the wave, 0 elsewhere (wave-level step counting)
+__device__ __forceinline__ unsigned first_active_lane() {
+    const unsigned long long ex = __builtin_amdgcn_read_exec();
+    return (unsigned)((threadIdx.x & 63u) == (unsigned)__builtin_ctzll(ex));
+}
+
 __device__ __forceinline__ float ubyte(unsigned w, int b) { return (float)((w >> (8 * b)) & 0xFFu); }
 
 // Tests the 8 children of wide node `node`: nh = hit interior slots as bits (s ^ oct), th = triangle
@@ -311,18 +318,18 @@ __device__ __forceinline__ void wide_node(const DWide& W, int node, const RayPre
         const float tfy = __builtin_fmaf(ubyte(by ? ly[h] : hy[h], b), ky, ay);
         const float tnz = __builtin_fmaf(ubyte(bz ? hz[h] : lz[h], b), kz, az);
         const float tfz = __builtin_fmaf(ubyte(bz ? lz[h] : hz[h], b), kz, az);
-        const float tmin = fmaxf(fmaxf(tnx, tny), tnz);
-        const float tmax = fminf(fminf(tfx, tfy), tfz) * 1.00000024f;
-        const bool hit = tmax >= tmin && tmax > 0.0f && tmin <= lim;
-        const unsigned meta = (m[h] >> (8 * b)) & 0xFFu;
-        if (hit) {
-            if ((imask >> s) & 1u) {
-                nh |= 1u << (s ^ oct);
-            } else if (meta) {
-                th |= ((1u << (meta >> 5)) - 1u) << (meta & 31u);
-                nleaf++;
-            }
-        }
+        // Inflation (2^-16 max|coord|) puts every computed near plane strictly before and every far plane
+        // strictly after the child's true box, per axis, so the interval below contains the true one; the
+        // folded test max(tmin, 0) <= min(tmax, lim) only adds visits (e.g. tmax == 0): conservative.
+        const float lo = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f));
+        const float hi = fminf(fminf(tfx, tfy), fminf(tfz, lim));
+        const unsigned hm = lo <= hi ? ~0u : 0u;
+        const unsigned ib = (imask >> s) & 1u;
+        const unsigned meta = (m[h] >> (8 * b)) & 0xFFu;  // leaf: count << 5 | offset; 0 for empty / interior
+        nh |= hm & (0u - ib) & (1u << (s ^ oct));
+        const unsigned lb = hm & (ib - 1u) & (((1u << (meta >> 5)) - 1u) << (meta & 31u));
+        th |= lb;
+        if (COUNT) nleaf += lb ? 1u : 0u;
     }
 }
 
@@ -340,6 +347,7 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
             c.chi++;
             c.chl += nl;
             c.nb += 10;
+            c.ws += first_active_lane();
         }
         while (th) {
             const int i = tb + __builtin_ctz(th);
@@ -394,6 +402,7 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
             c.shi++;
             c.shl += nl;
             c.nb += 10;
+            c.ws += first_active_lane();
         }
         while (th) {
             const int i = tb + __builtin_ctz(th);
@@ -430,6 +439,107 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
         node = cb + __popc(imask & ((1u << slot) - 1u));
     }
     return true;
+}
+
+// Shadow rays of all lights of one shading point in ONE traversal loop: a lane whose ray finishes
+// (occluded, or its stack empties) starts its next light's ray at once, so a wave runs max over lanes of
+// the SUM of their shadow walks instead of the sum over lights of the max. Bit j of `need`: light j needs
+// a shadow ray (j < 32); returns the visible ones. Each ray is visible_wide's walk exactly (same
+// direction, ld2 and pruning), so the visibility bits are the reference's.
+template <bool COUNT>
+__device__ __forceinline__ unsigned visible_wide_multi(const DScene& s, v3 ip, unsigned need, int* __restrict__ stk,
+                                                       Ctr& c) {
+    const DWide& W = s.wide;
+    unsigned vis = 0;
+    int j = 0, node = 0, sp = 0;
+    float best = FMAX, reach = FMAX;
+    v3 d = ip;
+    RayPre p = {};
+    unsigned oct = 0;
+    bool act = false;
+    auto start = [&]() {
+        act = need != 0u;
+        if (!act) return;
+        j = __builtin_ctz(need);
+        need &= need - 1u;
+        const v3 Lp = xyz(s.lights[2 * j]);
+        v3 l = sub(Lp, ip);  // raytracer.c:150-153 (same ops as path_step)
+        const float mg = mag(l);
+        l = dvs(l, mg);
+        const v3 tmp = sub(ip, Lp);
+        const float ld2 = dot(tmp, tmp);
+        d = l;
+        p = ray_pre(ip, d);
+        oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
+        best = FMAX;
+        reach = shadow_reach(ip, ld2);
+        node = 0;
+        sp = 0;
+    };
+    start();
+    while (act) {
+        unsigned nh, th, imask, nl;
+        int cb, tb;
+        wide_node<COUNT>(W, node, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nl);
+        if (COUNT) {
+            c.shi++;
+            c.shl += nl;
+            c.nb += 10;
+            c.ws += first_active_lane();
+        }
+        bool occluded = false;
+        if (th) {
+            const v3 Lp = xyz(s.lights[2 * j]);
+            const v3 tmp = sub(ip, Lp);
+            const float ld2 = dot(tmp, tmp);
+            while (th) {
+                const int i = tb + __builtin_ctz(th);
+                th &= th - 1u;
+                int k;
+                const float tt = hit_triangle(ip, d, W.tris + 3 * i, k);
+                if (COUNT) c.sht++;
+                if (tt < best) {
+                    best = tt;
+                    const v3 q = add(ip, mul(d, best));
+                    const v3 oi = sub(ip, q);
+                    if (ld2 > dot(oi, oi)) {
+                        occluded = true;
+                        break;
+                    }
+                }
+            }
+        }
+        if (occluded) {
+            start();
+            continue;
+        }
+        if (!nh) {
+            if (sp == 0) {  // walked everything up to the light: visible
+                vis |= 1u << j;
+                start();
+                continue;
+            }
+            --sp;
+            cb = stk[(2 * sp) * BLOCK];
+            const unsigned bits = (unsigned)stk[(2 * sp + 1) * BLOCK];
+            imask = bits >> 8;
+            nh = bits & 0xFFu;
+        }
+        const unsigned slot = (unsigned)__builtin_ctz(nh) ^ oct;
+        nh &= nh - 1u;
+        if (nh) {
+            if (sp >= WSTACK) {
+                c.err++;
+                start();
+                continue;
+            }
+            stk[(2 * sp) * BLOCK] = cb;
+            stk[(2 * sp + 1) * BLOCK] = (int)((imask << 8) | nh);
+            ++sp;
+        }
+        node = cb + __popc(imask & ((1u << slot) - 1u));
+    }
+    return vis;
 }
 
 // Closest hit with the kernel's policy; returns the ORIGINAL triangle index (-1 = miss).
@@ -483,87 +593,117 @@ __device__ __forceinline__ void seti(int (&a)[MAXB], int i, int v) {
         if (k == i) a[k] = v;
 }
 
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true>
-__device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0) {
-    const DScene& s = A.s;
-    v3 o = mk(A.pos[0], A.pos[1], A.pos[2]);
+// One level of the reference recursion (raytracer.c:101-177) for a path whose ray at level `it` is
+// (o, d): closest hit, Lambert/Blinn with one shadow ray per light, reflection. Stores the level's
+// colour and material; returns true when the path ends (L = levels kept, tail = the reference's
+// raytrace(.., BOUNCES) returned {0,0,0}), otherwise leaves the reflection ray in (o, d).
+template <int MAXB, bool STRICT, bool COUNT, bool REG>
+__device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, v3& o, v3& d, v3 (&cols)[MAXB],
+                                          int (&mats)[MAXB], int& L, bool& tail, int& hit0, float& t0,
+                                          int* __restrict__ stk, Ctr& c) {
     const v3 amb = mk(s.amb_x, s.amb_y, s.amb_z);
-    v3 cols[MAXB];
-    int mats[MAXB];
-#pragma unroll
-    for (int k = 0; k < MAXB; k++) {
-        cols[k] = mk(0.0f, 0.0f, 0.0f);
-        mats[k] = 0;
+    float best;
+    int nd;
+    if (it == 0) c.prim++;
+    else c.refl++;
+    const int orig = closest<STRICT, COUNT, REG>(s, o, d, best, nd, stk, c);
+    if (it == 0) {
+        hit0 = orig;
+        t0 = best;
     }
-    int L = 0;
-    bool tail = false;
-    for (int it = 0; it < A.bounces; ++it) {
-        float best;
-        int nd;
-        if (it == 0) c.prim++;
-        else c.refl++;
-        const int orig = closest<STRICT, COUNT, REG>(s, o, d, best, nd, stk, c);
-        if (it == 0) {
-            hit0 = orig;
-            t0 = best;
-        }
-        if (orig < 0) {  // raytracer.c:132-135
-            set3<MAXB>(cols, it, mk(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z));
-            L = it + 1;
-            break;
-        }
-        c.hits++;
-        const v3 ip = add(o, mul(d, best));  // raytracer.c:137-138
-        const float4 sh0 = s.shade[2 * orig], sh1 = s.shade[2 * orig + 1];
-        const int m = __float_as_int(sh0.w);
-        const v3 n = nd ? xyz(sh1) : xyz(sh0);
-        const v3 ks = xyz(s.mats[3 * m]), kd = xyz(s.mats[3 * m + 1]), kr = xyz(s.mats[3 * m + 2]);
-        v3 col = mk(0.0f + kd.x * amb.x, 0.0f + kd.y * amb.y, 0.0f + kd.z * amb.z);  // :144-146
-        const v3 v = mul(d, -1.0f);                                                      // :147
-        for (int j = 0; j < s.n_lights; ++j) {                                           // :149-160
-            const v3 Lp = xyz(s.lights[2 * j]), kl = xyz(s.lights[2 * j + 1]);
-            v3 l = sub(Lp, ip);
-            float mg = mag(l);
-            l = dvs(l, mg);
-            mg *= mg;
-            const float ndl = dot(n, l);
-            const v3 h = normalize(add(l, v));  // lambert_blinn, raytracer.c:21-33
-            const float coeff = fmaxf(0.0f, dot(n, h));
-            const v3 cr = mk(kd.x * fmaxf(0.0f, ndl) + ks.x * coeff, kd.y * fmaxf(0.0f, ndl) + ks.y * coeff,
-                             kd.z * fmaxf(0.0f, ndl) + ks.z * coeff);
-            const v3 tmp = sub(ip, Lp), tmp2 = sub(Lp, ip);  // light_v, raytracer.c:62-99
-            const float ld2 = dot(tmp, tmp);
-            int V;
-            if (dot(tmp2, n) < 0) {
-                V = 0;
+    if (orig < 0) {  // raytracer.c:132-135
+        set3<MAXB>(cols, it, mk(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z));
+        L = it + 1;
+        tail = false;
+        return true;
+    }
+    c.hits++;
+    const v3 ip = add(o, mul(d, best));  // raytracer.c:137-138
+    const float4 sh0 = s.shade[2 * orig], sh1 = s.shade[2 * orig + 1];
+    const int m = __float_as_int(sh0.w);
+    const v3 n = nd ? xyz(sh1) : xyz(sh0);
+    const v3 ks = xyz(s.mats[3 * m]), kd = xyz(s.mats[3 * m + 1]), kr = xyz(s.mats[3 * m + 2]);
+    v3 col = mk(0.0f + kd.x * amb.x, 0.0f + kd.y * amb.y, 0.0f + kd.z * amb.z);  // :144-146
+    const v3 v = mul(d, -1.0f);                                                      // :147
+    // fast walk over the wide view: visibility of every light first (one batched walk), then the
+    // reference's per-light accumulation in light order with those bits
+    const bool batched = !STRICT && s.wide.nodes != nullptr && s.n_lights <= 32;
+    unsigned vis = 0;
+    if (batched) {
+        unsigned need = 0;
+        for (int j = 0; j < s.n_lights; ++j) {
+            const v3 Lp = xyz(s.lights[2 * j]);
+            const v3 tmp2 = sub(Lp, ip);
+            if (dot(tmp2, n) < 0) {  // light_v's back-face early-out, raytracer.c:66-67
                 c.skip++;
-            } else {
-                c.shad++;
-                V = visible<STRICT, COUNT, REG>(s, ip, l, ld2, stk, c) ? 1 : 0;
+                continue;
             }
-            const float fV = (float)V;
-            col.x = col.x + fV * kl.x * cr.x / mg;
-            col.y = col.y + fV * kl.y * cr.y / mg;
-            col.z = col.z + fV * kl.z * cr.z / mg;
+            c.shad++;
+            v3 l = sub(Lp, ip);
+            const float mg = mag(l);
+            l = dvs(l, mg);
+            if (degenerate(l)) {  // NaN-slab semantics: the strict walk of the reference BVH
+                const v3 tmp = sub(ip, Lp);
+                c.fb++;
+                if (visible_walk<true, COUNT, REG>(s.ref, ip, l, dot(tmp, tmp), stk, c)) vis |= 1u << j;
+            } else {
+                need |= 1u << j;
+            }
         }
-        const v3 dd = mul(v, -1.0f);  // raytracer.c:163-166
-        const v3 ns = mul(n, 2.0f * __builtin_fabsf(dot(dd, n)));
-        const v3 r = normalize(add(dd, ns));
-        set3<MAXB>(cols, it, col);
-        seti<MAXB>(mats, it, m);
-        if (!(mag(kr) > 0.0f)) {  // raytracer.c:168
-            L = it + 1;
-            break;
-        }
-        if (it + 1 == A.bounces) {  // raytrace(.., BOUNCES) returns {0,0,0}: col += kr * 0
-            L = it + 1;
-            tail = true;
-            break;
-        }
-        o = ip;
-        d = r;
+        vis |= visible_wide_multi<COUNT>(s, ip, need, stk, c);
     }
-    // fold: R_i = c_i + kr_i * R_{i+1}, deepest level first (raytracer.c:169-172)
+    for (int j = 0; j < s.n_lights; ++j) {                                           // :149-160
+        const v3 Lp = xyz(s.lights[2 * j]), kl = xyz(s.lights[2 * j + 1]);
+        v3 l = sub(Lp, ip);
+        float mg = mag(l);
+        l = dvs(l, mg);
+        mg *= mg;
+        const float ndl = dot(n, l);
+        const v3 h = normalize(add(l, v));  // lambert_blinn, raytracer.c:21-33
+        const float coeff = fmaxf(0.0f, dot(n, h));
+        const v3 cr = mk(kd.x * fmaxf(0.0f, ndl) + ks.x * coeff, kd.y * fmaxf(0.0f, ndl) + ks.y * coeff,
+                         kd.z * fmaxf(0.0f, ndl) + ks.z * coeff);
+        const v3 tmp = sub(ip, Lp), tmp2 = sub(Lp, ip);  // light_v, raytracer.c:62-99
+        const float ld2 = dot(tmp, tmp);
+        int V;
+        if (batched) {
+            V = (int)((vis >> j) & 1u);
+        } else if (dot(tmp2, n) < 0) {
+            V = 0;
+            c.skip++;
+        } else {
+            c.shad++;
+            V = visible<STRICT, COUNT, REG>(s, ip, l, ld2, stk, c) ? 1 : 0;
+        }
+        const float fV = (float)V;
+        col.x = col.x + fV * kl.x * cr.x / mg;
+        col.y = col.y + fV * kl.y * cr.y / mg;
+        col.z = col.z + fV * kl.z * cr.z / mg;
+    }
+    const v3 dd = mul(v, -1.0f);  // raytracer.c:163-166
+    const v3 ns = mul(n, 2.0f * __builtin_fabsf(dot(dd, n)));
+    const v3 r = normalize(add(dd, ns));
+    set3<MAXB>(cols, it, col);
+    seti<MAXB>(mats, it, m);
+    if (!(mag(kr) > 0.0f)) {  // raytracer.c:168
+        L = it + 1;
+        tail = false;
+        return true;
+    }
+    if (it + 1 == bounces) {  // raytrace(.., BOUNCES) returns {0,0,0}: col += kr * 0
+        L = it + 1;
+        tail = true;
+        return true;
+    }
+    o = ip;
+    d = r;
+    return false;
+}
+
+// fold: R_i = c_i + kr_i * R_{i+1}, deepest level first (raytracer.c:169-172)
+template <int MAXB>
+__device__ __forceinline__ v3 fold_path(const DScene& s, const v3 (&cols)[MAXB], const int (&mats)[MAXB], int L,
+                                        bool tail) {
     v3 acc = mk(0.0f, 0.0f, 0.0f);
     bool have = false;
 #pragma unroll
@@ -583,6 +723,23 @@ __device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, in
         }
     }
     return acc;
+}
+
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true>
+__device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0) {
+    v3 o = mk(A.pos[0], A.pos[1], A.pos[2]);
+    v3 cols[MAXB];
+    int mats[MAXB];
+#pragma unroll
+    for (int k = 0; k < MAXB; k++) {
+        cols[k] = mk(0.0f, 0.0f, 0.0f);
+        mats[k] = 0;
+    }
+    int L = 0;
+    bool tail = false;
+    for (int it = 0; it < A.bounces; ++it)
+        if (path_step<MAXB, STRICT, COUNT, REG>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0, stk, c)) break;
+    return fold_path<MAXB>(A.s, cols, mats, L, tail);
 }
 
 __device__ __forceinline__ v3 clamp01(v3 c) {  // vec_constrain(col, 0, 1), vec.c:47-54
@@ -652,9 +809,10 @@ __global__ __launch_bounds__(BLOCK) void k_tiles(KArgs A) {
 // (one returning atomic per wave per tile; microarch row "dequeue"). Tiles are dealt in row-major
 // order of 8x8 blocks so that concurrently running waves trace neighbouring pixels (shared L1/L2
 // lines for the upper BVH levels).
-// OCC: waves per SIMD the register allocation must allow (0 = compiler's choice); 4 caps VGPRs at 128
-// (the LDS stack allows 4 workgroups per CU).
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int OCC = 0>
+// OCC: waves per SIMD the register allocation must allow: 3 caps VGPRs at 168 (512 / 3 in 8-register
+// granules; one register more halves nothing but drops a whole wave per SIMD), 4 at 128 (the LDS
+// stack allows 4 workgroups per CU).
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int OCC = 3, bool TRACE = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(OCC > 0 ? OCC : 1)))
 void k_persist(KArgs A) {
     __shared__ int lds[STACK * BLOCK];
@@ -666,9 +824,105 @@ void k_persist(KArgs A) {
         if (lane == 0) tile = atomicAdd(A.work, 1u);
         tile = __shfl(tile, 0, 64);
         if (tile >= (unsigned)A.n_tiles) break;
+        if (A.tile_order) tile = (unsigned)A.tile_order[tile];
         const int tx = (int)(tile % (unsigned)A.tiles_x), ty = (int)(tile / (unsigned)A.tiles_x);
         const int x = tx * 8 + (lane & 7), k = ty * 8 + (lane >> 3);
+        unsigned long long t0 = 0;
+        const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
+        if (TRACE) t0 = __builtin_amdgcn_s_memrealtime();
         if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT, REG>(A, x, k, stk, c);
+        if (TRACE) {  // {begin, end, wave | fallbacks << 32, wave steps | lane node visits << 32} (COUNT)
+            const unsigned fb = wave_sum(c.fb - fb0), ws = wave_sum(c.ws - ws0), nv = wave_sum(c.chi + c.shi - nd0);
+            if (lane == 0) {
+                A.tile_trace[4 * tile] = t0;
+                A.tile_trace[4 * tile + 1] = __builtin_amdgcn_s_memrealtime();
+                A.tile_trace[4 * tile + 2] = (blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6)) | ((unsigned long long)fb << 32);
+                A.tile_trace[4 * tile + 3] = ws | ((unsigned long long)nv << 32);
+            }
+        }
+    }
+    flush<COUNT>(c, A.counters);
+}
+
+}  // namespace rtd
+
+namespace rtd {
+
+// Path regeneration: persistent waves, one lane = one pixel path as in k_persist, but a lane whose path
+// ends takes the next pixel at once, from a wave-local pool filled one 8x8 tile at a time (one atomic
+// per tile), instead of idling until the whole tile's deepest path is done. Primary and reflection rays
+// run the same closest-hit code, so lanes at different bounce levels still traverse in lockstep.
+// Per-pixel arithmetic is path_step/fold_path's: results are k_persist's bit for bit. spp == 1 only.
+template <int MAXB, bool COUNT>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(3))) void k_regen(KArgs A) {
+    __shared__ int lds[STACK * BLOCK];
+    int* stk = lds + threadIdx.x;
+    const unsigned lane = threadIdx.x & 63u;
+    Ctr c = {};
+    int px = -1, pk = 0, it = 0, L = 0, hit0 = -1;
+    bool tail = false;
+    float t0 = FMAX;
+    v3 o = mk(0.0f, 0.0f, 0.0f), d = o;
+    v3 cols[MAXB];
+    int mats[MAXB];
+#pragma unroll
+    for (int q = 0; q < MAXB; q++) {
+        cols[q] = o;
+        mats[q] = 0;
+    }
+    unsigned tile = 0, nxt = 64;  // wave-uniform pixel pool: the 64 slots of `tile`, next unassigned slot
+    bool drained = false;
+    for (;;) {
+        // ---- give every idle lane the next pixel of the pool
+        for (;;) {
+            const unsigned long long need = __ballot(px < 0);
+            if (!need || drained) break;
+            if (nxt >= 64u) {
+                unsigned t = 0;
+                if (lane == 0) t = atomicAdd(A.work, 1u);
+                t = __shfl(t, 0, 64);
+                if (t >= (unsigned)A.n_tiles) {
+                    drained = true;
+                    break;
+                }
+                tile = t;
+                nxt = 0;
+            }
+            const unsigned take = min((unsigned)__popcll(need), 64u - nxt);
+            const unsigned rank = (unsigned)__popcll(need & ((1ull << lane) - 1ull));
+            if (px < 0 && rank < take) {
+                const unsigned q = nxt + rank;
+                const int x = (int)(tile % (unsigned)A.tiles_x) * 8 + (int)(q & 7u);
+                const int k = (int)(tile / (unsigned)A.tiles_x) * 8 + (int)(q >> 3);
+                if (x < A.W && k < A.n_rows) {  // slots outside the frame stay idle and refill again
+                    px = x;
+                    pk = k;
+                    it = 0;
+                    o = mk(A.pos[0], A.pos[1], A.pos[2]);
+                    d = primary_dir(A, (float)x, (float)(A.row_offset + k * A.row_stride));
+                }
+            }
+            nxt += take;
+        }
+        if (!__ballot(px >= 0)) break;
+        // ---- one bounce level of every busy lane's path
+        if (px >= 0) {
+            if (path_step<MAXB, false, COUNT, true>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0, stk, c)) {
+                const v3 col = clamp01(fold_path<MAXB>(A.s, cols, mats, L, tail));
+                const size_t w = (size_t)pk * A.W + px;
+                c.pix++;
+                if (A.rgb) {
+                    A.rgb[3 * w] = col.x;
+                    A.rgb[3 * w + 1] = col.y;
+                    A.rgb[3 * w + 2] = col.z;
+                }
+                if (A.hit) A.hit[w] = hit0;
+                if (A.t) A.t[w] = t0;
+                px = -1;
+            } else {
+                ++it;
+            }
+        }
     }
     flush<COUNT>(c, A.counters);
 }

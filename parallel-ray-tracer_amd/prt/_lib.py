@@ -61,7 +61,7 @@ class Frame(ctypes.Structure):
 
 
 STAT_FIELDS = ["primary", "reflection", "shadow", "shadow_skipped", "hits", "ch_inner", "ch_leaf",
-               "ch_tri", "sh_inner", "sh_leaf", "sh_tri", "pixels", "fallbacks", "stack_overflows", "node_bytes"]
+               "ch_tri", "sh_inner", "sh_leaf", "sh_tri", "pixels", "fallbacks", "stack_overflows", "node_bytes", "wave_steps"]
 
 
 class WbvhInfo(ctypes.Structure):
@@ -70,7 +70,7 @@ class WbvhInfo(ctypes.Structure):
 
 
 class Stats(ctypes.Structure):
-    _fields_ = [(f, ctypes.c_ulonglong) for f in STAT_FIELDS] + [("reserved", ctypes.c_ulonglong * 1)]
+    _fields_ = [(f, ctypes.c_ulonglong) for f in STAT_FIELDS]
 
 
 _host = None

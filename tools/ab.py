@@ -43,6 +43,7 @@ def main():
                 os.environ[k] = val
         return parts[0]
 
+    ref, same = None, {}
     for rnd in range(a.rounds + 1):
         for v in a.variants:
             kern = setenv(v)
@@ -54,12 +55,20 @@ def main():
             st = r.stats()
             rays[v] = st["rays"]
             pixels[v] = st["pixels"]
+            if rnd == 0:  # every variant must render the first variant's frame bit for bit
+                frame = rgb.view(torch.int32).clone()
+                if ref is None:
+                    ref = frame
+                else:
+                    same[v] = bool(torch.equal(frame, ref))
     out = {}
     for v in a.variants:
         t = sorted(res[v])
         med = t[len(t) // 2]
-        out[v] = {"median_ms": med, "min_ms": t[0], "Mrays_s": rays[v] / med / 1e3, "rays": rays[v]}
-        print(f"{v:40s} median {med:8.3f} ms  min {t[0]:8.3f} ms  {rays[v] / med / 1e3:9.1f} Mrays/s  rays {rays[v]} px {pixels[v]}")
+        out[v] = {"median_ms": med, "min_ms": t[0], "Mrays_s": rays[v] / med / 1e3, "rays": rays[v],
+                  "bit_exact_vs_first": same.get(v, True)}
+        print(f"{v:40s} median {med:8.3f} ms  min {t[0]:8.3f} ms  {rays[v] / med / 1e3:9.1f} Mrays/s  rays {rays[v]} "
+              f"px {pixels[v]}  same={same.get(v, True)}")
     print(json.dumps({"scene": a.scene, "W": a.W, "H": a.H, "results": out}))
 
 

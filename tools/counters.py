@@ -26,6 +26,8 @@ for k in sys.argv[2:] or ["fast", "wavefront", "strict"]:
     st["ch_tri_per_ray"] = st["ch_tri"] / cl
     st["sh_inner_per_ray"] = st["sh_inner"] / max(1, st["shadow"])
     st["sh_tri_per_ray"] = st["sh_tri"] / max(1, st["shadow"])
+    if st.get("wave_steps"):
+        st["simd_eff_nodes"] = (st["ch_inner"] + st["sh_inner"]) / (64 * st["wave_steps"])
     out[k] = st
     print(k, {a: round(b, 2) if isinstance(b, float) else b for a, b in st.items()})
     r.close()

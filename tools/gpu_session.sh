@@ -50,6 +50,25 @@ for s in "${@:-smoke pytest bench}"; do
                   run abnew$i 300 python tools/ab.py --rounds 3 --frames 5 fast
                   PRT_LIB_DIR=build/old/lib run abold$i 300 python tools/ab.py --rounds 3 --frames 5 fast
               done ;;
+      abheadcar) for i in 1 2; do
+                  run abnewcar$i 300 python tools/ab.py --scene car_boxed --rounds 3 --frames 5 fast
+                  PRT_LIB_DIR=build/old/lib run aboldcar$i 300 python tools/ab.py --scene car_boxed --rounds 3 --frames 5 fast
+              done ;;
+      tiles)  run tiles 300 python tools/tile_trace.py
+              run tilescar 300 python tools/tile_trace.py --scene car_boxed ;;
+      tilesc) run tilesc 300 python tools/tile_trace.py --counters ;;
+      abregen) run abregen 300 python tools/ab.py --rounds 4 --frames 5 fast fast:PRT_REGEN=1
+              run abregencar 300 python tools/ab.py --scene car_boxed --rounds 4 --frames 5 fast fast:PRT_REGEN=1
+              run abregensc 300 python tools/ab.py --scene sportscar --rounds 2 --frames 5 fast fast:PRT_REGEN=1 ;;
+      aborder) run aborder 300 python tools/ab.py --rounds 4 --frames 5 fast fast:PRT_TILE_ORDER=center
+              run abordercar 300 python tools/ab.py --scene car_boxed --rounds 4 --frames 5 fast fast:PRT_TILE_ORDER=center
+              run aborderrand 300 python tools/ab.py --scene sportscar --rounds 3 --frames 5 fast fast:PRT_TILE_ORDER=center ;;
+      ab3)    for i in 1 2; do
+                  run ab3new$i 300 python tools/ab.py --rounds 3 --frames 5 fast fast:PRT_TILE_ORDER=rows
+                  PRT_LIB_DIR=build/old/lib run ab3old$i 300 python tools/ab.py --rounds 3 --frames 5 fast
+                  run ab3newcar$i 300 python tools/ab.py --scene car_boxed --rounds 3 --frames 5 fast fast:PRT_TILE_ORDER=rows
+                  PRT_LIB_DIR=build/old/lib run ab3oldcar$i 300 python tools/ab.py --scene car_boxed --rounds 3 --frames 5 fast
+              done ;;
       *) echo "unknown step $step"; exit 2 ;;
     esac
   done
