@@ -281,12 +281,18 @@ __device__ __forceinline__ float ubyte(unsigned w, int b) { return (float)((w >>
 
 // Tests the 8 children of wide node `node`: nh = hit interior slots as bits (s ^ oct), th = triangle
 // bits (relative to tbase) of every hit leaf slot.
-template <bool COUNT>
-__device__ __forceinline__ void wide_node(const DWide& W, int node, const RayPre& p, unsigned oct, float lim,
-                                          unsigned& nh, unsigned& th, int& cbase, int& tbase, unsigned& imask,
-                                          unsigned& nleaf) {
+struct WNode {
+    float4 f0, f1, f2, f3, f4;
+};
+__device__ __forceinline__ WNode wload(const DWide& W, int node) {
     const float4* N = W.nodes + 5 * node;
-    const float4 f0 = N[0], f1 = N[1], f2 = N[2], f3 = N[3], f4 = N[4];
+    return WNode{N[0], N[1], N[2], N[3], N[4]};
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsigned oct, float lim, unsigned& nh,
+                                          unsigned& th, int& cbase, int& tbase, unsigned& imask, unsigned& nleaf) {
+    const float4 f0 = nd.f0, f1 = nd.f1, f2 = nd.f2, f3 = nd.f3, f4 = nd.f4;
     const unsigned e = __float_as_uint(f0.w);
     const float sx = __uint_as_float((e & 0xFFu) << 23), sy = __uint_as_float(((e >> 8) & 0xFFu) << 23),
                 sz = __uint_as_float(((e >> 16) & 0xFFu) << 23);
@@ -333,22 +339,50 @@ __device__ __forceinline__ void wide_node(const DWide& W, int node, const RayPre
     }
 }
 
+// The node visited after this one: the nearest remaining hit child of this node, else the top group
+// of the stack (pushing / re-pushing the rest). It does not depend on this node's triangle tests, so
+// the walks issue its loads BEFORE those tests and their latency overlaps them. -1: walk done; -2: stack
+// overflow (reported, never silent).
+__device__ __forceinline__ int wide_next(unsigned nh, int cb, unsigned imask, unsigned oct, int& sp,
+                                         int* __restrict__ stk) {
+    if (!nh) {
+        if (sp == 0) return -1;
+        --sp;
+        cb = stk[(2 * sp) * BLOCK];
+        const unsigned bits = (unsigned)stk[(2 * sp + 1) * BLOCK];
+        imask = bits >> 8;
+        nh = bits & 0xFFu;
+    }
+    const unsigned slot = (unsigned)__builtin_ctz(nh) ^ oct;
+    nh &= nh - 1u;
+    if (nh) {
+        if (sp >= WSTACK) return -2;
+        stk[(2 * sp) * BLOCK] = cb;
+        stk[(2 * sp + 1) * BLOCK] = (int)((imask << 8) | nh);
+        ++sp;
+    }
+    return cb + __popc(imask & ((1u << slot) - 1u));
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& best, int& hp, int& nd, bool& tie,
                                              int* __restrict__ stk, Ctr& c) {
     const RayPre p = ray_pre(o, d);
     const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
-    int node = 0, sp = 0;
+    int sp = 0;
+    WNode N = wload(W, 0);
     for (;;) {
         unsigned nh, th, imask, nl;
         int cb, tb;
-        wide_node<COUNT>(W, node, p, oct, best * PRUNE_SLACK, nh, th, cb, tb, imask, nl);
+        wide_node<COUNT>(N, p, oct, best * PRUNE_SLACK, nh, th, cb, tb, imask, nl);
         if (COUNT) {
             c.chi++;
             c.chl += nl;
             c.nb += 10;
             c.ws += first_active_lane();
         }
+        const int next = wide_next(nh, cb, imask, oct, sp, stk);
+        if (next >= 0) N = wload(W, next);
         while (th) {
             const int i = tb + __builtin_ctz(th);
             th &= th - 1u;
@@ -364,26 +398,10 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
                 tie = true;
             }
         }
-        if (!nh) {
-            if (sp == 0) break;
-            --sp;
-            cb = stk[(2 * sp) * BLOCK];
-            const unsigned bits = (unsigned)stk[(2 * sp + 1) * BLOCK];
-            imask = bits >> 8;
-            nh = bits & 0xFFu;
+        if (next < 0) {
+            if (next == -2) c.err++;
+            break;
         }
-        const unsigned slot = (unsigned)__builtin_ctz(nh) ^ oct;
-        nh &= nh - 1u;
-        if (nh) {
-            if (sp >= WSTACK) {  // deeper than the builder allows: reported, never silent
-                c.err++;
-                break;
-            }
-            stk[(2 * sp) * BLOCK] = cb;
-            stk[(2 * sp + 1) * BLOCK] = (int)((imask << 8) | nh);
-            ++sp;
-        }
-        node = cb + __popc(imask & ((1u << slot) - 1u));
     }
 }
 
@@ -393,17 +411,20 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
     const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
     float best = FMAX;
     const float reach = shadow_reach(o, ld2);
-    int node = 0, sp = 0;
+    int sp = 0;
+    WNode N = wload(W, 0);
     for (;;) {
         unsigned nh, th, imask, nl;
         int cb, tb;
-        wide_node<COUNT>(W, node, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nl);
+        wide_node<COUNT>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nl);
         if (COUNT) {
             c.shi++;
             c.shl += nl;
             c.nb += 10;
             c.ws += first_active_lane();
         }
+        const int next = wide_next(nh, cb, imask, oct, sp, stk);
+        if (next >= 0) N = wload(W, next);
         while (th) {
             const int i = tb + __builtin_ctz(th);
             th &= th - 1u;
@@ -417,129 +438,12 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
                 if (ld2 > dot(oi, oi)) return false;
             }
         }
-        if (!nh) {
-            if (sp == 0) break;
-            --sp;
-            cb = stk[(2 * sp) * BLOCK];
-            const unsigned bits = (unsigned)stk[(2 * sp + 1) * BLOCK];
-            imask = bits >> 8;
-            nh = bits & 0xFFu;
+        if (next < 0) {
+            if (next == -2) c.err++;
+            break;
         }
-        const unsigned slot = (unsigned)__builtin_ctz(nh) ^ oct;
-        nh &= nh - 1u;
-        if (nh) {
-            if (sp >= WSTACK) {
-                c.err++;
-                break;
-            }
-            stk[(2 * sp) * BLOCK] = cb;
-            stk[(2 * sp + 1) * BLOCK] = (int)((imask << 8) | nh);
-            ++sp;
-        }
-        node = cb + __popc(imask & ((1u << slot) - 1u));
     }
     return true;
-}
-
-// Shadow rays of all lights of one shading point in ONE traversal loop: a lane whose ray finishes
-// (occluded, or its stack empties) starts its next light's ray at once, so a wave runs max over lanes of
-// the SUM of their shadow walks instead of the sum over lights of the max. Bit j of `need`: light j needs
-// a shadow ray (j < 32); returns the visible ones. Each ray is visible_wide's walk exactly (same
-// direction, ld2 and pruning), so the visibility bits are the reference's.
-template <bool COUNT>
-__device__ __forceinline__ unsigned visible_wide_multi(const DScene& s, v3 ip, unsigned need, int* __restrict__ stk,
-                                                       Ctr& c) {
-    const DWide& W = s.wide;
-    unsigned vis = 0;
-    int j = 0, node = 0, sp = 0;
-    float best = FMAX, reach = FMAX;
-    v3 d = ip;
-    RayPre p = {};
-    unsigned oct = 0;
-    bool act = false;
-    auto start = [&]() {
-        act = need != 0u;
-        if (!act) return;
-        j = __builtin_ctz(need);
-        need &= need - 1u;
-        const v3 Lp = xyz(s.lights[2 * j]);
-        v3 l = sub(Lp, ip);  // raytracer.c:150-153 (same ops as path_step)
-        const float mg = mag(l);
-        l = dvs(l, mg);
-        const v3 tmp = sub(ip, Lp);
-        const float ld2 = dot(tmp, tmp);
-        d = l;
-        p = ray_pre(ip, d);
-        oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
-        best = FMAX;
-        reach = shadow_reach(ip, ld2);
-        node = 0;
-        sp = 0;
-    };
-    start();
-    while (act) {
-        unsigned nh, th, imask, nl;
-        int cb, tb;
-        wide_node<COUNT>(W, node, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nl);
-        if (COUNT) {
-            c.shi++;
-            c.shl += nl;
-            c.nb += 10;
-            c.ws += first_active_lane();
-        }
-        bool occluded = false;
-        if (th) {
-            const v3 Lp = xyz(s.lights[2 * j]);
-            const v3 tmp = sub(ip, Lp);
-            const float ld2 = dot(tmp, tmp);
-            while (th) {
-                const int i = tb + __builtin_ctz(th);
-                th &= th - 1u;
-                int k;
-                const float tt = hit_triangle(ip, d, W.tris + 3 * i, k);
-                if (COUNT) c.sht++;
-                if (tt < best) {
-                    best = tt;
-                    const v3 q = add(ip, mul(d, best));
-                    const v3 oi = sub(ip, q);
-                    if (ld2 > dot(oi, oi)) {
-                        occluded = true;
-                        break;
-                    }
-                }
-            }
-        }
-        if (occluded) {
-            start();
-            continue;
-        }
-        if (!nh) {
-            if (sp == 0) {  // walked everything up to the light: visible
-                vis |= 1u << j;
-                start();
-                continue;
-            }
-            --sp;
-            cb = stk[(2 * sp) * BLOCK];
-            const unsigned bits = (unsigned)stk[(2 * sp + 1) * BLOCK];
-            imask = bits >> 8;
-            nh = bits & 0xFFu;
-        }
-        const unsigned slot = (unsigned)__builtin_ctz(nh) ^ oct;
-        nh &= nh - 1u;
-        if (nh) {
-            if (sp >= WSTACK) {
-                c.err++;
-                start();
-                continue;
-            }
-            stk[(2 * sp) * BLOCK] = cb;
-            stk[(2 * sp + 1) * BLOCK] = (int)((imask << 8) | nh);
-            ++sp;
-        }
-        node = cb + __popc(imask & ((1u << slot) - 1u));
-    }
-    return vis;
 }
 
 // Closest hit with the kernel's policy; returns the ORIGINAL triangle index (-1 = miss).
@@ -625,33 +529,6 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
     const v3 ks = xyz(s.mats[3 * m]), kd = xyz(s.mats[3 * m + 1]), kr = xyz(s.mats[3 * m + 2]);
     v3 col = mk(0.0f + kd.x * amb.x, 0.0f + kd.y * amb.y, 0.0f + kd.z * amb.z);  // :144-146
     const v3 v = mul(d, -1.0f);                                                      // :147
-    // fast walk over the wide view: visibility of every light first (one batched walk), then the
-    // reference's per-light accumulation in light order with those bits
-    const bool batched = !STRICT && s.wide.nodes != nullptr && s.n_lights <= 32;
-    unsigned vis = 0;
-    if (batched) {
-        unsigned need = 0;
-        for (int j = 0; j < s.n_lights; ++j) {
-            const v3 Lp = xyz(s.lights[2 * j]);
-            const v3 tmp2 = sub(Lp, ip);
-            if (dot(tmp2, n) < 0) {  // light_v's back-face early-out, raytracer.c:66-67
-                c.skip++;
-                continue;
-            }
-            c.shad++;
-            v3 l = sub(Lp, ip);
-            const float mg = mag(l);
-            l = dvs(l, mg);
-            if (degenerate(l)) {  // NaN-slab semantics: the strict walk of the reference BVH
-                const v3 tmp = sub(ip, Lp);
-                c.fb++;
-                if (visible_walk<true, COUNT, REG>(s.ref, ip, l, dot(tmp, tmp), stk, c)) vis |= 1u << j;
-            } else {
-                need |= 1u << j;
-            }
-        }
-        vis |= visible_wide_multi<COUNT>(s, ip, need, stk, c);
-    }
     for (int j = 0; j < s.n_lights; ++j) {                                           // :149-160
         const v3 Lp = xyz(s.lights[2 * j]), kl = xyz(s.lights[2 * j + 1]);
         v3 l = sub(Lp, ip);
@@ -666,9 +543,7 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
         const v3 tmp = sub(ip, Lp), tmp2 = sub(Lp, ip);  // light_v, raytracer.c:62-99
         const float ld2 = dot(tmp, tmp);
         int V;
-        if (batched) {
-            V = (int)((vis >> j) & 1u);
-        } else if (dot(tmp2, n) < 0) {
+        if (dot(tmp2, n) < 0) {
             V = 0;
             c.skip++;
         } else {

@@ -69,6 +69,15 @@ for s in "${@:-smoke pytest bench}"; do
                   run ab3newcar$i 300 python tools/ab.py --scene car_boxed --rounds 3 --frames 5 fast fast:PRT_TILE_ORDER=rows
                   PRT_LIB_DIR=build/old/lib run ab3oldcar$i 300 python tools/ab.py --scene car_boxed --rounds 3 --frames 5 fast
               done ;;
+      abbatch) run abbatch 300 python tools/ab.py --rounds 4 --frames 5 fast fast:PRT_SHADOW_BATCH=0
+              run abbatchcar 300 python tools/ab.py --scene car_boxed --rounds 4 --frames 5 fast fast:PRT_SHADOW_BATCH=0
+              run abbatchsc 300 python tools/ab.py --scene sportscar --rounds 3 --frames 5 fast fast:PRT_SHADOW_BATCH=0 ;;
+      abpf)   for i in 1 2; do
+                  run abpfnew$i 300 python tools/ab.py --rounds 3 --frames 5 fast
+                  PRT_LIB_DIR=build/old/lib run abpfold$i 300 python tools/ab.py --rounds 3 --frames 5 fast:PRT_SHADOW_BATCH=0
+                  run abpfnewcar$i 300 python tools/ab.py --scene car_boxed --rounds 3 --frames 5 fast
+                  PRT_LIB_DIR=build/old/lib run abpfoldcar$i 300 python tools/ab.py --scene car_boxed --rounds 3 --frames 5 fast:PRT_SHADOW_BATCH=0
+              done ;;
       *) echo "unknown step $step"; exit 2 ;;
     esac
   done
