@@ -51,8 +51,8 @@ def cpu_baseline(scene_files, W, H, gpu_rays_for_rows, args):
     if os.path.exists(ref) and os.access(ref, os.X_OK):
         kind = "reference"
 
-        def run(rows_stride, reps):
-            out = subprocess.run([ref, "time", obj, mtl, lts, str(W), str(H), str(threads), "0", str(rows_stride),
+        def run(rows_stride, reps, nthreads=threads):
+            out = subprocess.run([ref, "time", obj, mtl, lts, str(W), str(H), str(nthreads), "0", str(rows_stride),
                                   str(reps)], check=True, capture_output=True, text=True, timeout=600)
             return json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     else:
@@ -62,15 +62,15 @@ def cpu_baseline(scene_files, W, H, gpu_rays_for_rows, args):
         o = OracleScene.load(obj, mtl, lts, flavour="fast")
         o.build_bvh(3)
 
-        def run(rows_stride, reps):
+        def run(rows_stride, reps, nthreads=threads):
             nr = (H + rows_stride - 1) // rows_stride
             ts = []
             for _ in range(reps):
                 t0 = time.perf_counter()
-                o.render(W, H, rows=(0, rows_stride, nr), threads=threads)
+                o.render(W, H, rows=(0, rows_stride, nr), threads=nthreads)
                 ts.append((time.perf_counter() - t0) * 1e3)
             ts.sort()
-            return {"median_ms": ts[len(ts) // 2], "rows": nr, "threads": threads, "reps": reps}
+            return {"median_ms": ts[len(ts) // 2], "rows": nr, "threads": nthreads, "reps": reps}
     if not stride:  # calibrate: aim at ~15 s of CPU work in total
         probe = run(16, 1)
         frame_s = probe["median_ms"] / 1e3 * 16
@@ -80,10 +80,19 @@ def cpu_baseline(scene_files, W, H, gpu_rays_for_rows, args):
         reps = args.cpu_reps
     res = run(stride, reps)
     rays = gpu_rays_for_rows(stride)
-    return {"value": rays / (res["median_ms"] / 1e3) / 1e6, "unit": "Mrays/s", "cores": threads, "kind": kind,
-            "sample": f"rows y = k*{stride} of the same {W}x{H} frame ({res['rows']} rows, {rays} rays), "
-                      f"median of {reps} frames, {threads} pthreads, reference atomic row scheduler, "
-                      f"heuristic-3 BVH (build untimed)"}
+    out = {"value": rays / (res["median_ms"] / 1e3) / 1e6, "unit": "Mrays/s", "cores": threads, "kind": kind,
+           "sample": f"rows y = k*{stride} of the same {W}x{H} frame ({res['rows']} rows, {rays} rays), "
+                     f"median of {reps} frames, {threads} pthreads, reference atomic row scheduler, "
+                     f"heuristic-3 BVH (build untimed)"}
+    # the same at 1 thread, on a ~5 s sample (every stride1-th row, one frame)
+    if threads > 1 and not args.no_single_thread:
+        frame_1t = res["median_ms"] / 1e3 * stride * threads
+        stride1 = max(1, min(H, int(math.ceil(frame_1t / 5.0))))
+        r1 = run(stride1, 1, 1)
+        rays1 = gpu_rays_for_rows(stride1)
+        out["single_thread"] = {"value": rays1 / (r1["median_ms"] / 1e3) / 1e6, "unit": "Mrays/s", "cores": 1,
+                                "sample": f"rows y = k*{stride1} ({r1['rows']} rows, {rays1} rays), one frame"}
+    return out
 
 
 def main():
@@ -98,6 +107,7 @@ def main():
     ap.add_argument("--spp", type=int, default=1)
     ap.add_argument("--bvh", default="random", help="bvh_build heuristic handed over (reference default: 3 = random)")
     ap.add_argument("--accel", default="auto", help="auto: the library builds a binned-SAH BVH for the fast walk")
+    ap.add_argument("--no-single-thread", action="store_true", help="skip the 1-thread CPU baseline sample")
     ap.add_argument("--kernel", default="fast")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)

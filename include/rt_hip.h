@@ -18,6 +18,8 @@
 #ifndef RT_HIP_H
 #define RT_HIP_H
 
+#include <stddef.h>
+
 #include "rt_types.h"
 
 #ifdef __cplusplus
@@ -79,11 +81,14 @@ typedef struct rt_frame {
 
 /* Device output pointers (all nullable). rgb: [n_rows][width][3] f32 in [0,1] = vec_t pixels
  * (main.c:39); NULL -> a buffer owned by the context (read it with rt_download).
- * hit: [n_rows][width] int32 primary closest-hit triangle index (-1 = miss); t: its distance. */
+ * hit: [n_rows][width] int32 primary closest-hit triangle index (-1 = miss); t: its distance.
+ * bounce_hit: [n_rows][width][bounces] int32 closest-hit triangle index of every recursion level
+ * (raytrace(.., iter), raytracer.c:101-135): -1 = miss, -2 = level not reached (first sample when spp > 1). */
 typedef struct rt_outputs {
     float* rgb;
     int* hit;
     float* t;
+    int* bounce_hit;
 } rt_outputs;
 
 typedef struct rt_stats {
@@ -117,6 +122,17 @@ int rt_sync(rt_ctx* ctx, float* kernel_ms);
 /* per-launch kernel times (HIP events recorded on the context stream around each kernel) of the last
  * n launches (n <= 64), oldest first; synchronises; returns the number written or < 0 */
 int rt_kernel_times(rt_ctx* ctx, float* ms, int n);
+/* Multi-GPU in one process (the CLI's --gpus N): gathers the last frames of n contexts into ctxs[root]'s
+ * device frame. Every context must have rendered the same width x height, and their row sets must
+ * partition the frame (rank g of n: row_offset = g, row_stride = n, SURVEY §8e cyclic rows). Peer copies
+ * over xGMI are ordered on the root's stream after each source's last render (events); the rows are
+ * un-interleaved on the root. Afterwards the root's last frame is the full frame (rgb, and hit when every
+ * context wrote one): rt_download / rt_download_bmp read it. Asynchronous like rt_render. */
+int rt_gather(rt_ctx* const* ctxs, int n, int root);
+/* bmp_write_file's bytes of the last frame (cpu/src/bmp_writer.c:88-211): 54-B header + BGRA8 rows
+ * bottom-up, (uint8_t)(c * 255.0f) per channel (vec_to_bgra), quantised on the device. Needs a full
+ * frame (all rows; after rt_gather for multi-GPU). cap >= 54 + 4 * width * height; synchronous. */
+int rt_download_bmp(rt_ctx* ctx, unsigned char* h_bmp, size_t cap);
 /* counters of the last rendered frame (synchronises) */
 int rt_get_stats(rt_ctx* ctx, rt_stats* stats);
 const char* rt_last_error(rt_ctx* ctx);

@@ -77,6 +77,8 @@ int rth_camera(int width, int height, rt_camera* out);
 int rth_bmp_write(const float* rgb, int width, int height, const char* path);
 /* the same conversion into a caller buffer of 54 + 4*width*height bytes */
 int rth_bmp_encode(const float* rgb, int width, int height, uint8_t* out, size_t cap);
+/* its 54-byte header alone (bmp_writer.c:97-120) */
+int rth_bmp_header(int width, int height, uint8_t out[54]);
 
 void rth_free(void* p);
 

@@ -151,9 +151,8 @@ int main(int argc, char** argv) {
         return EXIT_FAILURE;
     }
     std::vector<float> frame((size_t)a.W * a.H * 3);
-    std::vector<std::vector<float>> part(G);
     unsigned long long rays = 0;
-    auto render_all = [&](bool keep) {
+    auto render_all = [&]() {
         std::vector<std::thread> th;
         std::vector<int> status(G, 0);
         for (int g = 0; g < G; g++)
@@ -161,12 +160,7 @@ int main(int argc, char** argv) {
                 int nr = (a.H - g + G - 1) / G;
                 rt_frame f{a.W, a.H, g, G, nr, a.bounces, a.spp, kern};
                 int s = rt_render(ctx[g], &cam, &f, nullptr);
-                if (s == RT_OK && keep) {
-                    part[g].resize((size_t)nr * a.W * 3);
-                    s = rt_download(ctx[g], part[g].data(), nullptr);
-                } else if (s == RT_OK) {
-                    s = rt_sync(ctx[g], nullptr);
-                }
+                if (s == RT_OK) s = rt_sync(ctx[g], nullptr);
                 status[g] = s;
             });
         for (auto& t : th) t.join();
@@ -177,16 +171,15 @@ int main(int argc, char** argv) {
             }
     };
     std::printf("\nRendering...\n");
-    for (int i = 0; i < a.warmup; i++) render_all(false);
+    for (int i = 0; i < a.warmup; i++) render_all();
     std::vector<double> times;
     for (int i = 0; i < a.iterations; i++) {  // main.c:171-185
         auto s = std::chrono::steady_clock::now();
-        render_all(true);
-        for (int g = 0; g < G; g++) {  // cyclic rows -> frame
-            int nr = (a.H - g + G - 1) / G;
-            for (int k = 0; k < nr; k++)
-                std::memcpy(&frame[(size_t)(g + k * G) * a.W * 3], &part[g][(size_t)k * a.W * 3],
-                            sizeof(float) * 3 * a.W);
+        render_all();
+        // cyclic rows of every GPU -> GPU 0's frame (peer copies over xGMI, rt_gather), then to the host
+        if ((G > 1 && rt_gather(ctx.data(), G, 0) != RT_OK) || rt_download(ctx[0], frame.data(), nullptr) != RT_OK) {
+            std::fprintf(stderr, "gather: %s\n", rt_last_error(ctx[0]));
+            return EXIT_FAILURE;
         }
         double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s).count();
         times.push_back(ms);
@@ -198,7 +191,16 @@ int main(int argc, char** argv) {
         rt_get_stats(ctx[g], &st);
         rays += st.primary + st.reflection + st.shadow;
     }
-    if (rth_bmp_write(frame.data(), a.W, a.H, a.out.c_str()) != RT_OK) return -1;  // main.c:191
+    {  // main.c:191 bmp_write_file: quantised on GPU 0 (rt_download_bmp), written by the host
+        std::vector<unsigned char> bmp(54 + (size_t)4 * a.W * a.H);
+        if (rt_download_bmp(ctx[0], bmp.data(), bmp.size()) != RT_OK) {
+            std::fprintf(stderr, "bmp: %s\n", rt_last_error(ctx[0]));
+            return EXIT_FAILURE;
+        }
+        FILE* fo = std::fopen(a.out.c_str(), "wb");
+        if (!fo || std::fwrite(bmp.data(), 1, bmp.size(), fo) != bmp.size()) return -1;
+        std::fclose(fo);
+    }
 
     double mean = 0;  // main.c:193-209
     for (double t : times) mean += t;

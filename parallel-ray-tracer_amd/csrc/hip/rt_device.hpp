@@ -68,12 +68,14 @@ struct KArgs {
     float* rgb;
     int* hit;
     float* t;
+    int* bounce_hit;               // nullable: [n_rows][W][bounces] per-level closest hit (-1 miss, -2 unreached)
     unsigned long long* counters;  // RT_NCOUNT slots (rt_stats order)
     unsigned int* work;            // persistent-kernel tile / pixel counter
     int n_tiles, tiles_x;
     int refill_below;              // k_wave: leave the traversal loop when fewer lanes than this still trace
     unsigned long long* tile_trace;  // diagnostics (PRT_TILE_TRACE): per-tile timeline (rt_kernels.hpp)
     const int* tile_order;           // nullable: k-th dealt tile = tile_order[k] (default: row-major)
+    int prio;                        // k_persist: raise the wave's issue priority with the bounce level
 };
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

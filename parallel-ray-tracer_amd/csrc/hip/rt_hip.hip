@@ -16,6 +16,7 @@
 #include "rt_hip.h"
 #include "rt_host.h"
 #include "rt_kernels.hpp"
+#include "rt_output.hpp"
 #include "rt_wave.hpp"
 #include "rt_wf.hpp"
 
@@ -66,6 +67,15 @@ struct rt_ctx {
     float* last_rgb = nullptr;
     int* last_hit = nullptr;
     size_t last_pixels = 0;
+    int last_W = 0, last_H = 0, last_off = 0, last_stride = 1, last_rows = 0;  // the last frame's rows
+    // output stage (rt_gather, rt_download_bmp)
+    float* d_full = nullptr;
+    int* d_full_hit = nullptr;
+    size_t full_cap = 0, full_hit_cap = 0;
+    char* d_stage = nullptr;
+    size_t stage_cap = 0;
+    unsigned* d_bmp = nullptr;
+    size_t bmp_cap = 0;
     unsigned long long* d_counters = nullptr;  // rtd::NCOUNT
     int* d_order = nullptr;                    // tile dealing order (PRT_TILE_ORDER), for order_tx x order_ty tiles
     int order_tx = 0, order_ty = 0;
@@ -592,13 +602,16 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     A.rgb = rgb;
     A.hit = out ? out->hit : nullptr;
     A.t = out ? out->t : nullptr;
+    A.bounce_hit = out ? out->bounce_hit : nullptr;
+    if (const char* e = std::getenv("PRT_PRIO")) A.prio = std::atoi(e);  // A/B knob
     A.counters = ctx->d_counters;
     A.work = ctx->d_work;
     A.tiles_x = (f->width + 7) / 8;
     A.n_tiles = A.tiles_x * ((f->n_rows + 7) / 8);
     int kernel = f->kernel == RT_KERNEL_AUTO ? RT_KERNEL_FAST : f->kernel;
     // the wavefront pipeline and k_wave render 1 spp; spp > 1 goes to the per-pixel path kernel
-    if ((kernel == RT_KERNEL_WAVEFRONT || kernel == RT_KERNEL_WAVE) && f->spp > 1) kernel = RT_KERNEL_FAST;
+    if ((kernel == RT_KERNEL_WAVEFRONT || kernel == RT_KERNEL_WAVE) && (f->spp > 1 || (out && out->bounce_hit)))
+        kernel = RT_KERNEL_FAST;  // spp > 1 and per-level hit dumps: the fused path kernels
     if ((f->bounces > rtd::WF_MAXB || ctx->n_lights > 32) && kernel == RT_KERNEL_WAVEFRONT) kernel = RT_KERNEL_FAST;
     A.refill_below = kernel == RT_KERNEL_WAVEFRONT ? 48 : 32;  // tuning knob, PRT_REFILL_BELOW overrides (0..64)
     if (const char* e = std::getenv("PRT_REFILL_BELOW")) A.refill_below = std::max(0, std::min(64, std::atoi(e)));
@@ -668,6 +681,11 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     ctx->last_rgb = rgb;
     ctx->last_hit = A.hit;
     ctx->last_pixels = pixels;
+    ctx->last_W = f->width;
+    ctx->last_H = f->height;
+    ctx->last_off = f->row_offset;
+    ctx->last_stride = f->row_stride;
+    ctx->last_rows = f->n_rows;
     ctx->rendered = true;
     return RT_OK;
 }
@@ -716,6 +734,115 @@ extern "C" int rt_download(rt_ctx* ctx, float* h_rgb, int* h_hit) {
     return RT_OK;
 }
 
+namespace {
+template <class T>
+int grow(rt_ctx* ctx, T** p, size_t& cap, size_t n) {
+    if (*p && cap >= n) return RT_OK;
+    if (*p) HIPC(hipFree(*p));
+    *p = nullptr;
+    cap = 0;
+    HIPC(hipMalloc((void**)p, sizeof(T) * std::max<size_t>(n, 1)));
+    cap = n;
+    return RT_OK;
+}
+}  // namespace
+
+extern "C" int rt_gather(rt_ctx* const* ctxs, int n, int root) {
+    if (!ctxs || n <= 0 || root < 0 || root >= n || !ctxs[root]) return RT_E_ARG;
+    rt_ctx* ctx = ctxs[root];
+    const int W = ctx->last_W, H = ctx->last_H;
+    std::vector<char> cover((size_t)std::max(H, 0), 0);
+    bool all_hit = true;
+    size_t stage = 0;
+    for (int i = 0; i < n; i++) {
+        rt_ctx* c = ctxs[i];
+        if (!c || !c->rendered) return arg_err(ctx, "rt_gather: a context has not rendered");
+        if (c->last_W != W || c->last_H != H) return arg_err(ctx, "rt_gather: frame sizes differ");
+        for (int k = 0; k < c->last_rows; k++) {
+            const long long y = c->last_off + (long long)k * c->last_stride;
+            if (y < 0 || y >= H || cover[y]) return arg_err(ctx, "rt_gather: row sets do not partition the frame");
+            cover[y] = 1;
+        }
+        all_hit = all_hit && c->last_hit;
+        if (c->device != ctx->device) stage += (size_t)W * c->last_rows * (3 * sizeof(float) + sizeof(int));
+    }
+    for (char v : cover)
+        if (!v) return arg_err(ctx, "rt_gather: row sets do not cover the frame");
+    HIPC(hipSetDevice(ctx->device));
+    const size_t px = (size_t)W * H;
+    int rc;
+    if ((rc = grow(ctx, &ctx->d_full, ctx->full_cap, 3 * px))) return rc;
+    if (all_hit && (rc = grow(ctx, &ctx->d_full_hit, ctx->full_hit_cap, px))) return rc;
+    if (stage && (rc = grow(ctx, &ctx->d_stage, ctx->stage_cap, stage))) return rc;
+    size_t at = 0;
+    for (int i = 0; i < n; i++) {
+        rt_ctx* c = ctxs[i];
+        const size_t cpx = (size_t)W * c->last_rows;
+        const float* src = c->last_rgb;
+        const int* src_hit = c->last_hit;
+        // after the source's last render (an event on its own stream; cross-device waits are legal)
+        if (c != ctx) HIPC(hipStreamWaitEvent(ctx->stream, c->ev1, 0));
+        if (c->device != ctx->device) {  // peer copy over xGMI into the root's staging area
+            int can = 0;
+            (void)hipDeviceCanAccessPeer(&can, ctx->device, c->device);
+            if (can) {
+                const hipError_t e = hipDeviceEnablePeerAccess(c->device, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return fail(ctx, e, "hipDeviceEnablePeerAccess");
+                (void)hipGetLastError();
+            }
+            float* dst = (float*)(ctx->d_stage + at);
+            HIPC(hipMemcpyPeerAsync(dst, ctx->device, src, c->device, sizeof(float) * 3 * cpx, ctx->stream));
+            at += sizeof(float) * 3 * cpx;
+            int* dst_hit = nullptr;
+            if (all_hit) {
+                dst_hit = (int*)(ctx->d_stage + at);
+                HIPC(hipMemcpyPeerAsync(dst_hit, ctx->device, src_hit, c->device, sizeof(int) * cpx, ctx->stream));
+                at += sizeof(int) * cpx;
+            }
+            src = dst;
+            src_hit = dst_hit;
+        }
+        const int grid = (int)std::max<size_t>(1, std::min<size_t>((cpx + 255) / 256, 4096));
+        rtd::k_unshuffle<<<grid, 256, 0, ctx->stream>>>(src, all_hit ? src_hit : nullptr, ctx->d_full,
+                                                         all_hit ? ctx->d_full_hit : nullptr, W, c->last_off,
+                                                         c->last_stride, c->last_rows);
+        HIPC(hipGetLastError());
+    }
+    HIPC(hipEventRecord(ctx->ev1, ctx->stream));
+    ctx->last_rgb = ctx->d_full;
+    ctx->last_hit = all_hit ? ctx->d_full_hit : nullptr;
+    ctx->last_pixels = px;
+    ctx->last_off = 0;
+    ctx->last_stride = 1;
+    ctx->last_rows = H;
+    return RT_OK;
+}
+
+extern "C" int rt_download_bmp(rt_ctx* ctx, unsigned char* h_bmp, size_t cap) {
+    if (!ctx || !h_bmp) return RT_E_ARG;
+    if (!ctx->rendered) {
+        ctx->err = "rt_download_bmp: nothing rendered";
+        return RT_E_STATE;
+    }
+    const int W = ctx->last_W, H = ctx->last_H;
+    if (ctx->last_off != 0 || ctx->last_stride != 1 || ctx->last_rows != H) {
+        ctx->err = "rt_download_bmp: the last frame is not a full frame (gather it first)";
+        return RT_E_STATE;
+    }
+    const size_t px = (size_t)W * H;
+    if (cap < 54 + 4 * px) return arg_err(ctx, "rt_download_bmp: buffer too small");
+    HIPC(hipSetDevice(ctx->device));
+    int rc;
+    if ((rc = grow(ctx, &ctx->d_bmp, ctx->bmp_cap, px))) return rc;
+    const int grid = (int)std::max<size_t>(1, std::min<size_t>((px + 255) / 256, 4096));
+    rtd::k_bgra<<<grid, 256, 0, ctx->stream>>>(ctx->last_rgb, ctx->d_bmp, W, H);
+    HIPC(hipGetLastError());
+    if (rth_bmp_header(W, H, h_bmp) != RT_OK) return arg_err(ctx, "rt_download_bmp: bad frame size");
+    HIPC(hipMemcpyAsync(h_bmp + 54, ctx->d_bmp, 4 * px, hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
 extern "C" int rt_get_stats(rt_ctx* ctx, rt_stats* st) {
     if (!ctx || !st) return RT_E_ARG;
     HIPC(hipSetDevice(ctx->device));
@@ -757,6 +884,8 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     if (ctx->d_rgb_own) (void)hipFree(ctx->d_rgb_own);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->d_order) (void)hipFree(ctx->d_order);
+    for (void* p : {(void*)ctx->d_full, (void*)ctx->d_full_hit, (void*)ctx->d_stage, (void*)ctx->d_bmp})
+        if (p) (void)hipFree(p);
     if (ctx->d_work) (void)hipFree(ctx->d_work);
     for (int i = 0; i < rt_ctx::NEV; i++) {
         if (ctx->ev0s[i]) (void)hipEventDestroy(ctx->ev0s[i]);

@@ -504,7 +504,7 @@ __device__ __forceinline__ void seti(int (&a)[MAXB], int i, int v) {
 template <int MAXB, bool STRICT, bool COUNT, bool REG>
 __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, v3& o, v3& d, v3 (&cols)[MAXB],
                                           int (&mats)[MAXB], int& L, bool& tail, int& hit0, float& t0,
-                                          int* __restrict__ stk, Ctr& c) {
+                                          int* __restrict__ bh, int bh_pix, int* __restrict__ stk, Ctr& c) {
     const v3 amb = mk(s.amb_x, s.amb_y, s.amb_z);
     float best;
     int nd;
@@ -515,6 +515,7 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
         hit0 = orig;
         t0 = best;
     }
+    if (bh && bh_pix >= 0) bh[(size_t)bh_pix * bounces + it] = orig;  // per-level dump (uniform base, nullable)
     if (orig < 0) {  // raytracer.c:132-135
         set3<MAXB>(cols, it, mk(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z));
         L = it + 1;
@@ -601,7 +602,7 @@ __device__ __forceinline__ v3 fold_path(const DScene& s, const v3 (&cols)[MAXB],
 }
 
 template <int MAXB, bool STRICT, bool COUNT, bool REG = true>
-__device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0) {
+__device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0, int bh_pix) {
     v3 o = mk(A.pos[0], A.pos[1], A.pos[2]);
     v3 cols[MAXB];
     int mats[MAXB];
@@ -612,8 +613,18 @@ __device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, in
     }
     int L = 0;
     bool tail = false;
-    for (int it = 0; it < A.bounces; ++it)
-        if (path_step<MAXB, STRICT, COUNT, REG>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0, stk, c)) break;
+    for (int it = 0; it < A.bounces; ++it) {
+        if (A.prio) {  // wave-uniform: deeper levels belong to the long tiles that end the frame
+            if (it == 0) __builtin_amdgcn_s_setprio(0);
+            else if (it == 1) __builtin_amdgcn_s_setprio(1);
+            else if (it == 2) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(3);
+        }
+        if (path_step<MAXB, STRICT, COUNT, REG>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0, A.bounce_hit,
+                                                bh_pix, stk, c))
+            break;
+    }
+    if (A.prio) __builtin_amdgcn_s_setprio(0);
     return fold_path<MAXB>(A.s, cols, mats, L, tail);
 }
 
@@ -636,8 +647,11 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, int x, int k, int* 
     int hit0 = -1;
     float t0 = FMAX;
     v3 col;
+    if (A.bounce_hit)
+        for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
     if (A.spp <= 1) {
-        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG>(A, primary_dir(A, (float)x, (float)y), stk, c, hit0, t0));
+        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG>(A, primary_dir(A, (float)x, (float)y), stk, c, hit0, t0,
+                                                           (int)o));
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples
         const int g = A.spp_grid;
         v3 acc = mk(0.0f, 0.0f, 0.0f);
@@ -647,7 +661,8 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, int x, int k, int* 
                 const float fy = (float)y + ((float)sj + 0.5f) / (float)g;
                 int h;
                 float tt;
-                const v3 cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG>(A, primary_dir(A, fx, fy), stk, c, h, tt));
+                const v3 cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG>(A, primary_dir(A, fx, fy), stk, c, h, tt,
+                                                                           si == 0 && sj == 0 ? (int)o : -1));
                 acc = add(acc, cs);
                 if (si == 0 && sj == 0) {
                     hit0 = h;
@@ -773,6 +788,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                     px = x;
                     pk = k;
                     it = 0;
+                    if (A.bounce_hit)
+                        for (int i = 0; i < A.bounces; i++) A.bounce_hit[((size_t)k * A.W + x) * A.bounces + i] = -2;
                     o = mk(A.pos[0], A.pos[1], A.pos[2]);
                     d = primary_dir(A, (float)x, (float)(A.row_offset + k * A.row_stride));
                 }
@@ -782,7 +799,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         if (!__ballot(px >= 0)) break;
         // ---- one bounce level of every busy lane's path
         if (px >= 0) {
-            if (path_step<MAXB, false, COUNT, true>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0, stk, c)) {
+            if (path_step<MAXB, false, COUNT, true>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0, A.bounce_hit,
+                                                    pk * A.W + px, stk, c)) {
                 const v3 col = clamp01(fold_path<MAXB>(A.s, cols, mats, L, tail));
                 const size_t w = (size_t)pk * A.W + px;
                 c.pix++;

@@ -537,12 +537,11 @@ extern "C" int rth_camera(int W, int H, rt_camera* out) {
 }
 
 // ------------------------------------------------------------------ BMP (cpu/src/bmp_writer.c)
-extern "C" int rth_bmp_encode(const float* rgb, int W, int H, uint8_t* buf, size_t cap) {
-    if (!rgb || W <= 0 || H <= 0 || !buf) return RT_E_ARG;
+extern "C" int rth_bmp_header(int W, int H, uint8_t* buf) {
+    if (W <= 0 || H <= 0 || !buf) return RT_E_ARG;
     const int row = W * 4, hdr = 14 + 40;
     const size_t fsz = (size_t)hdr + (size_t)row * H;
-    if (cap < fsz) return RT_E_ARG;
-    std::memset(buf, 0, fsz);
+    std::memset(buf, 0, hdr);
     int file_size = (int)fsz, hs = hdr, dib = 40;
     uint16_t planes = 1, bpp = 32;
     uint32_t comp = 0;
@@ -556,6 +555,15 @@ extern "C" int rth_bmp_encode(const float* rgb, int W, int H, uint8_t* buf, size
     std::memcpy(buf + 0x1A, &planes, 2);
     std::memcpy(buf + 0x1C, &bpp, 2);
     std::memcpy(buf + 0x1E, &comp, 4);
+    return RT_OK;
+}
+
+extern "C" int rth_bmp_encode(const float* rgb, int W, int H, uint8_t* buf, size_t cap) {
+    if (!rgb || W <= 0 || H <= 0 || !buf) return RT_E_ARG;
+    const int row = W * 4, hdr = 14 + 40;
+    const size_t fsz = (size_t)hdr + (size_t)row * H;
+    if (cap < fsz) return RT_E_ARG;
+    rth_bmp_header(W, H, buf);
     for (int y = 0; y < H; y++) {  // bottom-up, bmp_writer.c:131-143
         const float* src = rgb + (size_t)(H - 1 - y) * W * 3;
         uint8_t* dst = buf + hdr + (size_t)y * row;

@@ -22,16 +22,30 @@ class RtError(RuntimeError):
 
 
 class Outputs(ctypes.Structure):
-    _fields_ = [("rgb", ctypes.c_void_p), ("hit", ctypes.c_void_p), ("t", ctypes.c_void_p)]
+    _fields_ = [("rgb", ctypes.c_void_p), ("hit", ctypes.c_void_p), ("t", ctypes.c_void_p),
+                ("bounce_hit", ctypes.c_void_p)]
 
 
 _lib.hip()  # fail loudly at import if the HIP library is absent
 _L = _lib.hip()
 _L.rt_render.argtypes = [ctypes.c_void_p, P(Camera), P(Frame), P(Outputs)]
+_L.rt_gather.argtypes = [P(ctypes.c_void_p), ctypes.c_int, ctypes.c_int]
+_L.rt_download_bmp.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
 
 
 def device_count():
     return _L.rt_device_count()
+
+
+def gather(renderers, root=0):
+    """rt_gather: the last frames of several Renderers (rows partitioning one frame) -> renderers[root]'s
+    device frame; afterwards renderers[root].download() / download_bmp() return the full frame."""
+    arr = (ctypes.c_void_p * len(renderers))(*[r._ctx.value for r in renderers])
+    rc = _L.rt_gather(arr, len(renderers), root)
+    r = renderers[root]
+    r._chk(rc, "rt_gather")
+    W, H = r._size
+    r._last = (W, H)
 
 
 def _ptr(x):
@@ -77,14 +91,16 @@ class Renderer:
         self.scene = scene
         return self
 
-    def render(self, cam, width, height, rows=None, bounces=4, spp=1, kernel="auto", rgb=None, hit=None, t=None):
+    def render(self, cam, width, height, rows=None, bounces=4, spp=1, kernel="auto", rgb=None, hit=None, t=None,
+               bounce_hit=None):
         """render_frame(): asynchronous. rows = (offset, stride, n) or None for the full frame.
-        rgb / hit / t: optional device tensors (torch) or raw device pointers."""
+        rgb / hit / t / bounce_hit ([n, W, bounces] int32): optional device tensors (torch) or raw pointers."""
         ro, rs, nr = rows if rows is not None else (0, 1, height)
         f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel))
-        out = Outputs(_ptr(rgb), _ptr(hit), _ptr(t))
+        out = Outputs(_ptr(rgb), _ptr(hit), _ptr(t), _ptr(bounce_hit))
         self._chk(_L.rt_render(self._ctx, ctypes.byref(cam), ctypes.byref(f), ctypes.byref(out)), "rt_render")
         self._last = (width, nr)
+        self._size = (width, height)
 
     def sync(self):
         ms = ctypes.c_float()
@@ -106,6 +122,13 @@ class Renderer:
         h = np.zeros((nr, W), np.int32) if hit else None
         self._chk(_L.rt_download(self._ctx, rgb.ctypes.data, h.ctypes.data if hit else None), "rt_download")
         return rgb, h
+
+    def download_bmp(self):
+        """bmp_write_file's bytes of the last (full) frame, quantised on the device (rt_download_bmp)"""
+        W, H = self._size
+        buf = np.zeros(54 + 4 * W * H, np.uint8)
+        self._chk(_L.rt_download_bmp(self._ctx, buf.ctypes.data, buf.size), "rt_download_bmp")
+        return buf.tobytes()
 
     def stats(self):
         s = Stats()

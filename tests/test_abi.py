@@ -49,3 +49,39 @@ def test_code_object_targets_gfx950():
     assert b"amdgcn-amd-amdhsa--gfx950" in data
     for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
         assert other not in data
+
+
+def test_ctypes_mirrors_match_the_c_layouts(tmp_path):
+    """prt/_lib.py and prt/device.py mirror the C structs field by field: sizes and offsets from the C
+    compiler itself (gcc on include/*.h)"""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "parallel-ray-tracer_amd"))
+    from prt import _lib
+    Outputs = __import__("prt.device", fromlist=["Outputs"]).Outputs if _lib_has_hip() else None
+    structs = {"rt_opts": _lib.Opts, "rt_scene": _lib.SceneDesc, "rt_frame": _lib.Frame, "rt_stats": _lib.Stats,
+               "rt_camera": _lib.Camera, "rt_triangle": _lib.Triangle, "rt_bvh_node": _lib.BvhNode,
+               "rt_light": _lib.Light, "rth_rng": _lib.Rng, "rth_bvh_stats": _lib.BvhStats,
+               "rth_wbvh_info": _lib.WbvhInfo}
+    if Outputs is not None:
+        structs["rt_outputs"] = Outputs
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rt_hip.h"', '#include "rt_host.h"',
+             "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layouts.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layouts"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                        check=True).stdout.split("\n") if l)
+    for cname, py in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(py, f).offset, (cname, f)
+
+
+def _lib_has_hip():
+    return os.path.exists(os.path.join(LIB, "librt_hip.so"))

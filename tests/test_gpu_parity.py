@@ -220,3 +220,85 @@ def test_errors_are_reported(dev, scenes):
     with pytest.raises(dev.RtError):
         r.render(host.camera(16, 16), 16, 16, bounces=0)
     r.close()
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_bounce_hits_match_oracle(dev, scenes, kernel):
+    """per-level closest-hit indices: -1 miss, -2 level not reached, every level bit-exact"""
+    import torch
+    from tests.oracle_bind import OracleScene
+    from tests.scenes import scene_paths
+    o = OracleScene.load(*scene_paths("car_boxed"))
+    o.build_bvh(3)
+    ref = o.render(128, 72, bounce_hits=True)
+    r = dev.Renderer(0)
+    r.upload(scenes["car_boxed"])
+    bh = torch.full((72, 128, 4), -9, dtype=torch.int32, device="cuda")
+    rgb = torch.empty((72, 128, 3), dtype=torch.float32, device="cuda")
+    r.render(host.camera(128, 72), 128, 72, kernel=kernel, rgb=rgb, bounce_hit=bh)
+    r.sync()
+    np.testing.assert_array_equal(bh.cpu().numpy(), ref["bounce_hit"])
+    assert same_bits(rgb.cpu().numpy(), ref["rgb"])
+    r.close()
+
+
+def test_download_bmp_is_the_reference_writers_bytes(dev, scenes):
+    """on-GPU BGRA8 quantisation == rth_bmp_encode == bmp_write_file (tests/test_host.py)"""
+    ref = np.load(os.path.join(GOLD, "car_boxed_160x90_strict.npz"))
+    r = dev.Renderer(0)
+    r.upload(scenes["car_boxed"])
+    r.render(host.camera(160, 90), 160, 90)
+    data = r.download_bmp()
+    assert data == host.bmp_encode(ref["rgb"])
+    rgb, _ = r.download()
+    assert data == host.bmp_encode(rgb)
+    with pytest.raises(dev.RtError):  # a row subset is not a BMP
+        r.render(host.camera(160, 90), 160, 90, rows=(1, 2, 45))
+        r.download_bmp()
+    r.close()
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_gather_rows_of_several_contexts(dev, scenes, n):
+    """rt_gather (in-process multi-GPU): n contexts render cyclic row sets, the root
+    gathers them; equal to one full-frame render, BMP included (same-device path on a 1-GPU box)"""
+    import torch
+    W, H = 200, 113
+    full = render(dev, scenes["car_boxed"], W, H, "fast")
+    rs = [dev.Renderer(0) for _ in range(n)]
+    bufs = []
+    for g, r in enumerate(rs):
+        r.upload(scenes["car_boxed"])
+        nr = (H - g + n - 1) // n
+        hit = torch.empty((nr, W), dtype=torch.int32, device="cuda")
+        r.render(host.camera(W, H), W, H, rows=(g, n, nr), hit=hit)
+        bufs.append(hit)
+    dev.gather(rs, root=1)
+    rgb, hit = rs[1].download(hit=True)
+    assert same_bits(rgb, full["rgb"])
+    np.testing.assert_array_equal(hit, full["hit"])
+    assert rs[1].download_bmp() == host.bmp_encode(full["rgb"])
+    bad = dev.Renderer(0)
+    bad.upload(scenes["car_boxed"])
+    bad.render(host.camera(W, H), W, H, rows=(0, 2, 57))
+    with pytest.raises(dev.RtError):  # rows 1, 3, ... missing
+        dev.gather([bad], root=0)
+    for r in rs + [bad]:
+        r.close()
+
+
+def test_cli_drop_in_writes_the_reference_bmp(tmp_path):
+    """bin/raytracer (the cpu/raytracer drop-in): stdout metric lines and <scene>.bmp byte-identical to
+    the reference renderer's output for the same frame (fixture rgb -> bmp_write_file bytes)"""
+    import subprocess
+    from tests.scenes import scene_paths
+    exe = os.path.join(os.path.dirname(GOLD), "..", "parallel-ray-tracer_amd", "bin", "raytracer")
+    assets = os.path.dirname(os.path.dirname(scene_paths("car_boxed")[0]))
+    out = tmp_path / "car_boxed.bmp"
+    r = subprocess.run([exe, "4", "--scene", "car_boxed", "--assets", assets, "--width", "160", "--height", "90",
+                        "--iterations", "3", "--out", str(out)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    for line in ("Number of triangles: 45999", "Frame time (median):", "Rays per frame (primary+reflection+shadow):"):
+        assert line in r.stdout, line
+    ref = np.load(os.path.join(GOLD, "car_boxed_160x90_strict.npz"))
+    assert out.read_bytes() == host.bmp_encode(ref["rgb"])

@@ -78,6 +78,9 @@ for s in "${@:-smoke pytest bench}"; do
                   run abpfnewcar$i 300 python tools/ab.py --scene car_boxed --rounds 3 --frames 5 fast
                   PRT_LIB_DIR=build/old/lib run abpfoldcar$i 300 python tools/ab.py --scene car_boxed --rounds 3 --frames 5 fast:PRT_SHADOW_BATCH=0
               done ;;
+      abprio) run abprio 300 python tools/ab.py --rounds 4 --frames 5 fast fast:PRT_PRIO=1
+              run abpriocar 300 python tools/ab.py --scene car_boxed --rounds 4 --frames 5 fast fast:PRT_PRIO=1
+              run abpriosc 300 python tools/ab.py --scene sportscar --rounds 3 --frames 5 fast fast:PRT_PRIO=1 ;;
       *) echo "unknown step $step"; exit 2 ;;
     esac
   done

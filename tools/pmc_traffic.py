@@ -14,7 +14,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PROD = "k_persist<4, false, false, true>"
+PROD = "k_persist<4, false, false, true"  # production instantiation (no counters, no trace)
 
 
 def rows(path):
