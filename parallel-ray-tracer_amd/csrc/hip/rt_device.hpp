@@ -75,7 +75,6 @@ struct KArgs {
     int refill_below;              // k_wave: leave the traversal loop when fewer lanes than this still trace
     unsigned long long* tile_trace;  // diagnostics (PRT_TILE_TRACE): per-tile timeline (rt_kernels.hpp)
     const int* tile_order;           // nullable: k-th dealt tile = tile_order[k] (default: row-major)
-    int prio;                        // k_persist: raise the wave's issue priority with the bounce level
 };
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

@@ -603,7 +603,6 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     A.hit = out ? out->hit : nullptr;
     A.t = out ? out->t : nullptr;
     A.bounce_hit = out ? out->bounce_hit : nullptr;
-    if (const char* e = std::getenv("PRT_PRIO")) A.prio = std::atoi(e);  // A/B knob
     A.counters = ctx->d_counters;
     A.work = ctx->d_work;
     A.tiles_x = (f->width + 7) / 8;

@@ -614,17 +614,10 @@ __device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, in
     int L = 0;
     bool tail = false;
     for (int it = 0; it < A.bounces; ++it) {
-        if (A.prio) {  // wave-uniform: deeper levels belong to the long tiles that end the frame
-            if (it == 0) __builtin_amdgcn_s_setprio(0);
-            else if (it == 1) __builtin_amdgcn_s_setprio(1);
-            else if (it == 2) __builtin_amdgcn_s_setprio(2);
-            else __builtin_amdgcn_s_setprio(3);
-        }
         if (path_step<MAXB, STRICT, COUNT, REG>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0, A.bounce_hit,
                                                 bh_pix, stk, c))
             break;
     }
-    if (A.prio) __builtin_amdgcn_s_setprio(0);
     return fold_path<MAXB>(A.s, cols, mats, L, tail);
 }
 

@@ -346,6 +346,22 @@ struct Builder {
     // depth cap 24: the fast kernels stack only deferred far children, at most depth entries (26 slots)
     static constexpr int SAH_MAX_DEPTH = 24;
     std::vector<float> cen;  // centroid x,y,z per triangle (copied from triangle_t.centroid)
+    std::vector<float> tb;   // per-triangle box lo.xyz, hi.xyz (the SAH path only; plain min/max)
+    static rt_vec3 fmin3(const rt_vec3& a, const rt_vec3& b) {
+        return V(std::min(a.x, b.x), std::min(a.y, b.y), std::min(a.z, b.z));
+    }
+    static rt_vec3 fmax3(const rt_vec3& a, const rt_vec3& b) {
+        return V(std::max(a.x, b.x), std::max(a.y, b.y), std::max(a.z, b.z));
+    }
+    void grow_sah(rt_vec3& mn, rt_vec3& mx, int t) const {
+        const float* b = &tb[6 * (size_t)t];
+        mn.x = std::min(mn.x, b[0]);
+        mn.y = std::min(mn.y, b[1]);
+        mn.z = std::min(mn.z, b[2]);
+        mx.x = std::max(mx.x, b[3]);
+        mx.y = std::max(mx.y, b[4]);
+        mx.z = std::max(mx.z, b[5]);
+    }
 
     void sah_split(int ni, int depth) {
         rt_bvh_node* p = &bvh[ni];
@@ -362,14 +378,16 @@ struct Builder {
                 cmn[a] = std::min(cmn[a], c);
                 cmx[a] = std::max(cmx[a], c);
             }
-        const int NB = 32;
+        // 32 bins, or about one per triangle in small nodes (the per-node sweeps dominate otherwise)
+        constexpr int NBMAX = 32;
+        const int NB = cnt >= NBMAX ? NBMAX : std::max(4, cnt);
         float best = FLT_MAX;
         int best_axis = -1, best_bin = -1;
         for (int a = 0; a < 3; a++) {
             float ext = cmx[a] - cmn[a];
             if (!(ext > 0)) continue;
-            rt_vec3 bmn[NB], bmx[NB];
-            int bc[NB] = {0};
+            rt_vec3 bmn[NBMAX], bmx[NBMAX];
+            int bc[NBMAX] = {0};
             for (int b = 0; b < NB; b++) {
                 bmn[b] = V(FLT_MAX, FLT_MAX, FLT_MAX);
                 bmx[b] = V(-FLT_MAX, -FLT_MAX, -FLT_MAX);
@@ -379,16 +397,16 @@ struct Builder {
                 int t = idx[i];
                 int b = std::min(NB - 1, (int)((cen[3 * t + a] - cmn[a]) * sc));
                 bc[b]++;
-                grow(bmn[b], bmx[b], t);
+                grow_sah(bmn[b], bmx[b], t);
             }
-            float rA[NB];
-            int rN[NB];
+            float rA[NBMAX];
+            int rN[NBMAX];
             rt_vec3 mn = V(FLT_MAX, FLT_MAX, FLT_MAX), mx = V(-FLT_MAX, -FLT_MAX, -FLT_MAX);
             int acc = 0;
             for (int b = NB - 1; b > 0; b--) {
                 acc += bc[b];
-                mn = vmin(mn, bmn[b]);
-                mx = vmax(mx, bmx[b]);
+                mn = fmin3(mn, bmn[b]);
+                mx = fmax3(mx, bmx[b]);
                 rA[b] = area(mn, mx);
                 rN[b] = acc;
             }
@@ -397,8 +415,8 @@ struct Builder {
             acc = 0;
             for (int b = 0; b < NB - 1; b++) {
                 acc += bc[b];
-                mn = vmin(mn, bmn[b]);
-                mx = vmax(mx, bmx[b]);
+                mn = fmin3(mn, bmn[b]);
+                mx = fmax3(mx, bmx[b]);
                 if (acc == 0 || rN[b + 1] == 0) continue;
                 float cost = area(mn, mx) * acc + rA[b + 1] * rN[b + 1];
                 if (cost < best) {
@@ -443,7 +461,7 @@ struct Builder {
         for (rt_bvh_node* c : {L, R}) {
             c->min = V(1e10f, 1e10f, 1e10f);
             c->max = V(-1e10f, -1e10f, -1e10f);
-            for (int i = c->child; i < c->child + c->tr_len; i++) grow(c->min, c->max, idx[i]);
+            for (int i = c->child; i < c->child + c->tr_len; i++) grow_sah(c->min, c->max, idx[i]);
         }
         p->child = ci;
         p->tr_len = 0;
@@ -481,8 +499,18 @@ extern "C" int rth_bvh_build(const rt_triangle* tris, size_t n, int heuristic, r
     for (size_t i = 0; i < n; i++) b.grow(root.min, root.max, (int)i);
     if (heuristic == RTH_BVH_BINNED_SAH) {
         b.cen.resize(3 * n);
-        for (size_t i = 0; i < n; i++)
+        b.tb.resize(6 * n);
+        for (size_t i = 0; i < n; i++) {
             for (int a = 0; a < 3; a++) b.cen[3 * i + a] = tris[i].centroid[a];
+            rt_vec3 mn = tris[i].coords[0], mx = tris[i].coords[0];
+            for (int k = 1; k < 3; k++) {
+                const rt_vec3& c = tris[i].coords[k];
+                mn = V(std::min(mn.x, c.x), std::min(mn.y, c.y), std::min(mn.z, c.z));
+                mx = V(std::max(mx.x, c.x), std::max(mx.y, c.y), std::max(mx.z, c.z));
+            }
+            const float v[6] = {mn.x, mn.y, mn.z, mx.x, mx.y, mx.z};
+            std::memcpy(&b.tb[6 * i], v, sizeof v);
+        }
         b.sah_split(0, 0);
     } else {
         b.split(0, 0);
