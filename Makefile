@@ -23,7 +23,7 @@ host: $(LIB)/librt_host.so
 hip: $(LIB)/librt_hip.so
 cli: $(BIN)/raytracer
 
-HOST_SRCS := $(CSRC)/host/rt_host.cpp $(CSRC)/host/rt_wide.cpp
+HOST_SRCS := $(CSRC)/host/rt_host.cpp $(CSRC)/host/rt_wide.cpp $(CSRC)/host/rt_cache.cpp
 
 $(LIB)/librt_host.so: $(HOST_SRCS) include/rt_host.h include/rt_types.h
 	@mkdir -p $(LIB)

@@ -55,6 +55,17 @@ typedef struct rth_bvh_stats {
 int rth_bvh_build(const rt_triangle* tris, size_t n, int heuristic, rth_rng* g, rt_bvh_node** nodes,
                   int* bvh_len, int** tri_idx, rth_bvh_stats* stats);
 
+/* ---- binary scene cache (no reference counterpart). `cache` is a file path (NULL: no
+ * cache). An entry is keyed by a 64-bit hash of everything the result depends on and checksummed; a
+ * stale, foreign or damaged file is ignored and replaced, so the cached call returns exactly what the
+ * uncached one would. *from_cache (nullable) = 1 when the result was read from the cache. */
+/* triangles_load of an OBJ/MTL pair (key: both files' bytes) */
+int rth_triangles_load_cached(const char* obj, const char* mtl, const char* cache, rt_triangle** out, size_t* n,
+                              int* from_cache);
+/* bvh_build (key: the triangles, heuristic and RNG state; the RNG is left as after the real build) */
+int rth_bvh_build_cached(const rt_triangle* tris, size_t n, int heuristic, rth_rng* g, const char* cache,
+                         rt_bvh_node** nodes, int* bvh_len, int** tri_idx, rth_bvh_stats* stats, int* from_cache);
+
 /* ---- 8-wide quantised BVH: the fast walk's device layout (rt_device.hpp DWide), built
  * from any reference-layout binary BVH (bvh + tri_idx as rth_bvh_build returns them). Interior nodes
  * hold up to 8 children; child boxes are grown by `inflate` and quantised outward to 8 bits per

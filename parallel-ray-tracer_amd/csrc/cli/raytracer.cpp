@@ -2,14 +2,16 @@
 //
 //   raytracer [threads] [ntris] [--scene NAME] [--assets DIR] [--width W] [--height H]
 //             [--bounces B] [--iterations K] [--warmup W] [--bvh-heuristic H] [--seed S]
-//             [--gpus N] [--spp S] [--kernel fast|strict|wavefront|wave] [--out FILE.bmp]
+//             [--gpus N] [--spp S] [--kernel fast|strict|wavefront|wave] [--out FILE.bmp] [--cache DIR]
 //
 // Positional arguments and defaults are the reference's (options.h: 1920x1080, car_boxed, BOUNCES 4,
 // ITERATIONS 1, BVH_HEURISTIC 3, SEED 1; main.c:97-131: `threads` in 1..63, `ntris` = random mode).
 // Scenes load from <assets>/<scene>/{triangles.obj,triangles.mtl,lights.obj}, default assets "../assets"
 // as in main.c:113-114. The frame renders on the GPU(s) through the rt_* C-ABI; with --gpus N the
-// rows are dealt cyclically over N devices (one rt_ctx each, one host thread each) and assembled on
-// the host. Output: <scene>.bmp (main.c:191) and the reference's stdout metric lines, plus ray counts.
+// rows are dealt cyclically over N devices (one rt_ctx each, one host thread each) and gathered on GPU 0
+// (rt_gather). Output: <scene>.bmp (main.c:191, quantised on the GPU) and the reference's stdout metric
+// lines, plus ray counts. --cache DIR keeps the parsed triangles and the BVH in binary cache files
+// (rth_*_cached: identical results, no re-parse / re-build of unchanged scenes).
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -28,7 +30,7 @@ namespace {
 struct Args {
     int threads = 1;
     long ntris = -1;
-    std::string scene = "car_boxed", assets = "../assets", out, kernel = "fast";
+    std::string scene = "car_boxed", assets = "../assets", out, kernel = "fast", cache;
     int W = 1920, H = 1080, bounces = 4, iterations = 1, warmup = 0, heuristic = 3, gpus = 1, spp = 1;
     unsigned seed = 1;
 };
@@ -60,6 +62,7 @@ Args parse(int argc, char** argv) {
         else if (s == "--spp") a.spp = std::atoi(val().c_str());
         else if (s == "--kernel") a.kernel = val();
         else if (s == "--out") a.out = val();
+        else if (s == "--cache") a.cache = val();
         else if (s.rfind("--", 0) == 0) usage(("unknown option " + s).c_str());
         else pos.push_back(s);
     }
@@ -93,7 +96,9 @@ int main(int argc, char** argv) {
     size_t nl = 0;
     if (a.ntris < 0) {
         std::string d = a.assets + "/" + a.scene + "/";
-        if (rth_triangles_load((d + "triangles.obj").c_str(), (d + "triangles.mtl").c_str(), &tris, &n) != RT_OK)
+        const std::string tc = a.cache.empty() ? "" : a.cache + "/" + a.scene + ".tris.prtc";
+        if (rth_triangles_load_cached((d + "triangles.obj").c_str(), (d + "triangles.mtl").c_str(),
+                                      tc.empty() ? nullptr : tc.c_str(), &tris, &n, nullptr) != RT_OK)
             return EXIT_FAILURE;  // the loader printed "cannot load <file>" (triangle.c:29-30)
         if (rth_lights_load((d + "lights.obj").c_str(), &lights, &nl) != RT_OK) return EXIT_FAILURE;
     } else if (rth_triangles_random((size_t)a.ntris, &rng, &tris) == RT_OK) {
@@ -106,7 +111,11 @@ int main(int argc, char** argv) {
     int bvh_len = 0;
     int* tri_idx = nullptr;
     rth_bvh_stats bs{};
-    int rc = rth_bvh_build(tris, n, a.heuristic, &rng, &bvh, &bvh_len, &tri_idx, &bs);
+    const std::string bc = a.cache.empty() || a.ntris >= 0
+                               ? ""
+                               : a.cache + "/" + a.scene + ".bvh" + std::to_string(a.heuristic) + ".prtc";
+    int rc = rth_bvh_build_cached(tris, n, a.heuristic, &rng, bc.empty() ? nullptr : bc.c_str(), &bvh, &bvh_len,
+                                  &tri_idx, &bs, nullptr);
     if (rc == RT_E_EMPTY) return EXIT_FAILURE;  // "no triangles, cannot build bvh." (bvh.c:361-364)
     if (rc != RT_OK) usage("bvh build failed (heuristic must be 0, 1, 3, 6 or 16)");
     double bvh_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

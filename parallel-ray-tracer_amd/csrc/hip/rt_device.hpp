@@ -75,6 +75,12 @@ struct KArgs {
     int refill_below;              // k_wave: leave the traversal loop when fewer lanes than this still trace
     unsigned long long* tile_trace;  // diagnostics (PRT_TILE_TRACE): per-tile timeline (rt_kernels.hpp)
     const int* tile_order;           // nullable: k-th dealt tile = tile_order[k] (default: row-major)
+    // split pipeline (rt_split.hpp): per (level, tile slot) records, path info, visibility bytes, batches
+    float4* srec;
+    unsigned* spinfo;
+    unsigned char* svis;
+    unsigned* sbatch;
+    size_t nslots;
 };
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)
@@ -96,8 +102,7 @@ __device__ __forceinline__ v3 xyz(float4 f) { return mk(f.x, f.y, f.z); }
 
 // ---------------------------------------------------------------- ray-triangle (raytracer.c:35-59)
 // v0, e1, e2, n precomputed on the host with the reference's own roundings.
-__device__ __forceinline__ float hit_triangle(v3 o, v3 d, const float4* __restrict__ tri, int& nd) {
-    const float4 a = tri[0], b = tri[1], c = tri[2];
+__device__ __forceinline__ float hit_triangle_v(v3 o, v3 d, float4 a, float4 b, float4 c, int& nd) {
     const v3 v0 = mk(a.x, a.y, a.z), e1 = mk(a.w, b.x, b.y), e2 = mk(b.z, b.w, c.x), n = mk(c.y, c.z, c.w);
     const float det = -dot(d, n);
     nd = det < 0.0f;
@@ -110,6 +115,9 @@ __device__ __forceinline__ float hit_triangle(v3 o, v3 d, const float4* __restri
     const float t = dot(ao, n) * inv;
     if (t > EPS && u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f) return t;
     return FMAX;
+}
+__device__ __forceinline__ float hit_triangle(v3 o, v3 d, const float4* __restrict__ tri, int& nd) {
+    return hit_triangle_v(o, d, tri[0], tri[1], tri[2], nd);
 }
 
 // ---------------------------------------------------------------- exact slab test (bvh.c:48-59)

@@ -17,6 +17,7 @@
 #include "rt_host.h"
 #include "rt_kernels.hpp"
 #include "rt_output.hpp"
+#include "rt_split.hpp"
 #include "rt_wave.hpp"
 #include "rt_wf.hpp"
 
@@ -76,6 +77,12 @@ struct rt_ctx {
     size_t stage_cap = 0;
     unsigned* d_bmp = nullptr;
     size_t bmp_cap = 0;
+    // split pipeline buffers (rt_split.hpp)
+    float4* d_srec = nullptr;
+    unsigned* d_spinfo = nullptr;
+    unsigned char* d_svis = nullptr;
+    unsigned* d_sbatch = nullptr;
+    size_t srec_cap = 0, spinfo_cap = 0, svis_cap = 0, sbatch_cap = 0;
     unsigned long long* d_counters = nullptr;  // rtd::NCOUNT
     int* d_order = nullptr;                    // tile dealing order (PRT_TILE_ORDER), for order_tx x order_ty tiles
     int order_tx = 0, order_ty = 0;
@@ -272,7 +279,7 @@ extern "C" int rt_create(const rt_opts* opts, rt_ctx** out) {
         if (e == hipSuccess) e = hipEventCreate(&ctx->ev1s[i]);
     }
     if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_counters, sizeof(unsigned long long) * rtd::NCOUNT);
-    if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_work, 256);
+    if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_work, 1024);
     if (e == hipSuccess) e = hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT);
     if (e != hipSuccess) {
         rt_destroy(ctx);
@@ -543,6 +550,11 @@ int launch_wf(rt_ctx* ctx, const rtd::KArgs& K, bool count) {
 
 }  // namespace
 
+namespace {
+template <int MAXB>
+int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count);  // below
+}  // namespace
+
 extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, const rt_outputs* out) {
     if (!ctx) return RT_E_ARG;
     if (!ctx->has_scene) {
@@ -617,7 +629,7 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     const bool count = (ctx->flags & RT_FLAG_COUNTERS) != 0;
     dim3 grid((f->width + 15) / 16, (f->n_rows + 15) / 16);
     HIPC(hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT, ctx->stream));
-    HIPC(hipMemsetAsync(ctx->d_work, 0, 256, ctx->stream));
+    HIPC(hipMemsetAsync(ctx->d_work, 0, 1024, ctx->stream));
     const int slot = (int)(ctx->launches % rt_ctx::NEV);
     ctx->ev0 = ctx->ev0s[slot];
     ctx->ev1 = ctx->ev1s[slot];
@@ -656,7 +668,16 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
         }
         A.tile_order = ctx->d_order;
     }
-    if (kernel == RT_KERNEL_WAVEFRONT) {
+    // RT_KERNEL_FAST at 1 spp: k_persist, or the split pipeline (rt_split.hpp) when shadow rays dominate a
+    // tile's chain. Same-box A/B: 1 light +49 % time, 2 lights +7 %, 4 lights -21 % with the
+    // split, so it takes scenes with >= 3 lights. PRT_SPLIT=0/1 forces either.
+    const char* split_env = std::getenv("PRT_SPLIT");
+    const bool split_ok = kernel == RT_KERNEL_FAST && f->spp == 1 && ctx->n_lights <= 32 && !A.tile_trace;
+    const bool split = split_ok && (split_env ? std::atoi(split_env) == 1 : ctx->n_lights >= 3);
+    if (split) {
+        const int rc = f->bounces <= 4 ? launch_split<4>(ctx, A, count) : launch_split<8>(ctx, A, count);
+        if (rc) return rc;
+    } else if (kernel == RT_KERNEL_WAVEFRONT) {
         const int rc = launch_wf(ctx, A, count);
         if (rc) return rc;
     } else if (f->bounces <= 4) {
@@ -742,6 +763,34 @@ int grow(rt_ctx* ctx, T** p, size_t& cap, size_t n) {
     cap = 0;
     HIPC(hipMalloc((void**)p, sizeof(T) * std::max<size_t>(n, 1)));
     cap = n;
+    return RT_OK;
+}
+}  // namespace
+
+namespace {
+// the split pipeline (rt_split.hpp): closest chains, shadow batches, resolve — three launches
+template <int MAXB>
+int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count) {
+    const int nl = A.s.n_lights;
+    A.nslots = (size_t)A.n_tiles * 64;
+    int rc;
+    if ((rc = grow(ctx, &ctx->d_srec, ctx->srec_cap, (size_t)A.bounces * A.nslots * 3)) ||
+        (rc = grow(ctx, &ctx->d_spinfo, ctx->spinfo_cap, A.nslots)) ||
+        (rc = grow(ctx, &ctx->d_svis, ctx->svis_cap, (size_t)A.bounces * std::max(nl, 1) * A.nslots)) ||
+        (rc = grow(ctx, &ctx->d_sbatch, ctx->sbatch_cap, (size_t)A.n_tiles * A.bounces * std::max(nl, 1))))
+        return rc;
+    A.srec = ctx->d_srec;
+    A.spinfo = ctx->d_spinfo;
+    A.svis = ctx->d_svis;
+    A.sbatch = ctx->d_sbatch;
+    hipStream_t s = ctx->stream;
+    auto ka = count ? rtd::k_split_closest<MAXB, true> : rtd::k_split_closest<MAXB, false>;
+    auto kb = count ? rtd::k_split_shadow<true> : rtd::k_split_shadow<false>;
+    const int ga = std::max(1, std::min(resident(ka, ctx->device), (A.n_tiles + 3) / 4));
+    const int gb = std::max(1, resident(kb, ctx->device));
+    ka<<<ga, rtd::BLOCK, 0, s>>>(A);
+    kb<<<gb, rtd::BLOCK, 0, s>>>(A);
+    rtd::k_split_resolve<MAXB><<<(int)((A.nslots + 255) / 256), 256, 0, s>>>(A);
     return RT_OK;
 }
 }  // namespace
@@ -883,7 +932,8 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     if (ctx->d_rgb_own) (void)hipFree(ctx->d_rgb_own);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->d_order) (void)hipFree(ctx->d_order);
-    for (void* p : {(void*)ctx->d_full, (void*)ctx->d_full_hit, (void*)ctx->d_stage, (void*)ctx->d_bmp})
+    for (void* p : {(void*)ctx->d_full, (void*)ctx->d_full_hit, (void*)ctx->d_stage, (void*)ctx->d_bmp,
+                    (void*)ctx->d_srec, (void*)ctx->d_spinfo, (void*)ctx->d_svis, (void*)ctx->d_sbatch})
         if (p) (void)hipFree(p);
     if (ctx->d_work) (void)hipFree(ctx->d_work);
     for (int i = 0; i < rt_ctx::NEV; i++) {

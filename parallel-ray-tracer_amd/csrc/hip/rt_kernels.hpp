@@ -364,7 +364,9 @@ __device__ __forceinline__ int wide_next(unsigned nh, int cb, unsigned imask, un
     return cb + __popc(imask & ((1u << slot) - 1u));
 }
 
-template <bool COUNT>
+// PIPE: software-pipeline the leaf triangles (the next triangle's loads issued before this one's test);
+// pays where registers allow (the split kernels), not in k_persist (spills at its 168-VGPR cap).
+template <bool COUNT, bool PIPE = false>
 __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& best, int& hp, int& nd, bool& tie,
                                              int* __restrict__ stk, Ctr& c) {
     const RayPre p = ray_pre(o, d);
@@ -383,19 +385,53 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
         }
         const int next = wide_next(nh, cb, imask, oct, sp, stk);
         if (next >= 0) N = wload(W, next);
-        while (th) {
-            const int i = tb + __builtin_ctz(th);
+        if (!PIPE) {
+            while (th) {
+                const int i = tb + __builtin_ctz(th);
+                th &= th - 1u;
+                int k;
+                const float tt = hit_triangle(o, d, W.tris + 3 * i, k);
+                if (COUNT) c.cht++;
+                if (tt < best) {
+                    best = tt;
+                    nd = k;
+                    hp = i;
+                    tie = false;
+                } else if (tt == best && tt != FMAX) {
+                    tie = true;
+                }
+            }
+        } else if (th) {  // the next triangle's loads go out before this one's test
+            int i = tb + __builtin_ctz(th);
             th &= th - 1u;
-            int k;
-            const float tt = hit_triangle(o, d, W.tris + 3 * i, k);
-            if (COUNT) c.cht++;
-            if (tt < best) {
-                best = tt;
-                nd = k;
-                hp = i;
-                tie = false;
-            } else if (tt == best && tt != FMAX) {
-                tie = true;
+            float4 ta = W.tris[3 * i], tb4 = W.tris[3 * i + 1], tc = W.tris[3 * i + 2];
+            for (;;) {
+                const bool more = th != 0u;
+                int i2 = 0;
+                float4 na = ta, nb = tb4, nc = tc;
+                if (more) {
+                    i2 = tb + __builtin_ctz(th);
+                    th &= th - 1u;
+                    na = W.tris[3 * i2];
+                    nb = W.tris[3 * i2 + 1];
+                    nc = W.tris[3 * i2 + 2];
+                }
+                int k;
+                const float tt = hit_triangle_v(o, d, ta, tb4, tc, k);
+                if (COUNT) c.cht++;
+                if (tt < best) {
+                    best = tt;
+                    nd = k;
+                    hp = i;
+                    tie = false;
+                } else if (tt == best && tt != FMAX) {
+                    tie = true;
+                }
+                if (!more) break;
+                i = i2;
+                ta = na;
+                tb4 = nb;
+                tc = nc;
             }
         }
         if (next < 0) {
@@ -405,7 +441,7 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
     }
 }
 
-template <bool COUNT>
+template <bool COUNT, bool PIPE = false>
 __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c) {
     const RayPre p = ray_pre(o, d);
     const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
@@ -425,17 +461,47 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
         }
         const int next = wide_next(nh, cb, imask, oct, sp, stk);
         if (next >= 0) N = wload(W, next);
-        while (th) {
-            const int i = tb + __builtin_ctz(th);
+        if (!PIPE) {
+            while (th) {
+                const int i = tb + __builtin_ctz(th);
+                th &= th - 1u;
+                int k;
+                const float tt = hit_triangle(o, d, W.tris + 3 * i, k);
+                if (COUNT) c.sht++;
+                if (tt < best) {
+                    best = tt;
+                    const v3 ip = add(o, mul(d, best));
+                    const v3 oi = sub(o, ip);
+                    if (ld2 > dot(oi, oi)) return false;
+                }
+            }
+        } else if (th) {  // software-pipelined as in closest_wide
+            int i = tb + __builtin_ctz(th);
             th &= th - 1u;
-            int k;
-            const float tt = hit_triangle(o, d, W.tris + 3 * i, k);
-            if (COUNT) c.sht++;
-            if (tt < best) {
-                best = tt;
-                const v3 ip = add(o, mul(d, best));
-                const v3 oi = sub(o, ip);
-                if (ld2 > dot(oi, oi)) return false;
+            float4 ta = W.tris[3 * i], tb4 = W.tris[3 * i + 1], tc = W.tris[3 * i + 2];
+            for (;;) {
+                const bool more = th != 0u;
+                float4 na = ta, nb = tb4, nc = tc;
+                if (more) {
+                    const int i2 = tb + __builtin_ctz(th);
+                    th &= th - 1u;
+                    na = W.tris[3 * i2];
+                    nb = W.tris[3 * i2 + 1];
+                    nc = W.tris[3 * i2 + 2];
+                }
+                int k;
+                const float tt = hit_triangle_v(o, d, ta, tb4, tc, k);
+                if (COUNT) c.sht++;
+                if (tt < best) {
+                    best = tt;
+                    const v3 ip = add(o, mul(d, best));
+                    const v3 oi = sub(o, ip);
+                    if (ld2 > dot(oi, oi)) return false;
+                }
+                if (!more) break;
+                ta = na;
+                tb4 = nb;
+                tc = nc;
             }
         }
         if (next < 0) {
@@ -447,7 +513,7 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
 }
 
 // Closest hit with the kernel's policy; returns the ORIGINAL triangle index (-1 = miss).
-template <bool STRICT, bool COUNT, bool REG = true>
+template <bool STRICT, bool COUNT, bool REG = true, bool PIPE = false>
 __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best, int& nd, int* __restrict__ stk,
                                        Ctr& c) {
     int hp = -1;
@@ -456,7 +522,7 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
     nd = 0;
     if (!STRICT && !degenerate(d)) {
         if (s.wide.nodes) {
-            closest_wide<COUNT>(s.wide, o, d, best, hp, nd, tie, stk, c);
+            closest_wide<COUNT, PIPE>(s.wide, o, d, best, hp, nd, tie, stk, c);
             if (!tie) return hp >= 0 ? s.wide.tri_orig[hp] : -1;
         } else {
             closest_walk<false, COUNT, REG>(s.acc, o, d, best, hp, nd, tie, stk, c);
@@ -473,10 +539,10 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
     return hp >= 0 ? s.ref.tri_orig[hp] : -1;
 }
 
-template <bool STRICT, bool COUNT, bool REG = true>
+template <bool STRICT, bool COUNT, bool REG = true, bool PIPE = false>
 __device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c) {
     if (!STRICT && !degenerate(d)) {
-        if (s.wide.nodes) return visible_wide<COUNT>(s.wide, o, d, ld2, stk, c);
+        if (s.wide.nodes) return visible_wide<COUNT, PIPE>(s.wide, o, d, ld2, stk, c);
         return visible_walk<false, COUNT, REG>(s.acc, o, d, ld2, stk, c);
     }
     if (!STRICT) c.fb++;
@@ -489,6 +555,20 @@ __device__ __forceinline__ void set3(v3 (&a)[MAXB], int i, v3 v) {
 #pragma unroll
     for (int k = 0; k < MAXB; k++)
         if (k == i) a[k] = v;
+}
+template <int MAXB>
+__device__ __forceinline__ void set_u(unsigned (&a)[MAXB], int i, unsigned v) {
+#pragma unroll
+    for (int k = 0; k < MAXB; k++)
+        if (k == i) a[k] = v;
+}
+template <int MAXB>
+__device__ __forceinline__ unsigned get_u(const unsigned (&a)[MAXB], int i) {
+    unsigned r = 0;
+#pragma unroll
+    for (int k = 0; k < MAXB; k++)
+        if (k == i) r = a[k];
+    return r;
 }
 template <int MAXB>
 __device__ __forceinline__ void seti(int (&a)[MAXB], int i, int v) {

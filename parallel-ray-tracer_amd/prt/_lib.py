@@ -99,6 +99,12 @@ def host():
         if hasattr(L, "rth_wbvh_build"):  # absent from older builds (A/B via PRT_LIB_DIR)
             L.rth_wbvh_build.argtypes = [P(BvhNode), ctypes.c_int, P(ctypes.c_int), P(Triangle), ctypes.c_int,
                                          ctypes.c_float, P(P(ctypes.c_uint32)), P(P(ctypes.c_int)), P(WbvhInfo)]
+        if hasattr(L, "rth_triangles_load_cached"):
+            L.rth_triangles_load_cached.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                                    P(P(Triangle)), P(ctypes.c_size_t), P(ctypes.c_int)]
+            L.rth_bvh_build_cached.argtypes = [P(Triangle), ctypes.c_size_t, ctypes.c_int, P(Rng), ctypes.c_char_p,
+                                               P(P(BvhNode)), P(ctypes.c_int), P(P(ctypes.c_int)), P(BvhStats),
+                                               P(ctypes.c_int)]
         L.rth_camera.argtypes = [ctypes.c_int, ctypes.c_int, P(Camera)]
         L.rth_bmp_write.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
         L.rth_bmp_encode.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]

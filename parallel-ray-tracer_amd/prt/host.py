@@ -47,14 +47,40 @@ def _take(ptr, n, dtype):
     return arr
 
 
-def triangles_load(obj, mtl):
-    """triangles_load(objname, mtlname, &size), cpu/src/triangle.c:74-126 -> structured array"""
+def triangles_load(obj, mtl, cache=None):
+    """triangles_load(objname, mtlname, &size), cpu/src/triangle.c:74-126 -> structured array.
+    cache: binary cache file (rth_triangles_load_cached): identical triangles, no re-parse when unchanged."""
     L = _lib.host()
     out = P(Triangle)()
     n = ctypes.c_size_t()
-    _check(L.rth_triangles_load(obj.encode(), mtl.encode(), ctypes.byref(out), ctypes.byref(n)),
-           f"triangles_load({obj})")
+    if cache is None:
+        _check(L.rth_triangles_load(obj.encode(), mtl.encode(), ctypes.byref(out), ctypes.byref(n)),
+               f"triangles_load({obj})")
+    else:
+        hit = ctypes.c_int()
+        _check(L.rth_triangles_load_cached(obj.encode(), mtl.encode(), str(cache).encode(), ctypes.byref(out),
+                                           ctypes.byref(n), ctypes.byref(hit)), f"triangles_load({obj})")
+        triangles_load.last_from_cache = bool(hit.value)
     return _take(out, n.value, TRI_DTYPE)
+
+
+def bvh_build_cached(tris, heuristic, rng, cache):
+    """bvh_build through the binary cache (rth_bvh_build_cached) -> (nodes, tri_idx, stats, from_cache);
+    the RNG is left as after a real build"""
+    L = _lib.host()
+    h = HEURISTICS.get(heuristic, heuristic)
+    tris = np.ascontiguousarray(tris, dtype=TRI_DTYPE)
+    nodes = P(BvhNode)()
+    idx = P(ctypes.c_int)()
+    nlen = ctypes.c_int()
+    st = BvhStats()
+    hit = ctypes.c_int()
+    _check(L.rth_bvh_build_cached(tris.ctypes.data_as(P(Triangle)), len(tris), h,
+                                  ctypes.byref(rng.state) if rng is not None else None, str(cache).encode(),
+                                  ctypes.byref(nodes), ctypes.byref(nlen), ctypes.byref(idx), ctypes.byref(st),
+                                  ctypes.byref(hit)), "bvh_build_cached")
+    return _take(nodes, nlen.value, NODE_DTYPE), _take(idx, len(tris), np.dtype(np.int32)), \
+        {"leaves": st.leaves, "max_leaf": st.max_leaf, "max_depth": st.max_depth}, bool(hit.value)
 
 
 def lights_load(path):

@@ -294,11 +294,38 @@ def test_cli_drop_in_writes_the_reference_bmp(tmp_path):
     from tests.scenes import scene_paths
     exe = os.path.join(os.path.dirname(GOLD), "..", "parallel-ray-tracer_amd", "bin", "raytracer")
     assets = os.path.dirname(os.path.dirname(scene_paths("car_boxed")[0]))
-    out = tmp_path / "car_boxed.bmp"
-    r = subprocess.run([exe, "4", "--scene", "car_boxed", "--assets", assets, "--width", "160", "--height", "90",
-                        "--iterations", "3", "--out", str(out)], capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr
-    for line in ("Number of triangles: 45999", "Frame time (median):", "Rays per frame (primary+reflection+shadow):"):
-        assert line in r.stdout, line
     ref = np.load(os.path.join(GOLD, "car_boxed_160x90_strict.npz"))
-    assert out.read_bytes() == host.bmp_encode(ref["rgb"])
+    cache = tmp_path / "cache"
+    cache.mkdir()
+    for run in range(2):  # the second run reads triangles and BVH from the binary cache
+        out = tmp_path / f"car_boxed{run}.bmp"
+        r = subprocess.run([exe, "4", "--scene", "car_boxed", "--assets", assets, "--width", "160", "--height", "90",
+                            "--iterations", "3", "--out", str(out), "--cache", str(cache)], capture_output=True,
+                           text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        for line in ("Number of triangles: 45999", "Frame time (median):",
+                     "Rays per frame (primary+reflection+shadow):"):
+            assert line in r.stdout, line
+        assert out.read_bytes() == host.bmp_encode(ref["rgb"])
+    assert len(list(cache.iterdir())) == 2
+
+
+@pytest.mark.parametrize("name", ["car_boxed", "sportscar", "dragon"])
+def test_split_pipeline_equals_persistent_kernel(dev, name, monkeypatch):
+    """RT_KERNEL_FAST has two implementations (k_persist; closest/shadow/resolve split, chosen for >= 3
+    lights): both forced, on 1-, 4- and 2-light scenes, bit-exact to each other and to the fixtures,
+    with identical ray counts"""
+    s = host.Scene.named(name).build_bvh(3)
+    outs = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("PRT_SPLIT", v)
+        outs[v] = render(dev, s, 96, 54, "fast", counters=True)
+    a, b = outs["0"], outs["1"]
+    np.testing.assert_array_equal(a["hit"], b["hit"])
+    assert same_bits(a["t"], b["t"]) and same_bits(a["rgb"], b["rgb"])
+    for k in ("primary", "reflection", "shadow", "shadow_skipped", "hits", "pixels"):
+        assert a["stats"][k] == b["stats"][k], k
+    fx = f"{name}_96x54_strict.npz" if name != "car_boxed" else None
+    if fx:
+        ref = np.load(os.path.join(GOLD, fx))
+        assert same_bits(b["rgb"], ref["rgb"])

@@ -241,3 +241,38 @@ def test_wide_bvh_single_triangle():
     s = host.Scene.random(1).build_bvh("binned_sah")
     words, order, info = host.wbvh_build(s.nodes, s.tri_idx, s.triangles, 0.0)
     assert info["n_nodes"] == 1 and order.tolist() == [0]
+
+
+def test_scene_cache_returns_the_loaders_bytes(tmp_path):
+    """SURVEY §8f.2 binary cache: identical triangles and BVH (and RNG state after it) from the cache;
+    a changed source file or a damaged cache file is never trusted"""
+    import shutil
+    obj, mtl, lts = scene_paths("car_only")
+    o2, m2 = tmp_path / "t.obj", tmp_path / "t.mtl"
+    shutil.copy(obj, o2)
+    shutil.copy(mtl, m2)
+    cache = tmp_path / "tris.prtc"
+    ref = host.triangles_load(obj, mtl)
+    a = host.triangles_load(str(o2), str(m2), cache=cache)
+    assert not host.triangles_load.last_from_cache and cache.exists()
+    b = host.triangles_load(str(o2), str(m2), cache=cache)
+    assert host.triangles_load.last_from_cache
+    assert a.tobytes() == b.tobytes() == ref.tobytes()
+    with open(o2, "a") as f:  # stale: the OBJ changed
+        f.write("f 1 2 3\n")
+    c = host.triangles_load(str(o2), str(m2), cache=cache)
+    assert not host.triangles_load.last_from_cache and len(c) == len(ref) + 1
+    raw = bytearray(cache.read_bytes())  # damaged: one flipped payload byte
+    raw[100] ^= 0xFF
+    cache.write_bytes(bytes(raw))
+    d = host.triangles_load(str(o2), str(m2), cache=cache)
+    assert not host.triangles_load.last_from_cache and d.tobytes() == c.tobytes()
+    # the reference BVH (heuristic 3 consumes rand()): cached == built, RNG continues identically
+    bc = tmp_path / "bvh.prtc"
+    r1, r2, r3 = host.Rand(1), host.Rand(1), host.Rand(1)
+    n0, i0, _ = host.bvh_build(ref, 3, r1)
+    n1, i1, _, hit1 = host.bvh_build_cached(ref, 3, r2, bc)
+    n2, i2, _, hit2 = host.bvh_build_cached(ref, 3, r3, bc)
+    assert (hit1, hit2) == (False, True)
+    assert n0.tobytes() == n1.tobytes() == n2.tobytes() and i0.tobytes() == i2.tobytes()
+    assert r1.rand() == r2.rand() == r3.rand()

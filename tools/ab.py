@@ -33,10 +33,14 @@ def main():
     rays = {}
     pixels = {}
 
+    base_env = {k: v for k, v in os.environ.items() if k.startswith("PRT_")}  # the caller's knobs persist
+
     def setenv(v):
         parts = v.split(":")
-        for k in [k for k in os.environ if k.startswith("PRT_") and k != "PRT_SCENE_CACHE"]:
+        for k in [k for k in os.environ if k.startswith("PRT_") and k not in base_env]:
             os.environ.pop(k)
+        for k, val in base_env.items():
+            os.environ[k] = val
         if len(parts) > 1:
             for kv in parts[1].split(","):
                 k, val = kv.split("=")

@@ -81,6 +81,16 @@ for s in "${@:-smoke pytest bench}"; do
       abprio) run abprio 300 python tools/ab.py --rounds 4 --frames 5 fast fast:PRT_PRIO=1
               run abpriocar 300 python tools/ab.py --scene car_boxed --rounds 4 --frames 5 fast fast:PRT_PRIO=1
               run abpriosc 300 python tools/ab.py --scene sportscar --rounds 3 --frames 5 fast fast:PRT_PRIO=1 ;;
+      pytestsplit) PRT_SPLIT=1 run pytest_split 1200 python -m pytest tests -m gpu -q ;;
+      absplit) run absplit 300 python tools/ab.py --rounds 4 --frames 5 fast fast:PRT_SPLIT=1
+              run absplitcar 300 python tools/ab.py --scene car_boxed --rounds 4 --frames 5 fast fast:PRT_SPLIT=1
+              run absplitsc 300 python tools/ab.py --scene sportscar --rounds 3 --frames 5 fast fast:PRT_SPLIT=1 ;;
+      profsplit) PRT_SPLIT=1 run profsplit 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profsplit -o run --output-format csv -- python3 tools/ab.py --rounds 1 --frames 5 fast
+              PRT_SPLIT=1 run profsplitcar 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profsplitcar -o run --output-format csv -- python3 tools/ab.py --scene car_boxed --rounds 1 --frames 5 fast ;;
+      abtri)  for sc in dragon car_boxed sportscar; do
+                  run abtri_$sc 300 python tools/ab.py --scene $sc --rounds 3 --frames 5 fast fast:PRT_SPLIT=1
+                  PRT_LIB_DIR=build/old/lib run abtriold_$sc 300 python tools/ab.py --scene $sc --rounds 3 --frames 5 fast
+              done ;;
       *) echo "unknown step $step"; exit 2 ;;
     esac
   done
