@@ -129,6 +129,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from prt import device, host
+    from prt.dist import FrameGather
     from prt.scenes import is_standin, scene_paths
 
     W, H = args.width, args.height
@@ -138,23 +139,16 @@ def main():
     r = device.Renderer(local, stream=stream)
     r.upload(scene, accel=args.accel)
     cam = host.camera(W, H)
-    n_r = (H - rank + world - 1) // world  # cyclic rows: y = rank + k * world
-    n_max = (H + world - 1) // world
-    out = torch.zeros((n_max, W, 3), dtype=torch.float32, device="cuda")
-    frame = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda") if rank == 0 else None
-    parts = [torch.empty_like(out) for _ in range(world)] if (rank == 0 and world > 1) else None
+    # cyclic rows y = rank + k * world, gathered to rank 0 with one RCCL collective (prt/dist.py, tested
+    # with gloo in tests/test_multi.py)
+    fg = FrameGather(H, W, 3, rank, world, dist, like=torch.empty(0, dtype=torch.float32, device="cuda"))
+    _, _, n_r = fg.rows()
+    out = fg.block
 
     def step():
         r.render(cam, W, H, rows=(rank, world, n_r), bounces=args.bounces, spp=args.spp, kernel=args.kernel,
                  rgb=out)
-        if world > 1:
-            dist.gather(out, parts, dst=0)
-            if rank == 0:
-                for q in range(world):
-                    nq = (H - q + world - 1) // world
-                    frame[q::world] = parts[q][:nq]
-        elif rank == 0:
-            frame.copy_(out)
+        fg.gather()
 
     for _ in range(args.warmup):
         step()

@@ -83,6 +83,13 @@ struct KArgs {
     size_t nslots;
 };
 
+// Kernel arguments are laid out by the host compiler and read by the device compiler: both passes must
+// agree on every offset (an LDS pointer, 32-bit on gfx950 but 64-bit on the host, once shifted every
+// later field and hung a kernel). Pinned sizes catch such drift at compile time in whichever pass
+// disagrees; never put address-space-qualified pointers in these structs.
+static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 144 && sizeof(KArgs) == 344,
+              "kernel-argument layout changed: update the pinned sizes only after checking both passes agree");
+
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)
 struct v3 {
     float x, y, z;

@@ -48,6 +48,9 @@ struct WfArgs {
     int refill_below;
     int chunk_min, chunk_max;  // guided self-scheduling window bounds (entries per claim)
 };
+static_assert(sizeof(WfArgs) == 352, "kernel-argument layout changed (see rt_device.hpp)");
+
+
 
 __device__ __forceinline__ void ray_store(float4* q, unsigned e, v3 o, v3 d, int tag, float w) {
     q[2 * e] = make_float4(o.x, o.y, o.z, __int_as_float(tag));

@@ -78,3 +78,32 @@ def test_cyclic_partition_covers_every_row_once():
                 assert nr <= padded_rows(H, N)
                 seen += [ro + k * rs for k in range(nr)]
             assert sorted(seen) == list(range(H))
+
+
+def _prepare(cache, q):
+    import hashlib
+    import os
+    os.environ["PRT_SCENE_CACHE"] = cache
+    import importlib
+    import prt.scenes as sc
+    importlib.reload(sc)
+    obj = sc.scene_paths("dragon")[0]
+    q.put(hashlib.md5(open(obj, "rb").read()).hexdigest())
+
+
+def test_concurrent_ranks_prepare_one_scene_cache(tmp_path):
+    """the ranks of a multi-GPU run build the same stand-in at once: the cache lock makes them agree
+    on one complete file (md5 pinned in tests/golden/golden.json)"""
+    import json
+    import multiprocessing as mp
+    import os
+    G = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_prepare, args=(str(tmp_path / "cache"), q)) for _ in range(4)]
+    for p in ps:
+        p.start()
+    got = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    assert len(set(got)) == 1 and got[0] == G["standin"]["dragon"]["obj_md5"]

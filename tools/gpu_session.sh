@@ -91,6 +91,10 @@ for s in "${@:-smoke pytest bench}"; do
                   run abtri_$sc 300 python tools/ab.py --scene $sc --rounds 3 --frames 5 fast fast:PRT_SPLIT=1
                   PRT_LIB_DIR=build/old/lib run abtriold_$sc 300 python tools/ab.py --scene $sc --rounds 3 --frames 5 fast
               done ;;
+      abwc)   for sc in dragon car_boxed sportscar; do
+                  run abwc_$sc 300 python tools/ab.py --scene $sc --rounds 3 --frames 5 fast fast:PRT_WCACHE=0 fast:PRT_WCACHE=9
+                  PRT_LIB_DIR=build/old/lib run abwcold_$sc 300 python tools/ab.py --scene $sc --rounds 3 --frames 5 fast
+              done ;;
       *) echo "unknown step $step"; exit 2 ;;
     esac
   done
