@@ -16,6 +16,8 @@
 // (bit 0 = +x, bit 1 = +y, bit 2 = +z), so that a ray visiting slots in the order k ^ octant(ray)
 // for k = 0..7 meets them roughly front to back without sorting.
 #include <algorithm>
+#include <array>
+#include <cstdlib>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -111,8 +113,73 @@ struct WBuilder {
         x.r = r;
         x.b = bn[l].b;
         grow(x.b, bn[r].b);
+        // the subtree's triangles as one range of idx (every reference-layout builder partitions in place);
+        // cnt = -1: not contiguous, never merged into one leaf
+        const BNode &L = bn[l], &R = bn[r];
+        if (L.cnt >= 0 && R.cnt >= 0 && (L.first + L.cnt == R.first || R.first + R.cnt == L.first)) {
+            x.first = std::min(L.first, R.first);
+            x.cnt = L.cnt + R.cnt;
+        } else {
+            x.cnt = -1;
+        }
         bn.push_back(x);
         return (int)bn.size() - 1;
+    }
+
+    // ---- SAH-optimal collapse (Ylitie et al. 2017, §3.1): cost(n, i) = cheapest way to hang subtree n
+    // off a parent using at most i slots — as one leaf slot (<= LEAF_MAX triangles), as one wide node,
+    // or by distributing the slots over n's two children. Costs are surface area x (C_node per wide-node
+    // visit, 1 per triangle test).
+    std::vector<std::array<float, WIDTH + 1>> cost;
+    std::vector<std::array<signed char, WIDTH + 1>> split;  // dist(n, i): slots given to the left child
+    std::vector<char> as_leaf;                               // cost(n, 1) is the leaf form
+    void sah_costs(float c_node) {
+        const size_t N = bn.size();
+        cost.assign(N, {});
+        split.assign(N, {});
+        as_leaf.assign(N, 0);
+        std::vector<std::array<float, WIDTH + 1>> dist(N);
+        for (size_t n = 0; n < N; n++) {  // children precede parents in bn
+            const BNode& B = bn[n];
+            const float A = area(B.b);
+            const float leaf = (B.cnt > 0 && B.cnt <= LEAF_MAX) ? A * (float)B.cnt : INFINITY;
+            if (B.l < 0) {
+                for (int i = 1; i <= WIDTH; i++) {
+                    cost[n][i] = leaf;
+                    dist[n][i] = leaf;
+                }
+                as_leaf[n] = 1;
+                continue;
+            }
+            for (int j = 2; j <= WIDTH; j++) {
+                float best = INFINITY;
+                int bk = 1;
+                for (int k = 1; k < j; k++) {
+                    const float c = cost[B.l][k] + cost[B.r][j - k];
+                    if (c < best) {
+                        best = c;
+                        bk = k;
+                    }
+                }
+                dist[n][j] = best;
+                split[n][j] = (signed char)bk;
+            }
+            const float node = c_node * A + dist[n][WIDTH];
+            as_leaf[n] = leaf <= node;
+            cost[n][1] = std::min(leaf, node);
+            for (int i = 2; i <= WIDTH; i++) cost[n][i] = std::min(cost[n][1], dist[n][i]);
+        }
+    }
+    // the slots of subtree n given i of them: (bnode, as-leaf) pairs
+    void collect(int n, int i, std::vector<std::pair<int, bool>>& out) const {
+        const BNode& B = bn[n];
+        if (B.l < 0 || i == 1 || cost[n][i] == cost[n][1]) {
+            out.push_back({n, B.l < 0 || as_leaf[n] != 0});
+            return;
+        }
+        const int k = split[n][i];
+        collect(B.l, k, out);
+        collect(B.r, i - k, out);
     }
 
     // reference-layout node i -> BNode index (-1: empty subtree)
@@ -195,6 +262,12 @@ extern "C" int rth_wbvh_build(const rt_bvh_node* bvh, int n_nodes, const int* tr
     bool bad = false;
     const int root = w.make(bvh, n_nodes, 0, 0, bad);
     if (bad || root < 0) return RT_E_ARG;
+    // collapse policy: SAH-optimal (default) or greedy largest-area (PRT_WIDE_COLLAPSE=greedy, A/B);
+    // PRT_WIDE_CNODE: cost of a wide-node visit in triangle tests (default 4: ~250 vs ~60 VALU)
+    const char* ce = std::getenv("PRT_WIDE_COLLAPSE");
+    const bool sah = !(ce && std::strcmp(ce, "greedy") == 0);
+    const char* cn = std::getenv("PRT_WIDE_CNODE");
+    if (sah) w.sah_costs(cn ? (float)std::atof(cn) : 4.0f);
 
     // breadth-first: interior children of a wide node get consecutive indices
     struct Item {
@@ -209,11 +282,20 @@ extern "C" int rth_wbvh_build(const rt_bvh_node* bvh, int n_nodes, const int* tr
         const Item it = queue[qi];
         depth = std::max(depth, it.depth);
         const BNode& B = w.bn[it.b];
-        // children: open the largest-area interior child until WIDTH
         std::vector<int> kids;
-        if (B.l < 0) {
+        std::vector<char> kid_leaf;
+        if (B.l < 0 || (sah && w.as_leaf[it.b])) {
             kids.push_back(it.b);  // a leaf root
-        } else {
+            kid_leaf.push_back(1);
+        } else if (sah) {  // the cost-optimal distribution of this node's 8 slots
+            std::vector<std::pair<int, bool>> c2;
+            w.collect(B.l, w.split[it.b][WIDTH], c2);
+            w.collect(B.r, WIDTH - w.split[it.b][WIDTH], c2);
+            for (auto& pr : c2) {
+                kids.push_back(pr.first);
+                kid_leaf.push_back(pr.second ? 1 : 0);
+            }
+        } else {  // greedy: open the largest-area interior child until WIDTH
             kids = {B.l, B.r};
             while ((int)kids.size() < WIDTH) {
                 int best = -1;
@@ -228,6 +310,7 @@ extern "C" int rth_wbvh_build(const rt_bvh_node* bvh, int n_nodes, const int* tr
                 kids[best] = w.bn[o].l;
                 kids.push_back(w.bn[o].r);
             }
+            for (int c : kids) kid_leaf.push_back(w.bn[c].l < 0 ? 1 : 0);
         }
         const int k = (int)kids.size();
         max_kids = std::max(max_kids, k);
@@ -288,7 +371,7 @@ extern "C" int rth_wbvh_build(const rt_bvh_node* bvh, int n_nodes, const int* tr
         W[2] = f2u(p[2]);
         uint32_t imask = 0;
         for (int s = 0; s < WIDTH; s++)
-            if (kid_in[s] >= 0 && w.bn[kids[kid_in[s]]].l >= 0) imask |= 1u << s;
+            if (kid_in[s] >= 0 && !kid_leaf[kid_in[s]]) imask |= 1u << s;
         W[3] = (uint32_t)eb[0] | ((uint32_t)eb[1] << 8) | ((uint32_t)eb[2] << 16) | (imask << 24);
         const int child_base = (int)queue.size();
         const int tri_base = (int)order.size();
@@ -309,7 +392,7 @@ extern "C" int rth_wbvh_build(const rt_bvh_node* bvh, int n_nodes, const int* tr
                 q8[3 + a][s] = (uint8_t)qhi[a][j];
             }
             const BNode& c = w.bn[kids[kid_in[s]]];
-            if (c.l >= 0) {
+            if (!kid_leaf[kid_in[s]]) {
                 queue.push_back({kids[kid_in[s]], it.depth + 1});
             } else {
                 const int off = (int)order.size() - tri_base;

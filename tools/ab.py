@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--H", type=int, default=1080)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=5)
+    ap.add_argument("--reupload", action="store_true", help="rebuild the scene per variant (knobs read at upload)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
@@ -51,6 +52,8 @@ def main():
     for rnd in range(a.rounds + 1):
         for v in a.variants:
             kern = setenv(v)
+            if a.reupload:
+                r.upload(s)
             for _ in range(a.frames):
                 r.render(cam, a.W, a.H, kernel=kern, rgb=rgb)
             ts = r.kernel_times(a.frames)

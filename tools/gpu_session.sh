@@ -95,6 +95,13 @@ for s in "${@:-smoke pytest bench}"; do
                   run abwc_$sc 300 python tools/ab.py --scene $sc --rounds 3 --frames 5 fast fast:PRT_WCACHE=0 fast:PRT_WCACHE=9
                   PRT_LIB_DIR=build/old/lib run abwcold_$sc 300 python tools/ab.py --scene $sc --rounds 3 --frames 5 fast
               done ;;
+      abcol)  for sc in dragon car_boxed sportscar; do
+                  run abcol_$sc 300 python tools/ab.py --scene $sc --reupload --rounds 3 --frames 5 fast fast:PRT_WIDE_COLLAPSE=greedy fast:PRT_WIDE_CNODE=2 fast:PRT_WIDE_CNODE=8
+              done
+              run ctrscol 300 python tools/counters.py dragon fast ;;
+      abcn)   for sc in dragon car_boxed; do
+                  run abcn_$sc 300 python tools/ab.py --scene $sc --reupload --rounds 6 --frames 5 fast:PRT_WIDE_CNODE=2 fast:PRT_WIDE_CNODE=3 fast fast:PRT_WIDE_COLLAPSE=greedy
+              done ;;
       *) echo "unknown step $step"; exit 2 ;;
     esac
   done
