@@ -100,6 +100,20 @@ struct rt_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // the last launch's pair
     long long launches = 0;
     bool rendered = false;
+    // launch autotuning of RT_KERNEL_FAST (rt_render): the candidate configurations are timed on the
+    // first frame of a (scene upload, frame shape) and the fastest one renders the frames after it
+    static constexpr int TUNE_MAX = 3, TUNE_REPS = 3;
+    struct Tune {
+        long long scene = -1;
+        int W = 0, rows = 0, bounces = 0, spp = 0;
+        int n = 0, choice = -1;  // candidates; the chosen one (-1: not decided yet)
+        bool pending = false;    // trial launches enqueued, timings not read yet
+        bool split[TUNE_MAX] = {};
+        int cap[TUNE_MAX] = {};
+        float ms[TUNE_MAX] = {};
+        hipEvent_t e0[TUNE_MAX * TUNE_REPS] = {}, e1[TUNE_MAX * TUNE_REPS] = {};
+    } tune;
+    long long scene_gen = 0;  // bumped by every upload
 };
 
 namespace {
@@ -382,6 +396,7 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     ctx->amb[1] = sc->amb.y;
     ctx->amb[2] = sc->amb.z;
     ctx->has_scene = true;
+    ctx->scene_gen++;
     return RT_OK;
 }
 
@@ -389,17 +404,23 @@ namespace {
 
 // resident workgroups per CU of a persistent kernel (occupancy API, capped at 8)
 template <class K>
-int resident(K kernel, int device) {
+int resident(K kernel, int device, int cap = 8) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, rtd::BLOCK, 0) != hipSuccess || per_cu < 1)
         per_cu = 1;
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    return std::min(per_cu, 8) * cus;
+    return std::max(1, std::min(per_cu, cap)) * cus;
+}
+
+// per-CU block cap from the environment (A/B knobs), else `def`
+int env_cap(const char* name, int def) {
+    const char* e = std::getenv(name);
+    return e && std::atoi(e) > 0 ? std::atoi(e) : def;
 }
 
 template <int MAXB>
-void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int device, hipStream_t s) {
+void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int device, hipStream_t s, int cap) {
     if (kernel == RT_KERNEL_STRICT) {
         if (count) rtd::k_tiles<MAXB, true, true><<<grid_tiles, rtd::BLOCK, 0, s>>>(A);
         else rtd::k_tiles<MAXB, true, false><<<grid_tiles, rtd::BLOCK, 0, s>>>(A);
@@ -418,7 +439,7 @@ void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int de
             kr<<<blocks, rtd::BLOCK, 0, s>>>(A);
             return;
         }
-        int blocks = std::max(1, std::min(resident(k, device), (A.n_tiles + 3) / 4));
+        int blocks = std::max(1, std::min(resident(k, device, cap), (A.n_tiles + 3) / 4));
         k<<<blocks, rtd::BLOCK, 0, s>>>(A);
     } else {
         const char* ev = std::getenv("PRT_WAVE_VARIANT");  // "4": the 128-VGPR build (A/B knob)
@@ -552,7 +573,7 @@ int launch_wf(rt_ctx* ctx, const rtd::KArgs& K, bool count) {
 
 namespace {
 template <int MAXB>
-int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count);  // below
+int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count, int cap_a);  // below
 }  // namespace
 
 extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, const rt_outputs* out) {
@@ -629,11 +650,9 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     const bool count = (ctx->flags & RT_FLAG_COUNTERS) != 0;
     dim3 grid((f->width + 15) / 16, (f->n_rows + 15) / 16);
     HIPC(hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT, ctx->stream));
-    HIPC(hipMemsetAsync(ctx->d_work, 0, 1024, ctx->stream));
     const int slot = (int)(ctx->launches % rt_ctx::NEV);
     ctx->ev0 = ctx->ev0s[slot];
     ctx->ev1 = ctx->ev1s[slot];
-    HIPC(hipEventRecord(ctx->ev0, ctx->stream));
     // diagnostics: PRT_TILE_TRACE=<file> writes 4 x uint64 per tile of a k_persist frame (rt_kernels.hpp)
     // (s_memrealtime, 100 MHz); synchronous, never used by tests or the bench
     const char* trace_path = std::getenv("PRT_TILE_TRACE");
@@ -668,22 +687,103 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
         }
         A.tile_order = ctx->d_order;
     }
-    // RT_KERNEL_FAST at 1 spp: k_persist, or the split pipeline (rt_split.hpp) when shadow rays dominate a
-    // tile's chain. Same-box A/B: 1 light +49 % time, 2 lights +7 %, 4 lights -21 % with the
-    // split, so it takes scenes with >= 3 lights. PRT_SPLIT=0/1 forces either.
+    // RT_KERNEL_FAST: k_persist, or at 1 spp the split pipeline (rt_split.hpp), each a persistent grid of
+    // up to `cap` waves per SIMD. Which is fastest depends on the scene (same-box A/B): dragon
+    // wants k_persist at its full 3 waves/SIMD, car_boxed k_persist at 2 (-15 %: fewer incoherent
+    // reflection chains in flight thrash the caches less), sportscar (4 lights) the split pipeline at 2.
+    // Every configuration renders the same bits, so the context measures: the first frame of a
+    // (scene, frame shape) runs each candidate TUNE_REPS times (all into the same outputs), the next
+    // frame reads the timings and keeps the fastest. PRT_TUNE=0 (or forcing a configuration through
+    // PRT_SPLIT / PRT_PERSIST_CAP / PRT_SPLIT_OCC_A) disables it; PRT_TUNE_LOG=1 prints the timings.
     const char* split_env = std::getenv("PRT_SPLIT");
+    const char* cap_env = std::getenv("PRT_PERSIST_CAP");
+    const char* occa_env = std::getenv("PRT_SPLIT_OCC_A");
+    const char* tune_env = std::getenv("PRT_TUNE");
     const bool split_ok = kernel == RT_KERNEL_FAST && f->spp == 1 && ctx->n_lights <= 32 && !A.tile_trace;
-    const bool split = split_ok && (split_env ? std::atoi(split_env) == 1 : ctx->n_lights >= 3);
-    if (split) {
-        const int rc = f->bounces <= 4 ? launch_split<4>(ctx, A, count) : launch_split<8>(ctx, A, count);
-        if (rc) return rc;
-    } else if (kernel == RT_KERNEL_WAVEFRONT) {
-        const int rc = launch_wf(ctx, A, count);
-        if (rc) return rc;
-    } else if (f->bounces <= 4) {
-        launch<4>(A, kernel, count, grid, ctx->device, ctx->stream);
+    bool split = split_ok && (split_env ? std::atoi(split_env) == 1 : ctx->n_lights >= 3);
+    int cap = split ? env_cap("PRT_SPLIT_OCC_A", 2) : env_cap("PRT_PERSIST_CAP", 8);
+    const bool tunable = kernel == RT_KERNEL_FAST && !A.tile_trace && !split_env && !cap_env && !occa_env &&
+                         !(tune_env && std::atoi(tune_env) == 0);
+    rt_ctx::Tune& T = ctx->tune;
+    bool trial = false;
+    if (tunable) {
+        if (T.scene != ctx->scene_gen || T.W != f->width || T.rows != f->n_rows || T.bounces != f->bounces ||
+            T.spp != f->spp) {
+            T.scene = ctx->scene_gen;
+            T.W = f->width;
+            T.rows = f->n_rows;
+            T.bounces = f->bounces;
+            T.spp = f->spp;
+            T.n = 0;
+            T.choice = -1;
+            T.pending = false;
+            const bool sp[3] = {false, false, true};
+            const int cp[3] = {8, 2, 2};
+            for (int i = 0; i < 3; i++)
+                if (!sp[i] || (split_ok && ctx->n_lights >= 1)) {
+                    T.split[T.n] = sp[i];
+                    T.cap[T.n] = cp[i];
+                    T.n++;
+                }
+        }
+        if (T.pending) {
+            HIPC(hipEventSynchronize(T.e1[T.n * rt_ctx::TUNE_REPS - 1]));
+            int best = 0;
+            for (int c = 0; c < T.n; c++) {
+                float m = 1e30f;
+                for (int r = 0; r < rt_ctx::TUNE_REPS; r++) {
+                    float ms = 0.0f;
+                    HIPC(hipEventElapsedTime(&ms, T.e0[r * T.n + c], T.e1[r * T.n + c]));
+                    m = std::min(m, ms);
+                }
+                T.ms[c] = m;
+                if (m < T.ms[best]) best = c;
+            }
+            T.choice = best;
+            T.pending = false;
+            if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1) {
+                std::fprintf(stderr, "[prt tune] %dx%d b%d spp%d:", T.W, T.rows, T.bounces, T.spp);
+                for (int c = 0; c < T.n; c++)
+                    std::fprintf(stderr, " %s/%d %.3f ms", T.split[c] ? "split" : "persist", T.cap[c], T.ms[c]);
+                std::fprintf(stderr, " -> %d\n", best);
+            }
+        } else if (T.choice < 0) {
+            trial = !count;  // counters would add up over the trial launches: such a frame keeps the default
+        }
+        if (T.choice >= 0) {
+            split = T.split[T.choice];
+            cap = T.cap[T.choice];
+        }
+    }
+    // one frame of configuration (split, cap); d_work holds the persistent grids' work counters
+    auto dispatch = [&](bool sp, int cp) -> int {
+        HIPC(hipMemsetAsync(ctx->d_work, 0, 1024, ctx->stream));
+        if (sp) return f->bounces <= 4 ? launch_split<4>(ctx, A, count, cp) : launch_split<8>(ctx, A, count, cp);
+        if (kernel == RT_KERNEL_WAVEFRONT) return launch_wf(ctx, A, count);
+        if (f->bounces <= 4) launch<4>(A, kernel, count, grid, ctx->device, ctx->stream, cp);
+        else launch<8>(A, kernel, count, grid, ctx->device, ctx->stream, cp);
+        return RT_OK;
+    };
+    if (trial) {
+        const int nt = T.n * rt_ctx::TUNE_REPS;
+        for (int i = 0; i < nt; i++) {
+            if (!T.e0[i]) HIPC(hipEventCreate(&T.e0[i]));
+            if (!T.e1[i]) HIPC(hipEventCreate(&T.e1[i]));
+        }
+        for (int i = 0; i < nt; i++) {
+            const int c = i % T.n;
+            if (i == nt - 1) HIPC(hipEventRecord(ctx->ev0, ctx->stream));
+            HIPC(hipEventRecord(T.e0[i], ctx->stream));
+            const int rc = dispatch(T.split[c], T.cap[c]);
+            if (rc) return rc;
+            HIPC(hipGetLastError());
+            HIPC(hipEventRecord(T.e1[i], ctx->stream));
+        }
+        T.pending = true;
     } else {
-        launch<8>(A, kernel, count, grid, ctx->device, ctx->stream);
+        HIPC(hipEventRecord(ctx->ev0, ctx->stream));
+        const int rc = dispatch(split, cap);
+        if (rc) return rc;
     }
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(ctx->ev1, ctx->stream));
@@ -770,7 +870,7 @@ int grow(rt_ctx* ctx, T** p, size_t& cap, size_t n) {
 namespace {
 // the split pipeline (rt_split.hpp): closest chains, shadow batches, resolve — three launches
 template <int MAXB>
-int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count) {
+int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count, int cap_a) {
     const int nl = A.s.n_lights;
     A.nslots = (size_t)A.n_tiles * 64;
     int rc;
@@ -786,8 +886,9 @@ int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count) {
     hipStream_t s = ctx->stream;
     auto ka = count ? rtd::k_split_closest<MAXB, true> : rtd::k_split_closest<MAXB, false>;
     auto kb = count ? rtd::k_split_shadow<true> : rtd::k_split_shadow<false>;
-    const int ga = std::max(1, std::min(resident(ka, ctx->device), (A.n_tiles + 3) / 4));
-    const int gb = std::max(1, resident(kb, ctx->device));
+    // persistent grids; a block is one wave per SIMD, so the cap is waves per SIMD
+    const int ga = std::max(1, std::min(resident(ka, ctx->device, cap_a), (A.n_tiles + 3) / 4));
+    const int gb = std::max(1, resident(kb, ctx->device, env_cap("PRT_SPLIT_OCC_B", 8)));
     ka<<<ga, rtd::BLOCK, 0, s>>>(A);
     kb<<<gb, rtd::BLOCK, 0, s>>>(A);
     rtd::k_split_resolve<MAXB><<<(int)((A.nslots + 255) / 256), 256, 0, s>>>(A);
@@ -939,6 +1040,10 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     for (int i = 0; i < rt_ctx::NEV; i++) {
         if (ctx->ev0s[i]) (void)hipEventDestroy(ctx->ev0s[i]);
         if (ctx->ev1s[i]) (void)hipEventDestroy(ctx->ev1s[i]);
+    }
+    for (int i = 0; i < rt_ctx::TUNE_MAX * rt_ctx::TUNE_REPS; i++) {
+        if (ctx->tune.e0[i]) (void)hipEventDestroy(ctx->tune.e0[i]);
+        if (ctx->tune.e1[i]) (void)hipEventDestroy(ctx->tune.e1[i]);
     }
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

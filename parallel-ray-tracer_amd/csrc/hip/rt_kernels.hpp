@@ -312,9 +312,7 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
     const unsigned lx[2] = {__float_as_uint(f2.x), __float_as_uint(f2.y)}, ly[2] = {__float_as_uint(f2.z), __float_as_uint(f2.w)},
                    lz[2] = {__float_as_uint(f3.x), __float_as_uint(f3.y)}, hx[2] = {__float_as_uint(f3.z), __float_as_uint(f3.w)},
                    hy[2] = {__float_as_uint(f4.x), __float_as_uint(f4.y)}, hz[2] = {__float_as_uint(f4.z), __float_as_uint(f4.w)};
-    nh = 0;
-    th = 0;
-    nleaf = 0;
+    unsigned hit8 = 0;  // bit s: child slot s entered within [0, lim]
 #pragma unroll
     for (int s = 0; s < 8; s++) {
         const int h = s >> 2, b = s & 3;
@@ -329,13 +327,26 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
         // folded test max(tmin, 0) <= min(tmax, lim) only adds visits (e.g. tmax == 0): conservative.
         const float lo = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f));
         const float hi = fminf(fminf(tfx, tfy), fminf(tfz, lim));
-        const unsigned hm = lo <= hi ? ~0u : 0u;
-        const unsigned ib = (imask >> s) & 1u;
-        const unsigned meta = (m[h] >> (8 * b)) & 0xFFu;  // leaf: count << 5 | offset; 0 for empty / interior
-        nh |= hm & (0u - ib) & (1u << (s ^ oct));
-        const unsigned lb = hm & (ib - 1u) & (((1u << (meta >> 5)) - 1u) << (meta & 31u));
-        th |= lb;
-        if (COUNT) nleaf += lb ? 1u : 0u;
+        hit8 |= lo <= hi ? (1u << s) : 0u;
+    }
+    // interior hits, permuted into visiting order: bit k = slot k ^ oct (XOR by oct swaps bits, pairs and
+    // nibbles of the 8-bit mask)
+    unsigned x = hit8 & imask;
+    x = (oct & 1u) ? (((x & 0x55u) << 1) | ((x >> 1) & 0x55u)) : x;
+    x = (oct & 2u) ? (((x & 0x33u) << 2) | ((x >> 2) & 0x33u)) : x;
+    x = (oct & 4u) ? (((x & 0x0Fu) << 4) | ((x >> 4) & 0x0Fu)) : x;
+    nh = x;
+    // triangles of the hit leaf slots (meta = count << 5 | offset; an empty slot's inverted box never
+    // passes the test above except through underflow, and its meta 0 adds nothing then)
+    unsigned lh = hit8 & ~imask;
+    th = 0;
+    nleaf = 0;
+    while (lh) {
+        const unsigned sl = (unsigned)__builtin_ctz(lh);
+        lh &= lh - 1u;
+        const unsigned meta = (m[sl >> 2] >> (8u * (sl & 3u))) & 0xFFu;
+        th |= ((1u << (meta >> 5)) - 1u) << (meta & 31u);
+        if (COUNT) nleaf += meta ? 1u : 0u;
     }
 }
 

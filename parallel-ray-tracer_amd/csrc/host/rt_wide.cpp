@@ -263,11 +263,12 @@ extern "C" int rth_wbvh_build(const rt_bvh_node* bvh, int n_nodes, const int* tr
     const int root = w.make(bvh, n_nodes, 0, 0, bad);
     if (bad || root < 0) return RT_E_ARG;
     // collapse policy: SAH-optimal (default) or greedy largest-area (PRT_WIDE_COLLAPSE=greedy, A/B);
-    // PRT_WIDE_CNODE: cost of a wide-node visit in triangle tests (default 4: ~250 vs ~60 VALU)
+    // PRT_WIDE_CNODE: cost of a wide-node visit in triangle tests (default 2: the best of 2/3/4 in the
+    // measured sweep — dragon -3.5 % vs 4, car_boxed even)
     const char* ce = std::getenv("PRT_WIDE_COLLAPSE");
     const bool sah = !(ce && std::strcmp(ce, "greedy") == 0);
     const char* cn = std::getenv("PRT_WIDE_CNODE");
-    if (sah) w.sah_costs(cn ? (float)std::atof(cn) : 4.0f);
+    if (sah) w.sah_costs(cn ? (float)std::atof(cn) : 2.0f);
 
     // breadth-first: interior children of a wide node get consecutive indices
     struct Item {

@@ -329,3 +329,30 @@ def test_split_pipeline_equals_persistent_kernel(dev, name, monkeypatch):
     if fx:
         ref = np.load(os.path.join(GOLD, fx))
         assert same_bits(b["rgb"], ref["rgb"])
+
+
+@pytest.mark.parametrize("name,n_cand", [("sportscar", 3), ("car_boxed", 3), ("dragon", 3)])
+def test_autotuned_frames_equal_forced_configuration(dev, name, n_cand, monkeypatch, capfd):
+    """rt_render's launch autotuner (rt_hip.hip, RT_KERNEL_FAST): the trial frame (every candidate, each
+    TUNE_REPS times, into the same outputs) and the frames after the decision are bit-exact to a forced
+    k_persist frame; the decision is logged once, over all candidates"""
+    import torch
+    s = host.Scene.named(name).build_bvh(3)
+    W, H = 96, 54
+    monkeypatch.setenv("PRT_SPLIT", "0")
+    ref = render(dev, s, W, H, "fast")
+    monkeypatch.delenv("PRT_SPLIT")
+    monkeypatch.setenv("PRT_TUNE_LOG", "1")
+    r = dev.Renderer(0)
+    r.upload(s)
+    for frame in range(3):
+        hit = torch.full((H, W), -7, dtype=torch.int32, device="cuda")
+        t = torch.zeros((H, W), dtype=torch.float32, device="cuda")
+        rgb = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
+        r.render(host.camera(W, H), W, H, kernel="fast", rgb=rgb, hit=hit, t=t)
+        r.sync()
+        np.testing.assert_array_equal(hit.cpu().numpy(), ref["hit"])
+        assert same_bits(t.cpu().numpy(), ref["t"]) and same_bits(rgb.cpu().numpy(), ref["rgb"]), frame
+    r.close()
+    log = [l for l in capfd.readouterr().err.splitlines() if l.startswith("[prt tune]")]
+    assert len(log) == 1 and log[0].count(" ms") == n_cand, log

@@ -102,6 +102,30 @@ for s in "${@:-smoke pytest bench}"; do
       abcn)   for sc in dragon car_boxed; do
                   run abcn_$sc 300 python tools/ab.py --scene $sc --reupload --rounds 6 --frames 5 fast:PRT_WIDE_CNODE=2 fast:PRT_WIDE_CNODE=3 fast fast:PRT_WIDE_COLLAPSE=greedy
               done ;;
+      abbits) for i in 1 2; do for sc in dragon car_boxed sportscar; do
+                  run abbits_${sc}_$i 300 python tools/ab.py --scene $sc --rounds 3 --frames 5 fast
+                  PRT_LIB_DIR=build/old/lib run abbitsold_${sc}_$i 300 python tools/ab.py --scene $sc --rounds 3 --frames 5 fast
+              done; done ;;
+      abbits3) for i in 1 2; do for sc in dragon car_boxed sportscar; do
+                  run ab3u_${sc}_$i 300 python tools/ab.py --scene $sc --rounds 3 --frames 5 fast
+                  PRT_LIB_DIR=build/loop/lib run ab3l_${sc}_$i 300 python tools/ab.py --scene $sc --rounds 3 --frames 5 fast
+                  PRT_LIB_DIR=build/old/lib run ab3o_${sc}_$i 300 python tools/ab.py --scene $sc --rounds 3 --frames 5 fast
+              done; done ;;
+      absc)   for L in parallel-ray-tracer_amd/lib build/old/lib; do
+                  t=$(basename $(dirname $L))
+                  PRT_LIB_DIR=$L run absc_$t 300 python tools/ab.py --scene sportscar --rounds 3 --frames 5 fast fast:PRT_SPLIT=0
+                  PRT_LIB_DIR=$L run profsc_$t 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profsc_$t -o run --output-format csv -- python3 tools/ab.py --scene sportscar --rounds 1 --frames 5 fast
+              done ;;
+      absocc) run abocc_sportscar 300 python tools/ab.py --scene sportscar --rounds 4 --frames 5 fast fast:PRT_SPLIT_OCC_A=3 fast:PRT_SPLIT_OCC_A=2 fast:PRT_SPLIT_OCC_B=3 fast:PRT_SPLIT_OCC_B=2 fast:PRT_SPLIT_OCC_A=3,PRT_SPLIT_OCC_B=3
+              run abocc_car 300 python tools/ab.py --scene car_boxed --rounds 3 --frames 5 fast:PRT_SPLIT=1 fast:PRT_SPLIT=1,PRT_SPLIT_OCC_A=3 fast:PRT_SPLIT=1,PRT_SPLIT_OCC_A=2
+              PRT_LIB_DIR=build/old/lib run abocc_old 300 python tools/ab.py --scene sportscar --rounds 4 --frames 5 fast ;;
+      abcap)  run abcap_sportscar 300 python tools/ab.py --scene sportscar --rounds 4 --frames 5 fast:PRT_SPLIT_OCC_A=2 fast:PRT_SPLIT_OCC_A=1 fast:PRT_SPLIT_OCC_A=2,PRT_SPLIT_OCC_B=3 fast:PRT_SPLIT_OCC_A=1,PRT_SPLIT_OCC_B=2
+              for sc in dragon car_boxed; do
+                  run abcap_$sc 300 python tools/ab.py --scene $sc --rounds 4 --frames 5 fast fast:PRT_PERSIST_CAP=2 fast:PRT_PERSIST_CAP=1 fast:PRT_SPLIT=1,PRT_SPLIT_OCC_A=2 fast:PRT_SPLIT=1,PRT_SPLIT_OCC_A=1
+              done ;;
+      abtune) for sc in dragon car_boxed sportscar; do
+                  PRT_TUNE_LOG=1 run abtune_$sc 300 python tools/ab.py --scene $sc --rounds 4 --frames 5 fast fast:PRT_TUNE=0
+              done ;;
       *) echo "unknown step $step"; exit 2 ;;
     esac
   done
