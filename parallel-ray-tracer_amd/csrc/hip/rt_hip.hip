@@ -649,7 +649,6 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     if (const char* e = std::getenv("PRT_REFILL_BELOW")) A.refill_below = std::max(0, std::min(64, std::atoi(e)));
     const bool count = (ctx->flags & RT_FLAG_COUNTERS) != 0;
     dim3 grid((f->width + 15) / 16, (f->n_rows + 15) / 16);
-    HIPC(hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT, ctx->stream));
     const int slot = (int)(ctx->launches % rt_ctx::NEV);
     ctx->ev0 = ctx->ev0s[slot];
     ctx->ev1 = ctx->ev1s[slot];
@@ -755,8 +754,10 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
             cap = T.cap[T.choice];
         }
     }
-    // one frame of configuration (split, cap); d_work holds the persistent grids' work counters
+    // one frame of configuration (split, cap); d_work holds the persistent grids' work counters, and the
+    // ray counters restart with every launch (rt_get_stats reports the frame, not the trial launches)
     auto dispatch = [&](bool sp, int cp) -> int {
+        HIPC(hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT, ctx->stream));
         HIPC(hipMemsetAsync(ctx->d_work, 0, 1024, ctx->stream));
         if (sp) return f->bounces <= 4 ? launch_split<4>(ctx, A, count, cp) : launch_split<8>(ctx, A, count, cp);
         if (kernel == RT_KERNEL_WAVEFRONT) return launch_wf(ctx, A, count);

@@ -353,6 +353,9 @@ def test_autotuned_frames_equal_forced_configuration(dev, name, n_cand, monkeypa
         r.sync()
         np.testing.assert_array_equal(hit.cpu().numpy(), ref["hit"])
         assert same_bits(t.cpu().numpy(), ref["t"]) and same_bits(rgb.cpu().numpy(), ref["rgb"]), frame
+        st = r.stats()  # one frame's rays, not the trial launches' sum
+        for k in ("rays", "primary", "shadow", "pixels"):
+            assert st[k] == ref["stats"][k], (frame, k, st[k], ref["stats"][k])
     r.close()
     log = [l for l in capfd.readouterr().err.splitlines() if l.startswith("[prt tune]")]
     assert len(log) == 1 and log[0].count(" ms") == n_cand, log

@@ -10,6 +10,7 @@ usage: tools/pmc_traffic.py gpurun_out/prof_<tag> <round-tag> [bench key]
 import csv
 import json
 import os
+import shutil
 import statistics
 import sys
 
@@ -45,12 +46,29 @@ def main():
     # kernel trace stats
     stats = rows(os.path.join(prof, "trace", "run_kernel_stats.csv"))
     lines = [f"# rocprofv3 --kernel-trace --stats ({tag})", "",
-             f"command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline`",
+             f"command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline`",
              "", "| kernel | calls | total ms | avg ms | min ms | max ms | % |", "|---|---|---|---|---|---|---|"]
     for r in stats:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
                      f"{float(r['AverageNs']) / 1e6:.4f} | {float(r['MinNs']) / 1e6:.4f} | "
                      f"{float(r['MaxNs']) / 1e6:.4f} | {float(r['Percentage']):.2f} |")
+    # per-dispatch durations of the production kernel, grouped by grid size: the first frame of a scene
+    # is rt_render's autotuning frame (each candidate grid 3 times), the frames after it use one grid
+    tr = os.path.join(prof, "trace", "run_kernel_trace.csv")
+    groups = {}
+    if os.path.exists(tr):
+        for r in rows(tr):
+            if PROD in r["Kernel_Name"]:
+                groups.setdefault(int(r["Grid_Size_X"]) // 256, []).append(
+                    (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    prod_grid = max(groups, key=lambda g: len(groups[g])) if groups else None
+    if groups:
+        lines += ["", f"## `{PROD}` per dispatch (kernel trace), by grid", "",
+                  "| workgroups | launches | median ms | mean ms |", "|---|---|---|---|"]
+        for g in sorted(groups):
+            v = groups[g]
+            lines.append(f"| {g}{' (frames after tuning)' if g == prod_grid else ''} | {len(v)} | "
+                         f"{statistics.median(v):.4f} | {statistics.mean(v):.4f} |")
     fetch = per_kernel(os.path.join(prof, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(prof, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     kf, vf = find(fetch, PROD)
@@ -62,6 +80,8 @@ def main():
         _, avg = find({r["Name"]: float(r["AverageNs"]) for r in stats}, PROD)
         res = {"kernel": kf, "launches": len(vf), "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
                "hbm_bytes_per_launch": hbm, "trace_avg_ms": avg / 1e6 if avg else None,
+               "trace_median_ms_production_grid": statistics.median(groups[prod_grid]) if groups else None,
+               "production_grid_workgroups": prod_grid,
                "hbm_gbs_at_trace_avg": hbm / (avg / 1e9) / 1e9 if avg else None,
                "rule": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md §HBM, gfx950 FETCH_SIZE halving)",
                "source": f"profiles/{tag}_kernel_stats.md, gpurun_out/{os.path.basename(prof)}", "round": tag}
@@ -85,6 +105,23 @@ def main():
         if agg:
             lines += ["", f"### {sub} (`{PROD}`, median per launch)", ""]
             lines += [f"- {k}: {statistics.median(v):.4g}" for k, v in sorted(agg.items())]
+    # CSV copies under profiles/<tag>/: the trace stats as rocprofv3 wrote them, the PMC passes as
+    # per-kernel medians (kernel, counter, launches, median, min, max)
+    cdir = os.path.join(pdir, tag)
+    os.makedirs(cdir, exist_ok=True)
+    shutil.copyfile(os.path.join(prof, "trace", "run_kernel_stats.csv"), os.path.join(cdir, "kernel_stats.csv"))
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_l2", "pmc_valu"):
+        p = os.path.join(prof, sub, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        agg = {}
+        for r in rows(p):
+            agg.setdefault((r["Kernel_Name"], r["Counter_Name"]), []).append(float(r["Counter_Value"]))
+        with open(os.path.join(cdir, f"{sub}_summary.csv"), "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["kernel", "counter", "launches", "median", "min", "max"])
+            for (k, c), v in sorted(agg.items()):
+                w.writerow([k, c, len(v), statistics.median(v), min(v), max(v)])
     with open(os.path.join(pdir, f"{tag}_kernel_stats.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
