@@ -16,6 +16,8 @@
 #include "rt_hip.h"
 #include "rt_host.h"
 #include "rt_kernels.hpp"
+#include "rt_coop.hpp"
+#include "rt_fan.hpp"
 #include "rt_output.hpp"
 #include "rt_split.hpp"
 #include "rt_wave.hpp"
@@ -84,8 +86,7 @@ struct rt_ctx {
     unsigned* d_sbatch = nullptr;
     size_t srec_cap = 0, spinfo_cap = 0, svis_cap = 0, sbatch_cap = 0;
     unsigned long long* d_counters = nullptr;  // rtd::NCOUNT
-    int* d_order = nullptr;                    // tile dealing order (PRT_TILE_ORDER), for order_tx x order_ty tiles
-    int order_tx = 0, order_ty = 0;
+    std::unordered_map<long long, int*> orders;  // tile dealing orders (PRT_TILE_ORDER), per tx x ty tile grid
     unsigned int* d_work = nullptr;
     // wavefront pipeline buffers (rt_wf.hpp), sized for wf_pix pixels x wf_lights lights
     void* wf_mem = nullptr;
@@ -102,13 +103,13 @@ struct rt_ctx {
     bool rendered = false;
     // launch autotuning of RT_KERNEL_FAST (rt_render): the candidate configurations are timed on the
     // first frame of a (scene upload, frame shape) and the fastest one renders the frames after it
-    static constexpr int TUNE_MAX = 3, TUNE_REPS = 3;
+    static constexpr int TUNE_MAX = 8, TUNE_REPS = 3;
     struct Tune {
         long long scene = -1;
         int W = 0, rows = 0, bounces = 0, spp = 0;
         int n = 0, choice = -1;  // candidates; the chosen one (-1: not decided yet)
         bool pending = false;    // trial launches enqueued, timings not read yet
-        bool split[TUNE_MAX] = {};
+        int mode[TUNE_MAX] = {};  // M_PERSIST, M_SPLIT, or the group size G of k_coop (2, 4, 8)
         int cap[TUNE_MAX] = {};
         float ms[TUNE_MAX] = {};
         hipEvent_t e0[TUNE_MAX * TUNE_REPS] = {}, e1[TUNE_MAX * TUNE_REPS] = {};
@@ -572,6 +573,33 @@ int launch_wf(rt_ctx* ctx, const rtd::KArgs& K, bool count) {
 }  // namespace
 
 namespace {
+// k_fan (rt_fan.hpp): R lanes per pixel (closest chain + R - 1 shadow lanes), 64 / R-pixel tiles
+template <int MAXB>
+int launch_fan(const rtd::KArgs& A, int R, bool count, int device, hipStream_t s, int cap) {
+    auto k = count ? rtd::k_fan<MAXB, true, 4> : rtd::k_fan<MAXB, false, 4>;
+    if (R == 2) k = count ? rtd::k_fan<MAXB, true, 2> : rtd::k_fan<MAXB, false, 2>;
+    if (R == 8) k = count ? rtd::k_fan<MAXB, true, 8> : rtd::k_fan<MAXB, false, 8>;
+    if (A.tile_trace && R == 4)  // diagnostics (PRT_TILE_TRACE with PRT_FAN=1 on a 2-3-light scene)
+        k = count ? rtd::k_fan<MAXB, true, 4, 3, true> : rtd::k_fan<MAXB, false, 4, 3, true>;
+    const int blocks = std::max(1, std::min(resident(k, device, cap), (A.n_tiles + 3) / 4));
+    k<<<blocks, rtd::BLOCK, 0, s>>>(A);
+    return RT_OK;
+}
+
+// k_coop (rt_coop.hpp): G lanes per ray; one wave per tile of 64 / G pixels, never more workgroups than
+// tiles / 4
+template <int MAXB>
+int launch_coop(const rtd::KArgs& A, int G, bool count, int device, hipStream_t s, int cap) {
+    auto k = count ? rtd::k_coop<MAXB, true, 4> : rtd::k_coop<MAXB, false, 4>;
+    if (G == 2) k = count ? rtd::k_coop<MAXB, true, 2> : rtd::k_coop<MAXB, false, 2>;
+    if (G == 8) k = count ? rtd::k_coop<MAXB, true, 8> : rtd::k_coop<MAXB, false, 8>;
+    if (A.tile_trace && G == 4)  // diagnostics (PRT_TILE_TRACE with PRT_COOP=4)
+        k = count ? rtd::k_coop<MAXB, true, 4, 3, true> : rtd::k_coop<MAXB, false, 4, 3, true>;
+    const int blocks = std::max(1, std::min(resident(k, device, cap), (A.n_tiles + 3) / 4));
+    k<<<blocks, rtd::BLOCK, 0, s>>>(A);
+    return RT_OK;
+}
+
 template <int MAXB>
 int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count, int cap_a);  // below
 }  // namespace
@@ -655,54 +683,78 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     // diagnostics: PRT_TILE_TRACE=<file> writes 4 x uint64 per tile of a k_persist frame (rt_kernels.hpp)
     // (s_memrealtime, 100 MHz); synchronous, never used by tests or the bench
     const char* trace_path = std::getenv("PRT_TILE_TRACE");
+    // The buffer holds one record per tile of the FINEST tiling any configuration deals (k_coop<8>: 4x2
+    // pixels); trace_n = the tiles of the configuration that ran.
     unsigned long long* d_trace = nullptr;
+    size_t trace_n = (size_t)A.n_tiles;
     if (trace_path && kernel == RT_KERNEL_FAST) {
-        HIPC(hipMalloc((void**)&d_trace, sizeof(unsigned long long) * 4 * (size_t)A.n_tiles));
-        HIPC(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * 4 * (size_t)A.n_tiles, ctx->stream));
+        const size_t cap = (size_t)((f->width + 3) / 4) * (size_t)((f->n_rows + 1) / 2);
+        HIPC(hipMalloc((void**)&d_trace, sizeof(unsigned long long) * 4 * cap));
+        HIPC(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * 4 * cap, ctx->stream));
         A.tile_trace = d_trace;
     }
-    // Tile dealing order of the persistent kernel: centre-out (default). The frame ends when the slowest
+    // Tile dealing order of the persistent kernels: centre-out (default). The frame ends when the slowest
     // tile does (PRT_TILE_TRACE: 8x8 tiles range from 2 us to ~1.9 ms; expensive ones are deep reflection
     // chains, usually on the object in view); dealing from the centre starts them first (bench frame
-    // -7 %). PRT_TILE_ORDER=rows: row-major (A/B knob).
+    // -7 %). PRT_TILE_ORDER=rows: row-major (A/B knob). One cached permutation per tile grid.
     const char* order_env = std::getenv("PRT_TILE_ORDER");
-    if (kernel == RT_KERNEL_FAST && !(order_env && std::strcmp(order_env, "rows") == 0)) {
-        const int ty = A.n_tiles / A.tiles_x;
-        if (!ctx->d_order || ctx->order_tx != A.tiles_x || ctx->order_ty != ty) {
-            std::vector<int> ord(A.n_tiles);
-            for (int i = 0; i < A.n_tiles; i++) ord[i] = i;
-            const float cx = 0.5f * A.tiles_x, cy = 0.5f * ty;
-            std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
-                const float ax = a % A.tiles_x + 0.5f - cx, ay = a / A.tiles_x + 0.5f - cy;
-                const float bx = b % A.tiles_x + 0.5f - cx, by = b / A.tiles_x + 0.5f - cy;
-                return ax * ax + ay * ay < bx * bx + by * by;
-            });
-            if (ctx->d_order) HIPC(hipFree(ctx->d_order));
-            ctx->d_order = nullptr;
-            HIPC(hipMalloc((void**)&ctx->d_order, sizeof(int) * ord.size()));
-            HIPC(hipMemcpy(ctx->d_order, ord.data(), sizeof(int) * ord.size(), hipMemcpyHostToDevice));
-            ctx->order_tx = A.tiles_x;
-            ctx->order_ty = ty;
+    const bool centre_out = kernel == RT_KERNEL_FAST && !(order_env && std::strcmp(order_env, "rows") == 0);
+    auto order_for = [&](int tx, int ty, const int*& out_ord) -> int {
+        out_ord = nullptr;
+        if (!centre_out) return RT_OK;
+        const long long key = ((long long)tx << 32) | (unsigned)ty;
+        auto it = ctx->orders.find(key);
+        if (it != ctx->orders.end()) {
+            out_ord = it->second;
+            return RT_OK;
         }
-        A.tile_order = ctx->d_order;
-    }
-    // RT_KERNEL_FAST: k_persist, or at 1 spp the split pipeline (rt_split.hpp), each a persistent grid of
-    // up to `cap` waves per SIMD. Which is fastest depends on the scene (same-box A/B): dragon
+        const int n = tx * ty;
+        std::vector<int> ord(n);
+        for (int i = 0; i < n; i++) ord[i] = i;
+        const float cx = 0.5f * tx, cy = 0.5f * ty;
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+            const float ax = a % tx + 0.5f - cx, ay = a / tx + 0.5f - cy;
+            const float bx = b % tx + 0.5f - cx, by = b / tx + 0.5f - cy;
+            return ax * ax + ay * ay < bx * bx + by * by;
+        });
+        int* d = nullptr;
+        HIPC(hipMalloc((void**)&d, sizeof(int) * ord.size()));
+        HIPC(hipMemcpy(d, ord.data(), sizeof(int) * ord.size(), hipMemcpyHostToDevice));
+        ctx->orders[key] = d;
+        out_ord = d;
+        return RT_OK;
+    };
+    if (int rc = order_for(A.tiles_x, A.n_tiles / A.tiles_x, A.tile_order)) return rc;
+    // RT_KERNEL_FAST has several launch configurations (`mode`, `cap` waves per SIMD of a persistent grid):
+    //   M_PERSIST  k_persist, one lane per pixel path, 8x8 tiles;
+    //   M_SPLIT    (1 spp) the split pipeline (rt_split.hpp): closest chains, shadow batches, resolve;
+    //   G = 2/4/8  k_coop (rt_coop.hpp): G lanes per ray, 64/G-pixel tiles — shorter chains per tile,
+    //              which is what a frame split over many GPUs (few tiles per wave) is bound by.
+    // Which is fastest depends on the scene and on the frame shape (same-box A/B): dragon
     // wants k_persist at its full 3 waves/SIMD, car_boxed k_persist at 2 (-15 %: fewer incoherent
     // reflection chains in flight thrash the caches less), sportscar (4 lights) the split pipeline at 2.
     // Every configuration renders the same bits, so the context measures: the first frame of a
     // (scene, frame shape) runs each candidate TUNE_REPS times (all into the same outputs), the next
     // frame reads the timings and keeps the fastest. PRT_TUNE=0 (or forcing a configuration through
-    // PRT_SPLIT / PRT_PERSIST_CAP / PRT_SPLIT_OCC_A) disables it; PRT_TUNE_LOG=1 prints the timings.
+    // PRT_SPLIT / PRT_PERSIST_CAP / PRT_SPLIT_OCC_A / PRT_COOP) disables it; PRT_TUNE_LOG=1 prints the timings.
+    enum { M_PERSIST = 0, M_SPLIT = 1, M_FAN = 3 };  // 2, 4, 8: k_coop with G = mode
     const char* split_env = std::getenv("PRT_SPLIT");
     const char* cap_env = std::getenv("PRT_PERSIST_CAP");
     const char* occa_env = std::getenv("PRT_SPLIT_OCC_A");
+    const char* coop_env = std::getenv("PRT_COOP");
     const char* tune_env = std::getenv("PRT_TUNE");
     const bool split_ok = kernel == RT_KERNEL_FAST && f->spp == 1 && ctx->n_lights <= 32 && !A.tile_trace;
-    bool split = split_ok && (split_env ? std::atoi(split_env) == 1 : ctx->n_lights >= 3);
-    int cap = split ? env_cap("PRT_SPLIT_OCC_A", 2) : env_cap("PRT_PERSIST_CAP", 8);
+    const bool coop_ok = kernel == RT_KERNEL_FAST && ctx->wide_n > 0;
+    const bool fan_ok = coop_ok && ctx->n_lights >= 1 && ctx->n_lights <= 7;
+    const int fan_r = ctx->n_lights <= 1 ? 2 : ctx->n_lights <= 3 ? 4 : 8;  // lanes per pixel: 1 + lights
+    const char* fan_env = std::getenv("PRT_FAN");
+    int mode = split_ok && (split_env ? std::atoi(split_env) == 1 : ctx->n_lights >= 3) ? M_SPLIT : M_PERSIST;
+    if (coop_ok && coop_env && (std::atoi(coop_env) == 2 || std::atoi(coop_env) == 4 || std::atoi(coop_env) == 8))
+        mode = std::atoi(coop_env);
+    if (fan_ok && fan_env && std::atoi(fan_env) == 1) mode = M_FAN;
+    int cap = mode == M_SPLIT ? env_cap("PRT_SPLIT_OCC_A", 2) : env_cap("PRT_PERSIST_CAP", 8);
     const bool tunable = kernel == RT_KERNEL_FAST && !A.tile_trace && !split_env && !cap_env && !occa_env &&
-                         !(tune_env && std::atoi(tune_env) == 0);
+                         !coop_env && !fan_env && !(tune_env && std::atoi(tune_env) == 0);
     rt_ctx::Tune& T = ctx->tune;
     bool trial = false;
     if (tunable) {
@@ -716,11 +768,12 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
             T.n = 0;
             T.choice = -1;
             T.pending = false;
-            const bool sp[3] = {false, false, true};
-            const int cp[3] = {8, 2, 2};
-            for (int i = 0; i < 3; i++)
-                if (!sp[i] || (split_ok && ctx->n_lights >= 1)) {
-                    T.split[T.n] = sp[i];
+            const int md[7] = {M_PERSIST, M_PERSIST, M_SPLIT, 4, 2, 8, M_FAN};  // (no trial with PRT_TILE_TRACE)
+            const int cp[7] = {8, 2, 2, 8, 8, 8, 8};
+            for (int i = 0; i < 7 && T.n < rt_ctx::TUNE_MAX; i++)
+                if ((md[i] != M_SPLIT || (split_ok && ctx->n_lights >= 1)) && (md[i] != M_FAN || fan_ok) &&
+                    (md[i] < 2 || md[i] == M_FAN || coop_ok)) {
+                    T.mode[T.n] = md[i];
                     T.cap[T.n] = cp[i];
                     T.n++;
                 }
@@ -742,24 +795,44 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
             T.pending = false;
             if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1) {
                 std::fprintf(stderr, "[prt tune] %dx%d b%d spp%d:", T.W, T.rows, T.bounces, T.spp);
-                for (int c = 0; c < T.n; c++)
-                    std::fprintf(stderr, " %s/%d %.3f ms", T.split[c] ? "split" : "persist", T.cap[c], T.ms[c]);
+                for (int c = 0; c < T.n; c++) {
+                    const int m = T.mode[c];
+                    std::fprintf(stderr, " %s%s/%d %.3f ms",
+                                 m == M_PERSIST ? "persist" : m == M_SPLIT ? "split" : m == M_FAN ? "fan" : "coop",
+                                 m == M_FAN ? std::to_string(fan_r).c_str() : m >= 2 ? std::to_string(m).c_str() : "",
+                                 T.cap[c], T.ms[c]);
+                }
                 std::fprintf(stderr, " -> %d\n", best);
             }
         } else if (T.choice < 0) {
             trial = !count;  // counters would add up over the trial launches: such a frame keeps the default
         }
         if (T.choice >= 0) {
-            split = T.split[T.choice];
+            mode = T.mode[T.choice];
             cap = T.cap[T.choice];
         }
     }
-    // one frame of configuration (split, cap); d_work holds the persistent grids' work counters, and the
+    // one frame of configuration (mode, cap); d_work holds the persistent grids' work counters, and the
     // ray counters restart with every launch (rt_get_stats reports the frame, not the trial launches)
-    auto dispatch = [&](bool sp, int cp) -> int {
+    auto dispatch = [&](int md, int cp) -> int {
         HIPC(hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT, ctx->stream));
         HIPC(hipMemsetAsync(ctx->d_work, 0, 1024, ctx->stream));
-        if (sp) return f->bounces <= 4 ? launch_split<4>(ctx, A, count, cp) : launch_split<8>(ctx, A, count, cp);
+        if (md == M_SPLIT) return f->bounces <= 4 ? launch_split<4>(ctx, A, count, cp) : launch_split<8>(ctx, A, count, cp);
+        if (md >= 2) {
+            rtd::KArgs B = A;
+            const int gr = md == M_FAN ? fan_r : md;  // lanes per pixel
+            const int tw = gr == 2 ? 8 : 4, th = gr == 8 ? 2 : 4;  // rtd::GTile<gr>
+            B.tiles_x = (f->width + tw - 1) / tw;
+            const int ty = (f->n_rows + th - 1) / th;
+            B.n_tiles = B.tiles_x * ty;
+            if (int rc = order_for(B.tiles_x, ty, B.tile_order)) return rc;
+            trace_n = (size_t)B.n_tiles;
+            if (md == M_FAN)
+                return f->bounces <= 4 ? launch_fan<4>(B, gr, count, ctx->device, ctx->stream, cp)
+                                       : launch_fan<8>(B, gr, count, ctx->device, ctx->stream, cp);
+            return f->bounces <= 4 ? launch_coop<4>(B, md, count, ctx->device, ctx->stream, cp)
+                                   : launch_coop<8>(B, md, count, ctx->device, ctx->stream, cp);
+        }
         if (kernel == RT_KERNEL_WAVEFRONT) return launch_wf(ctx, A, count);
         if (f->bounces <= 4) launch<4>(A, kernel, count, grid, ctx->device, ctx->stream, cp);
         else launch<8>(A, kernel, count, grid, ctx->device, ctx->stream, cp);
@@ -775,7 +848,7 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
             const int c = i % T.n;
             if (i == nt - 1) HIPC(hipEventRecord(ctx->ev0, ctx->stream));
             HIPC(hipEventRecord(T.e0[i], ctx->stream));
-            const int rc = dispatch(T.split[c], T.cap[c]);
+            const int rc = dispatch(T.mode[c], T.cap[c]);
             if (rc) return rc;
             HIPC(hipGetLastError());
             HIPC(hipEventRecord(T.e1[i], ctx->stream));
@@ -783,13 +856,13 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
         T.pending = true;
     } else {
         HIPC(hipEventRecord(ctx->ev0, ctx->stream));
-        const int rc = dispatch(split, cap);
+        const int rc = dispatch(mode, cap);
         if (rc) return rc;
     }
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(ctx->ev1, ctx->stream));
     if (d_trace) {
-        std::vector<unsigned long long> h(4 * (size_t)A.n_tiles);
+        std::vector<unsigned long long> h(4 * trace_n);
         HIPC(hipStreamSynchronize(ctx->stream));
         HIPC(hipMemcpy(h.data(), d_trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
         HIPC(hipFree(d_trace));
@@ -1033,7 +1106,7 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     if (ctx->wf_mem) (void)hipFree(ctx->wf_mem);
     if (ctx->d_rgb_own) (void)hipFree(ctx->d_rgb_own);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
-    if (ctx->d_order) (void)hipFree(ctx->d_order);
+    for (auto& o : ctx->orders) (void)hipFree(o.second);
     for (void* p : {(void*)ctx->d_full, (void*)ctx->d_full_hit, (void*)ctx->d_stage, (void*)ctx->d_bmp,
                     (void*)ctx->d_srec, (void*)ctx->d_spinfo, (void*)ctx->d_svis, (void*)ctx->d_sbatch})
         if (p) (void)hipFree(p);

@@ -560,6 +560,14 @@ __device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, 
     return visible_walk<true, COUNT, REG>(s.ref, o, d, ld2, stk, c);
 }
 
+// group-cooperative walks (rt_coop.hpp): G lanes per ray
+template <int G, bool COUNT>
+__device__ __forceinline__ int closest_g(const DScene& s, v3 o, v3 d, float& best, int& nd, int* __restrict__ stk,
+                                         Ctr& c, unsigned q);
+template <int G, bool COUNT>
+__device__ __forceinline__ bool visible_g(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c,
+                                          unsigned q);
+
 // ---------------------------------------------------------------- one path (raytrace, iterative)
 template <int MAXB>
 __device__ __forceinline__ void set3(v3 (&a)[MAXB], int i, v3 v) {
@@ -592,16 +600,20 @@ __device__ __forceinline__ void seti(int (&a)[MAXB], int i, int v) {
 // (o, d): closest hit, Lambert/Blinn with one shadow ray per light, reflection. Stores the level's
 // colour and material; returns true when the path ends (L = levels kept, tail = the reference's
 // raytrace(.., BOUNCES) returned {0,0,0}), otherwise leaves the reflection ray in (o, d).
-template <int MAXB, bool STRICT, bool COUNT, bool REG>
+// G > 1: the traversals are group-cooperative (rt_coop.hpp), q = the lane's place in its group.
+template <int MAXB, bool STRICT, bool COUNT, bool REG, int G = 1>
 __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, v3& o, v3& d, v3 (&cols)[MAXB],
                                           int (&mats)[MAXB], int& L, bool& tail, int& hit0, float& t0,
-                                          int* __restrict__ bh, int bh_pix, int* __restrict__ stk, Ctr& c) {
+                                          int* __restrict__ bh, int bh_pix, int* __restrict__ stk, Ctr& c,
+                                          unsigned q = 0) {
     const v3 amb = mk(s.amb_x, s.amb_y, s.amb_z);
     float best;
     int nd;
     if (it == 0) c.prim++;
     else c.refl++;
-    const int orig = closest<STRICT, COUNT, REG>(s, o, d, best, nd, stk, c);
+    int orig;
+    if constexpr (G > 1) orig = closest_g<G, COUNT>(s, o, d, best, nd, stk, c, q);
+    else orig = closest<STRICT, COUNT, REG>(s, o, d, best, nd, stk, c);
     if (it == 0) {
         hit0 = orig;
         t0 = best;
@@ -640,7 +652,8 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
             c.skip++;
         } else {
             c.shad++;
-            V = visible<STRICT, COUNT, REG>(s, ip, l, ld2, stk, c) ? 1 : 0;
+            if constexpr (G > 1) V = visible_g<G, COUNT>(s, ip, l, ld2, stk, c, q) ? 1 : 0;
+            else V = visible<STRICT, COUNT, REG>(s, ip, l, ld2, stk, c) ? 1 : 0;
         }
         const float fV = (float)V;
         col.x = col.x + fV * kl.x * cr.x / mg;
@@ -692,8 +705,9 @@ __device__ __forceinline__ v3 fold_path(const DScene& s, const v3 (&cols)[MAXB],
     return acc;
 }
 
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true>
-__device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0, int bh_pix) {
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1>
+__device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0, int bh_pix,
+                         unsigned q = 0) {
     v3 o = mk(A.pos[0], A.pos[1], A.pos[2]);
     v3 cols[MAXB];
     int mats[MAXB];
@@ -705,8 +719,8 @@ __device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, in
     int L = 0;
     bool tail = false;
     for (int it = 0; it < A.bounces; ++it) {
-        if (path_step<MAXB, STRICT, COUNT, REG>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0, A.bounce_hit,
-                                                bh_pix, stk, c))
+        if (path_step<MAXB, STRICT, COUNT, REG, G>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0,
+                                                   A.bounce_hit, bh_pix, stk, c, q))
             break;
     }
     return fold_path<MAXB>(A.s, cols, mats, L, tail);
@@ -724,8 +738,9 @@ __device__ __forceinline__ v3 primary_dir(const KArgs& A, float fx, float fy) {
     return d;
 }
 
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true>
-__device__ __forceinline__ void render_pixel(const KArgs& A, int x, int k, int* __restrict__ stk, Ctr& c) {
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1>
+__device__ __forceinline__ void render_pixel(const KArgs& A, int x, int k, int* __restrict__ stk, Ctr& c,
+                                             unsigned q = 0) {
     const int y = A.row_offset + k * A.row_stride;
     const size_t o = (size_t)k * A.W + x;
     int hit0 = -1;
@@ -734,8 +749,8 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, int x, int k, int* 
     if (A.bounce_hit)
         for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
     if (A.spp <= 1) {
-        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG>(A, primary_dir(A, (float)x, (float)y), stk, c, hit0, t0,
-                                                           (int)o));
+        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G>(A, primary_dir(A, (float)x, (float)y), stk, c, hit0,
+                                                              t0, (int)o, q));
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples
         const int g = A.spp_grid;
         v3 acc = mk(0.0f, 0.0f, 0.0f);
@@ -745,8 +760,8 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, int x, int k, int* 
                 const float fy = (float)y + ((float)sj + 0.5f) / (float)g;
                 int h;
                 float tt;
-                const v3 cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG>(A, primary_dir(A, fx, fy), stk, c, h, tt,
-                                                                           si == 0 && sj == 0 ? (int)o : -1));
+                const v3 cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G>(
+                    A, primary_dir(A, fx, fy), stk, c, h, tt, si == 0 && sj == 0 ? (int)o : -1, q));
                 acc = add(acc, cs);
                 if (si == 0 && sj == 0) {
                     hit0 = h;
@@ -757,6 +772,7 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, int x, int k, int* 
         col = mk(acc.x / nn, acc.y / nn, acc.z / nn);
     }
     c.pix++;
+    if (q != 0) return;  // a group's pixel is written once
     if (A.rgb) {
         A.rgb[3 * o] = col.x;
         A.rgb[3 * o + 1] = col.y;

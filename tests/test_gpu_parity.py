@@ -16,8 +16,25 @@ from prt import host
 
 pytestmark = pytest.mark.gpu
 RGB_TOL = 1e-5
-# every kernel the C-ABI exposes: STRICT, FAST (production), and the A/B variants WAVEFRONT and WAVE
-KERNELS = ["strict", "fast", "wavefront", "wave"]
+# every kernel the C-ABI exposes: STRICT, FAST (production), and the A/B variants WAVEFRONT and WAVE;
+# "coopG" = FAST forced to its group-cooperative configuration (k_coop, G lanes per ray, PRT_COOP=G);
+# "fan" = FAST forced to the shadow fan-out (k_fan, 1 + lights lanes per pixel, PRT_FAN=1)
+KERNELS = ["strict", "fast", "wavefront", "wave", "coop2", "coop4", "coop8", "fan"]
+FORCE = {"coop2": ("PRT_COOP", "2"), "coop4": ("PRT_COOP", "4"), "coop8": ("PRT_COOP", "8"), "fan": ("PRT_FAN", "1")}
+
+
+def select(kernel):
+    """kernel name -> rt_kernel name, with PRT_COOP / PRT_FAN set (or cleared) for the library"""
+    unforce()
+    if kernel in FORCE:
+        os.environ[FORCE[kernel][0]] = FORCE[kernel][1]
+        return "fast"
+    return kernel
+
+
+def unforce():
+    for k in ("PRT_COOP", "PRT_FAN"):
+        os.environ.pop(k, None)
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 G = json.load(open(os.path.join(GOLD, "golden.json")))
 
@@ -46,8 +63,10 @@ def render(dev, scene, W, H, kernel, rows=None, spp=1, bounces=4, counters=False
     hit = torch.empty((nr, W), dtype=torch.int32, device="cuda")
     t = torch.empty((nr, W), dtype=torch.float32, device="cuda")
     rgb = torch.empty((nr, W, 3), dtype=torch.float32, device="cuda")
-    r.render(host.camera(W, H), W, H, rows=rows, bounces=bounces, spp=spp, kernel=kernel, rgb=rgb, hit=hit, t=t)
+    r.render(host.camera(W, H), W, H, rows=rows, bounces=bounces, spp=spp, kernel=select(kernel), rgb=rgb, hit=hit,
+             t=t)
     r.sync()
+    unforce()
     st = r.stats()
     out = {"rgb": rgb.cpu().numpy(), "hit": hit.cpu().numpy(), "t": t.cpu().numpy(), "stats": st}
     r.close()
@@ -159,14 +178,15 @@ def test_strict_traversal_counters_match_reference_order(dev, scenes):
         assert st[k] == c[k], k
 
 
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan"])
 @pytest.mark.parametrize("spp", [4, 16])
-def test_spp_matches_oracle(dev, scenes, spp):
+def test_spp_matches_oracle(dev, scenes, spp, kernel):
     from tests.oracle_bind import OracleScene
     from tests.scenes import scene_paths
     o = OracleScene.load(*scene_paths("car_only"))
     o.build_bvh(3)
     ref, c = o.render_spp(64, 36, spp)
-    out = render(dev, scenes["car_only"], 64, 36, "fast", spp=spp, counters=True)
+    out = render(dev, scenes["car_only"], 64, 36, kernel, spp=spp, counters=True)
     assert same_bits(out["rgb"], ref)
     assert out["stats"]["primary"] == 64 * 36 * spp
 
@@ -188,17 +208,23 @@ def test_standin_scenes_vs_reference_fixture(dev, name):
         assert md5.hexdigest() == G["standin"][name]["320x180_md5"], k
 
 
+_ORACLE_FRAMES = {}
+
+
 @pytest.mark.slow
-def test_bench_config_full_frame_vs_oracle(dev):
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan"])
+def test_bench_config_full_frame_vs_oracle(dev, kernel):
     """the bench workload (dragon stand-in, 1920x1080, fast kernel, library SAH BVH) against the oracle
     at full size: hit indices, t and colours bit-exact"""
     from tests.oracle_bind import OracleScene
     from tests.scenes import scene_paths
     s = host.Scene.named("dragon").build_bvh(3)
-    out = render(dev, s, 1920, 1080, "fast", counters=True)
-    o = OracleScene.load(*scene_paths("dragon"))
-    o.build_bvh(3)
-    ref = o.render(1920, 1080, threads=min(32, os.cpu_count() or 8))
+    out = render(dev, s, 1920, 1080, kernel, counters=True)
+    if "dragon1080" not in _ORACLE_FRAMES:  # one oracle frame for both kernels
+        o = OracleScene.load(*scene_paths("dragon"))
+        o.build_bvh(3)
+        _ORACLE_FRAMES["dragon1080"] = o.render(1920, 1080, threads=min(32, os.cpu_count() or 8))
+    ref = _ORACLE_FRAMES["dragon1080"]
     bad = np.argwhere(out["hit"] != ref["hit"])
     assert len(bad) == 0, (len(bad), bad[:10])
     assert same_bits(out["t"], ref["t"])
@@ -235,8 +261,9 @@ def test_bounce_hits_match_oracle(dev, scenes, kernel):
     r.upload(scenes["car_boxed"])
     bh = torch.full((72, 128, 4), -9, dtype=torch.int32, device="cuda")
     rgb = torch.empty((72, 128, 3), dtype=torch.float32, device="cuda")
-    r.render(host.camera(128, 72), 128, 72, kernel=kernel, rgb=rgb, bounce_hit=bh)
+    r.render(host.camera(128, 72), 128, 72, kernel=select(kernel), rgb=rgb, bounce_hit=bh)
     r.sync()
+    unforce()
     np.testing.assert_array_equal(bh.cpu().numpy(), ref["bounce_hit"])
     assert same_bits(rgb.cpu().numpy(), ref["rgb"])
     r.close()
@@ -331,7 +358,7 @@ def test_split_pipeline_equals_persistent_kernel(dev, name, monkeypatch):
         assert same_bits(b["rgb"], ref["rgb"])
 
 
-@pytest.mark.parametrize("name,n_cand", [("sportscar", 3), ("car_boxed", 3), ("dragon", 3)])
+@pytest.mark.parametrize("name,n_cand", [("sportscar", 7), ("car_boxed", 7), ("dragon", 7)])
 def test_autotuned_frames_equal_forced_configuration(dev, name, n_cand, monkeypatch, capfd):
     """rt_render's launch autotuner (rt_hip.hip, RT_KERNEL_FAST): the trial frame (every candidate, each
     TUNE_REPS times, into the same outputs) and the frames after the decision are bit-exact to a forced

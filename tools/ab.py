@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=5)
     ap.add_argument("--reupload", action="store_true", help="rebuild the scene per variant (knobs read at upload)")
+    ap.add_argument("--world", type=int, default=1, help="render rank --rank's cyclic rows of a --world split")
+    ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
@@ -29,7 +31,9 @@ def main():
     r = device.Renderer(0)
     r.upload(s)
     cam = host.camera(a.W, a.H)
-    rgb = torch.empty((a.H, a.W, 3), dtype=torch.float32, device="cuda")
+    from prt.dist import cyclic_rows
+    rows = cyclic_rows(a.H, a.rank, a.world)
+    rgb = torch.empty((rows[2], a.W, 3), dtype=torch.float32, device="cuda")
     res = {v: [] for v in a.variants}
     rays = {}
     pixels = {}
@@ -55,7 +59,7 @@ def main():
             if a.reupload:
                 r.upload(s)
             for _ in range(a.frames):
-                r.render(cam, a.W, a.H, kernel=kern, rgb=rgb)
+                r.render(cam, a.W, a.H, rows=rows, kernel=kern, rgb=rgb)
             ts = r.kernel_times(a.frames)
             if rnd > 0:  # round 0 = warm-up
                 res[v] += ts

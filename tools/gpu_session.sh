@@ -126,6 +126,8 @@ for s in "${@:-smoke pytest bench}"; do
       abtune) for sc in dragon car_boxed sportscar; do
                   PRT_TUNE_LOG=1 run abtune_$sc 300 python tools/ab.py --scene $sc --rounds 4 --frames 5 fast fast:PRT_TUNE=0
               done ;;
+      ranks)  run ranks 300 python tools/rank_rows.py
+              run ranks_car 300 python tools/rank_rows.py --scene car_boxed ;;
       *) echo "unknown step $step"; exit 2 ;;
     esac
   done

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Per-rank kernel time of the cyclic row partition, simulated on ONE GPU (§8e rehearsal).
+
+For each N, renders every rank's compact rows (row_offset = r, row_stride = N) in turn on this device and
+prints the max-over-ranks kernel time, i.e. the kernel part of an N-GPU frame, and the implied kernel-only
+scaling against N = 1. The gather is not included (it needs the real node).
+usage: python tools/rank_rows.py [--scene dragon] [--W 1920 --H 1080] [--frames 10] [--ns 1,2,4,8]"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "parallel-ray-tracer_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="dragon")
+    ap.add_argument("--W", type=int, default=1920)
+    ap.add_argument("--H", type=int, default=1080)
+    ap.add_argument("--frames", type=int, default=10)
+    ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--kernel", default="fast")
+    a = ap.parse_args()
+    import torch
+    from prt import device, host
+    from prt.dist import cyclic_rows, padded_rows
+    s = host.Scene.named(a.scene).build_bvh(3)
+    cam = host.camera(a.W, a.H)
+    out = {}
+    base = None
+    for n in [int(x) for x in a.ns.split(",")]:
+        per_rank = []
+        for q in range(n):
+            r = device.Renderer(0)
+            r.upload(s)
+            ro, rs, nr = cyclic_rows(a.H, q, n)
+            rgb = torch.empty((padded_rows(a.H, n), a.W, 3), dtype=torch.float32, device="cuda")
+            for _ in range(2):  # tuning frame + warm-up
+                r.render(cam, a.W, a.H, rows=(ro, rs, nr), kernel=a.kernel, rgb=rgb)
+                r.sync()
+            for _ in range(a.frames):
+                r.render(cam, a.W, a.H, rows=(ro, rs, nr), kernel=a.kernel, rgb=rgb)
+            ts = sorted(r.kernel_times(a.frames))
+            per_rank.append(ts[len(ts) // 2])
+            r.close()
+        mx = max(per_rank)
+        if base is None:
+            base = mx * n
+        out[n] = {"max_ms": mx, "ranks_ms": per_rank, "kernel_scaling": base / mx}
+        print(f"N={n}: max over ranks {mx:.4f} ms  ranks {['%.3f' % t for t in per_rank]}  "
+              f"kernel-only scaling {base / mx:.2f}x", flush=True)
+    print(json.dumps({"scene": a.scene, "W": a.W, "H": a.H, "results": out}))
+
+
+if __name__ == "__main__":
+    main()

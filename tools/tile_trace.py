@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--H", type=int, default=1080)
     ap.add_argument("--out", default=None)
     ap.add_argument("--counters", action="store_true", help="COUNT kernel: per-tile wave steps and node visits")
+    ap.add_argument("--world", type=int, default=1, help="render rank --rank's cyclic rows of a --world split")
+    ap.add_argument("--rank", type=int, default=0)
     a = ap.parse_args()
     import torch
     from prt import device, host
@@ -26,14 +28,16 @@ def main():
     r = device.Renderer(0, counters=a.counters)
     r.upload(s)
     cam = host.camera(a.W, a.H)
-    rgb = torch.empty((a.H, a.W, 3), dtype=torch.float32, device="cuda")
+    from prt.dist import cyclic_rows
+    rows = cyclic_rows(a.H, a.rank, a.world)
+    rgb = torch.empty((rows[2], a.W, 3), dtype=torch.float32, device="cuda")
     for _ in range(5):
-        r.render(cam, a.W, a.H, rgb=rgb)
+        r.render(cam, a.W, a.H, rows=rows, rgb=rgb)
     r.sync()
     a.out = a.out or os.path.join(ROOT, "gpurun_out", f"tile_trace_{a.scene}.bin")
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     os.environ["PRT_TILE_TRACE"] = a.out
-    r.render(cam, a.W, a.H, rgb=rgb)
+    r.render(cam, a.W, a.H, rows=rows, rgb=rgb)
     r.sync()
     del os.environ["PRT_TILE_TRACE"]
     ms = r.kernel_times(1)[0]
@@ -48,7 +52,9 @@ def main():
     first = np.array([b[w == x].min() for x in waves])
     last = np.array([e[w == x].max() for x in waves])
     busy = np.array([dur[w == x].sum() for x in waves])
-    tx = (a.W + 7) // 8
+    # k_coop<4> and k_fan<4> (2-3 lights) deal 4x4 tiles
+    tw, tht = (4, 4) if os.environ.get("PRT_COOP") == "4" or os.environ.get("PRT_FAN") == "1" else (8, 8)
+    tx = (a.W + tw - 1) // tw
     rows = dur.reshape(-1, tx).mean(1) if len(dur) % tx == 0 else None
     res = {
         "kernel_ms_event": ms, "tile_span_us": float(span), "tiles": int(len(tr)), "waves": int(len(waves)),
@@ -64,7 +70,7 @@ def main():
         "tail_us_after_first_idle_wave": float(span - last.min()),
     }
     top = np.argsort(-dur)[:12]
-    res["slowest_tiles"] = [{"x": int(i % tx) * 8, "y": int(i // tx) * 8, "us": round(float(dur[i]), 1),
+    res["slowest_tiles"] = [{"x": int(i % tx) * tw, "y_compact": int(i // tx) * tht, "us": round(float(dur[i]), 1),
                              "fallback_rays": int(fb[i]), "start_us": round(float(b[i]), 1),
                              "wave_steps": int(ws[i]), "lane_node_visits": int(nv[i])} for i in top]
     if a.counters:
