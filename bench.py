@@ -4,7 +4,15 @@
 One step = one full frame of the hot path (ray generation, BVH traversal, ray-triangle intersection,
 shading with shadow rays, 4 reflection bounces, clamp) for the workload below, with the scene resident
 in HBM before timing starts; for N > 1 the frame's rows are dealt cyclically over the ranks (row y on
-rank y % N: cost-balanced) and gathered to rank 0 over RCCL inside the step.
+rank y % N: cost-balanced) and gathered to rank 0 over RCCL inside the timed region.
+
+Frames in flight: the K timed frames (the reference's ITERATIONS loop of one camera, main.c) are traced
+in batches of F frames per launch (rt_render_frames: one persistent launch whose tile dealing interleaves
+the batch's frames, so the long reflection chains of one frame overlap the others' work instead of
+leaving the chip idle at the frame's tail), and each batch's gather overlaps the next batch's render
+(ping-pong blocks). Every frame is traced in full into its own output (bit-exact to a single rt_render,
+tests/test_gpu_parity.py::test_frame_batch_equals_single_frames); the single-frame kernel latency is
+reported next to the throughput (frame_latency_ms).
 
 Rays counted as the reference defines its work: primary + traced reflection + traced
 shadow rays (light_v calls past the back-face test), from the kernel's own counters (equal to the
@@ -98,8 +106,9 @@ def cpu_baseline(scene_files, W, H, gpu_rays_for_rows, args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=64, help="timed frames")
+    ap.add_argument("--warmup", type=int, default=16, help="untimed frames (after the tuning launches)")
+    ap.add_argument("--frames", type=int, default=0, help="frames per launch (0: 16 x world size, at most --steps)")
     ap.add_argument("--scene", default="dragon")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -139,39 +148,59 @@ def main():
     r = device.Renderer(local, stream=stream)
     r.upload(scene, accel=args.accel)
     cam = host.camera(W, H)
-    # cyclic rows y = rank + k * world, gathered to rank 0 with one RCCL collective (prt/dist.py, tested
-    # with gloo in tests/test_multi.py)
-    fg = FrameGather(H, W, 3, rank, world, dist, like=torch.empty(0, dtype=torch.float32, device="cuda"))
+    K = args.steps
+    F = max(1, min(args.frames or 16 * world, K))
+    plan = [F] * (K // F) + ([K % F] if K % F else [])  # launches covering exactly K frames
+    # cyclic rows y = rank + k * world, gathered to rank 0 with one RCCL collective per batch (prt/dist.py,
+    # tested with gloo in tests/test_multi.py); two ping-pong blocks so a batch's gather overlaps the next
+    # batch's render
+    fg = FrameGather(H, W, 3, rank, world, dist, like=torch.empty(0, dtype=torch.float32, device="cuda"),
+                     frames=F, buffers=2)
     _, _, n_r = fg.rows()
-    out = fg.block
+    launch_no = [0]
 
-    def step():
-        r.render(cam, W, H, rows=(rank, world, n_r), bounces=args.bounces, spp=args.spp, kernel=args.kernel,
-                 rgb=out)
-        fg.gather()
+    def launch(nf):
+        b = launch_no[0] % 2
+        launch_no[0] += 1
+        if fg.pending(b):
+            fg.finish(b)
+        r.render_frames([cam] * nf, W, H, rows=(rank, world, n_r), bounces=args.bounces, spp=args.spp,
+                        kernel=args.kernel, rgb=fg.blocks[b])
+        fg.start(b)
 
-    # setup, like the upload: the first frame of a scene and frame shape is rt_render's launch-autotuning
-    # frame (every candidate configuration timed, rt_hip.hip); the next render reads the timings
-    step()
-    torch.cuda.synchronize()
-    for _ in range(args.warmup):
-        step()
+    def drain():
+        for b in range(2):
+            if fg.pending(b):
+                fg.finish(b)
+
+    # setup, like the upload: the first launch of a scene and batch shape is rt_render's launch-autotuning
+    # launch (every candidate configuration timed, rt_hip.hip); the next launch of that shape reads the
+    # timings. Each batch size of the plan is tuned here, then `warmup` frames run untimed.
+    for nf in sorted(set(plan)):
+        launch(nf)
+        launch(nf)
+    for _ in range(max(1, -(-args.warmup // F))):
+        launch(F)
+    drain()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for nf in plan:
+        launch(nf)
+    drain()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    ktimes = r.kernel_times(min(args.steps, 64))
+    ktimes = r.kernel_times(min(len(plan), 64))
+    kfull = [t for t, nf in zip(ktimes, plan[-len(ktimes):]) if nf == F] or ktimes
     st = r.stats()
-    # whole-job ray count per frame (identical every step: the render is deterministic)
-    rays_local = st["rays"]
+    # whole-job ray count per frame (identical every frame: the render is deterministic), from the last
+    # launch's counters (a batch: the sum over its frames)
+    rays_local = st["rays"] // plan[-1]
     el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     rays_t = torch.tensor([rays_local], dtype=torch.float64, device="cuda")
     if dist:
@@ -180,14 +209,26 @@ def main():
     elapsed = el.item()
     rays_frame = int(rays_t.item())
 
-    # algorithmic bytes of this rank's launch: one extra untimed launch with traversal counters
+    # algorithmic bytes of this rank's full-batch launch: one extra untimed launch with traversal counters
     rc = device.Renderer(local, counters=True, stream=stream)
     rc.upload(scene, accel=args.accel)
-    rc.render(cam, W, H, rows=(rank, world, n_r), bounces=args.bounces, spp=args.spp, kernel=args.kernel, rgb=out)
+    rc.render_frames([cam] * F, W, H, rows=(rank, world, n_r), bounces=args.bounces, spp=args.spp,
+                     kernel=args.kernel, rgb=fg.blocks[0])
     stc = rc.stats()
     rc.close()
-    bytes_launch = alg_bytes(stc, W * n_r, len(scene.lights))
-    k_avg_ms = sum(ktimes) / len(ktimes)
+    bytes_launch = alg_bytes(stc, F * W * n_r, len(scene.lights))
+    k_avg_ms = sum(kfull) / len(kfull)
+    # single-frame latency of this rank's rows (one launch, one frame; its own tuning launch first)
+    rl = device.Renderer(local, stream=stream)
+    rl.upload(scene, accel=args.accel)
+    for _ in range(3):
+        rl.render(cam, W, H, rows=(rank, world, n_r), bounces=args.bounces, spp=args.spp, kernel=args.kernel,
+                  rgb=fg.blocks[0])
+    lat_ms = sorted(rl.kernel_times(2))[0]
+    rl.close()
+    lat = torch.tensor([lat_ms], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(lat, op=dist.ReduceOp.MAX)
 
     if rank == 0:
         traffic = None
@@ -202,12 +243,12 @@ def main():
         achieved = bytes_launch / (k_avg_ms / 1e3) / 1e9
         result = {
             "metric": METRIC,
-            "value": rays_frame * args.steps / elapsed / 1e6,
+            "value": rays_frame * K / elapsed / 1e6,
             "unit": "Mrays/s",
             "n_gpus": world,
-            "steps": args.steps,
+            "steps": K,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": elapsed / K * 1e3,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -216,14 +257,15 @@ def main():
                      "(.MISSING_LARGE_BLOBS); prt/scenes.py generates a Cornell room + 98,304-tri knot with the "
                      "real dragon .mtl and lights.obj" if is_standin(args.scene) else "reference asset"),
             "config": {"workload": f"{args.scene} {W}x{H}, {args.spp} spp, {args.bounces} bounces, one fused "
-                                   f"traversal+intersect+shade kernel per frame",
+                                   f"traversal+intersect+shade persistent launch per batch of {F} frames",
                        "scene": args.scene, "triangles": scene.n_triangles, "lights": len(scene.lights),
                        "width": W, "height": H, "bvh": args.bvh, "accel": args.accel, "kernel": args.kernel,
                        "rays_per_frame": rays_frame, "parallelism": f"rows-cyclic x{world} + RCCL gather"
-                       if world > 1 else "single GPU"},
+                       if world > 1 else "single GPU", "frames_per_launch": F},
+            "frame_latency_ms": lat.item(),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel_ms": k_avg_ms, "alg_bytes_per_launch": bytes_launch,
+                         "kernel_ms": k_avg_ms, "alg_bytes_per_launch": bytes_launch, "frames_per_launch": F,
                          "note": "algorithmic bytes (node/triangle/shading records the kernel reads) / HIP-event "
                                  "kernel time; the ~10 MB scene stays L2/MALL-resident, so HBM traffic is far lower"},
         }

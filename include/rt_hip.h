@@ -115,6 +115,15 @@ int rt_create(const rt_opts* opts, rt_ctx** out);
 int rt_upload_scene(rt_ctx* ctx, const rt_scene* scene);
 /* render_frame(): enqueues ONE kernel on the context stream (asynchronous) */
 int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* frame, const rt_outputs* out);
+/* A batch of n_frames frames of the same shape (a camera sequence; main.c:141-160's ITERATIONS loop when
+ * the cameras are equal): frame i uses cams[i] and writes its outputs at frame offset i, i.e. rgb
+ * [n_frames][n_rows][width][3], hit / t [n_frames][n_rows][width], bounce_hit [n_frames][n_rows][width]
+ * [bounces]. RT_KERNEL_FAST traces the whole batch in ONE persistent launch whose tile dealing interleaves
+ * the frames (the long reflection chains of every frame start first, so one frame's tail overlaps the
+ * others' work); other kernels launch once per frame. Each frame equals its rt_render bit for bit; the
+ * stats of the call are the batch's sums. rt_gather / rt_download_bmp need a single-frame render. */
+int rt_render_frames(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_frame* frame,
+                     const rt_outputs* out);
 /* load_from_gpu(): copies the last frame's compact rows to host (synchronous); nullable args */
 int rt_download(rt_ctx* ctx, float* h_rgb, int* h_hit);
 /* waits for the stream; kernel_ms (nullable) = the last render's kernel time from HIP events */

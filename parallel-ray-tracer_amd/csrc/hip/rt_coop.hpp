@@ -301,7 +301,7 @@ template <> struct GTile<8> { static constexpr int TW = 4, TH = 2; };
 
 // Persistent waves pulling TW x TH pixel tiles (k_persist's dealing: one atomic per wave per tile,
 // optional centre-out order); lane = (pixel lane / G, group member lane % G).
-template <int MAXB, bool COUNT, int G, int OCC = 3, bool TRACE = false>
+template <int MAXB, bool COUNT, int G, int OCC = 3, bool TRACE = false, bool BATCH = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(OCC))) void k_coop(KArgs A) {
     __shared__ int lds[STACK * BLOCK];
     int* stk = lds + threadIdx.x;
@@ -310,18 +310,21 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     const int pi = lane / G;
     constexpr int TW = GTile<G>::TW;
     Ctr c = {};
+    const unsigned items = (unsigned)A.n_tiles * (unsigned)A.n_frames;  // frame batches: as k_persist
     for (;;) {
-        unsigned tile = 0;
-        if (lane == 0) tile = atomicAdd(A.work, 1u);
-        tile = __shfl(tile, 0, 64);
-        if (tile >= (unsigned)A.n_tiles) break;
+        unsigned t = 0;
+        if (lane == 0) t = atomicAdd(A.work, 1u);
+        t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+        if (t >= items) break;
+        const int frame = (int)(t % (unsigned)A.n_frames);
+        unsigned tile = t / (unsigned)A.n_frames;
         if (A.tile_order) tile = (unsigned)A.tile_order[tile];
         const int tx = (int)(tile % (unsigned)A.tiles_x), ty = (int)(tile / (unsigned)A.tiles_x);
         const int x = tx * TW + pi % TW, k = ty * GTile<G>::TH + pi / TW;
         unsigned long long t0 = 0;
         const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
         if (TRACE) t0 = __builtin_amdgcn_s_memrealtime();
-        if (x < A.W && k < A.n_rows) render_pixel<MAXB, false, COUNT, true, G>(A, x, k, stk, c, q);
+        if (x < A.W && k < A.n_rows) render_pixel<MAXB, false, COUNT, true, G>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, q);
         if (TRACE) {  // as k_persist's: {begin, end, wave | fallbacks << 32, wave steps | ray node visits << 32}
             const unsigned fb = wave_sum(q == 0 ? c.fb - fb0 : 0u), ws = wave_sum(c.ws - ws0),
                            nv = wave_sum(q == 0 ? c.chi + c.shi - nd0 : 0u);

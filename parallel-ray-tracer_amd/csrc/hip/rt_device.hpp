@@ -81,13 +81,20 @@ struct KArgs {
     unsigned char* svis;
     unsigned* sbatch;
     size_t nslots;
+    // frame batches (rt_render_frames): n_frames frames of the same shape, frame f's camera at
+    // cams[12 f .. 12 f + 11] (pos, ul, inc_x, inc_y; nullable when n_frames == 1: the fields above),
+    // its outputs at pixel offset f * frame_px (frame_px = n_rows * W)
+    const float* cams;
+    int n_frames;
+    int frames_pad;
+    unsigned long long frame_px;
 };
 
 // Kernel arguments are laid out by the host compiler and read by the device compiler: both passes must
 // agree on every offset (an LDS pointer, 32-bit on gfx950 but 64-bit on the host, once shifted every
 // later field and hung a kernel). Pinned sizes catch such drift at compile time in whichever pass
 // disagrees; never put address-space-qualified pointers in these structs.
-static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 144 && sizeof(KArgs) == 344,
+static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 144 && sizeof(KArgs) == 368,
               "kernel-argument layout changed: update the pinned sizes only after checking both passes agree");
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

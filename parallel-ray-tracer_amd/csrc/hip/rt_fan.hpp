@@ -95,7 +95,7 @@ __device__ __forceinline__ v3 shfl3(v3 v, int src) { return mk(shfl_f(v.x, src),
 // Persistent waves pulling TW x TH pixel tiles (GTile<R>: 64 / R pixels); lane = (pixel lane / R, role
 // lane % R). Role 0 owns the pixel's path (path_step's state), role j in 1..R-1 the shadow ray toward
 // light j - 1 (the host launches this kernel only for 1 <= lights <= R - 1).
-template <int MAXB, bool COUNT, int R, int OCC = 3, bool TRACE = false>
+template <int MAXB, bool COUNT, int R, int OCC = 3, bool TRACE = false, bool BATCH = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(OCC))) void k_fan(KArgs A) {
     __shared__ int lds[STACK * BLOCK];
     int* stk = lds + threadIdx.x;
@@ -113,12 +113,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         kl = xyz(s.lights[2 * lj + 1]);
     }
     Ctr c = {};
+    const unsigned items = (unsigned)A.n_tiles * (unsigned)A.n_frames;  // frame batches: as k_persist
     for (;;) {
-        unsigned tile = 0;
-        if (lane == 0) tile = atomicAdd(A.work, 1u);
-        tile = __shfl(tile, 0, 64);
-        if (tile >= (unsigned)A.n_tiles) break;
+        unsigned t = 0;
+        if (lane == 0) t = atomicAdd(A.work, 1u);
+        t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+        if (t >= items) break;
+        const int frame = (int)(t % (unsigned)A.n_frames);
+        unsigned tile = t / (unsigned)A.n_frames;
         if (A.tile_order) tile = (unsigned)A.tile_order[tile];
+        const Cam C = cam_of<BATCH>(A, frame);
         const int tx = (int)(tile % (unsigned)A.tiles_x), ty = (int)(tile / (unsigned)A.tiles_x);
         const int x = tx * TW + pi % TW, k = ty * TH + pi / TW;
         const bool valid = x < A.W && k < A.n_rows;  // uniform in the group
@@ -126,7 +130,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
         if (TRACE) tr0 = __builtin_amdgcn_s_memrealtime();
         const int y = A.row_offset + k * A.row_stride;
-        const size_t po = (size_t)k * A.W + x;
+        const size_t po = (size_t)frame * A.frame_px + (size_t)k * A.W + x;
         if (valid && role == 0 && A.bounce_hit)
             for (int i = 0; i < A.bounces; i++) A.bounce_hit[po * (size_t)A.bounces + i] = -2;
         const int g = A.spp <= 1 ? 1 : A.spp_grid;
@@ -138,7 +142,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                 // ---- role 0: the path (trace_path's state)
                 const float fx = g == 1 ? (float)x : (float)x + ((float)si + 0.5f) / (float)g;
                 const float fy = g == 1 ? (float)y : (float)y + ((float)sj + 0.5f) / (float)g;
-                v3 o = mk(A.pos[0], A.pos[1], A.pos[2]), d = primary_dir(A, fx, fy);
+                v3 o = C.pos, d = primary_dir(C, fx, fy);
                 v3 cols[MAXB];
                 int mats[MAXB];
 #pragma unroll

@@ -71,6 +71,12 @@ struct rt_ctx {
     int* last_hit = nullptr;
     size_t last_pixels = 0;
     int last_W = 0, last_H = 0, last_off = 0, last_stride = 1, last_rows = 0;  // the last frame's rows
+    int last_frames = 1;     // frames of the last render (rt_render_frames)
+    bool batch_sum = false;  // set while rt_render_frames launches frames one by one (counters add up)
+    // frame batches: the cameras on the device (d_cams) and the host copy they were uploaded from
+    float* d_cams = nullptr;
+    float* h_cams = nullptr;  // pinned
+    int cams_cap = 0, cams_n = 0;
     // output stage (rt_gather, rt_download_bmp)
     float* d_full = nullptr;
     int* d_full_hit = nullptr;
@@ -106,14 +112,17 @@ struct rt_ctx {
     static constexpr int TUNE_MAX = 8, TUNE_REPS = 3;
     struct Tune {
         long long scene = -1;
-        int W = 0, rows = 0, bounces = 0, spp = 0;
+        int W = 0, rows = 0, bounces = 0, spp = 0, frames = 0;
         int n = 0, choice = -1;  // candidates; the chosen one (-1: not decided yet)
         bool pending = false;    // trial launches enqueued, timings not read yet
         int mode[TUNE_MAX] = {};  // M_PERSIST, M_SPLIT, or the group size G of k_coop (2, 4, 8)
         int cap[TUNE_MAX] = {};
         float ms[TUNE_MAX] = {};
         hipEvent_t e0[TUNE_MAX * TUNE_REPS] = {}, e1[TUNE_MAX * TUNE_REPS] = {};
-    } tune;
+    };
+    // one tuning state per (scene upload, width, rows, bounces, spp, frames): a context that alternates
+    // frame shapes (e.g. batches of two sizes) keeps every decision
+    std::vector<Tune> tunes;
     long long scene_gen = 0;  // bumped by every upload
 };
 
@@ -434,6 +443,9 @@ void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int de
             k = count ? rtd::k_persist<MAXB, false, true, true, 4> : rtd::k_persist<MAXB, false, false, true, 4>;
         if (A.tile_trace)  // diagnostics (PRT_TILE_TRACE)
             k = count ? rtd::k_persist<MAXB, false, true, true, 3, true> : rtd::k_persist<MAXB, false, false, true, 3, true>;
+        if (A.n_frames > 1)  // frame batch: cameras from A.cams
+            k = count ? rtd::k_persist<MAXB, false, true, true, 3, false, true>
+                      : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
         if (const char* e = std::getenv("PRT_REGEN"); e && std::atoi(e) == 1 && A.spp <= 1) {  // A/B: path regeneration
             auto kr = count ? rtd::k_regen<MAXB, true> : rtd::k_regen<MAXB, false>;
             int blocks = std::max(1, std::min(resident(kr, device), (A.n_tiles + 3) / 4));
@@ -581,6 +593,11 @@ int launch_fan(const rtd::KArgs& A, int R, bool count, int device, hipStream_t s
     if (R == 8) k = count ? rtd::k_fan<MAXB, true, 8> : rtd::k_fan<MAXB, false, 8>;
     if (A.tile_trace && R == 4)  // diagnostics (PRT_TILE_TRACE with PRT_FAN=1 on a 2-3-light scene)
         k = count ? rtd::k_fan<MAXB, true, 4, 3, true> : rtd::k_fan<MAXB, false, 4, 3, true>;
+    if (A.n_frames > 1) {  // frame batch: cameras from A.cams
+        k = count ? rtd::k_fan<MAXB, true, 4, 3, false, true> : rtd::k_fan<MAXB, false, 4, 3, false, true>;
+        if (R == 2) k = count ? rtd::k_fan<MAXB, true, 2, 3, false, true> : rtd::k_fan<MAXB, false, 2, 3, false, true>;
+        if (R == 8) k = count ? rtd::k_fan<MAXB, true, 8, 3, false, true> : rtd::k_fan<MAXB, false, 8, 3, false, true>;
+    }
     const int blocks = std::max(1, std::min(resident(k, device, cap), (A.n_tiles + 3) / 4));
     k<<<blocks, rtd::BLOCK, 0, s>>>(A);
     return RT_OK;
@@ -595,6 +612,11 @@ int launch_coop(const rtd::KArgs& A, int G, bool count, int device, hipStream_t 
     if (G == 8) k = count ? rtd::k_coop<MAXB, true, 8> : rtd::k_coop<MAXB, false, 8>;
     if (A.tile_trace && G == 4)  // diagnostics (PRT_TILE_TRACE with PRT_COOP=4)
         k = count ? rtd::k_coop<MAXB, true, 4, 3, true> : rtd::k_coop<MAXB, false, 4, 3, true>;
+    if (A.n_frames > 1) {  // frame batch: cameras from A.cams
+        k = count ? rtd::k_coop<MAXB, true, 4, 3, false, true> : rtd::k_coop<MAXB, false, 4, 3, false, true>;
+        if (G == 2) k = count ? rtd::k_coop<MAXB, true, 2, 3, false, true> : rtd::k_coop<MAXB, false, 2, 3, false, true>;
+        if (G == 8) k = count ? rtd::k_coop<MAXB, true, 8, 3, false, true> : rtd::k_coop<MAXB, false, 8, 3, false, true>;
+    }
     const int blocks = std::max(1, std::min(resident(k, device, cap), (A.n_tiles + 3) / 4));
     k<<<blocks, rtd::BLOCK, 0, s>>>(A);
     return RT_OK;
@@ -604,13 +626,19 @@ template <int MAXB>
 int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count, int cap_a);  // below
 }  // namespace
 
-extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, const rt_outputs* out) {
+namespace {
+// rt_render / rt_render_frames: n_frames frames of the same shape (cameras cams[0..n_frames-1]); outputs
+// [n_frames][n_rows][width]... Persistent fast configurations trace the whole batch in ONE launch (frames'
+// tiles interleaved in the dealing order); other kernels launch once per frame.
+int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_frame* f, const rt_outputs* out) {
     if (!ctx) return RT_E_ARG;
     if (!ctx->has_scene) {
         ctx->err = "rt_render: no scene uploaded";
         return RT_E_STATE;
     }
-    if (!cam || !f) return arg_err(ctx, "rt_render: null camera/frame");
+    if (!cams || !f) return arg_err(ctx, "rt_render: null camera/frame");
+    if (n_frames < 1 || n_frames > 4096) return arg_err(ctx, "rt_render_frames: n_frames must be 1..4096");
+    const rt_camera* cam = cams;
     if (f->width <= 0 || f->height <= 0 || f->row_stride <= 0 || f->n_rows <= 0 || f->row_offset < 0 ||
         (long long)f->row_offset + (long long)(f->n_rows - 1) * f->row_stride >= f->height)
         return arg_err(ctx, "rt_render: rows outside the frame");
@@ -620,15 +648,16 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     if (f->spp < 1 || g * g != f->spp || g > 16) return arg_err(ctx, "rt_render: spp must be a square 1..256");
     if (f->kernel < RT_KERNEL_AUTO || f->kernel > RT_KERNEL_WAVE) return arg_err(ctx, "rt_render: bad kernel");
     HIPC(hipSetDevice(ctx->device));
-    const size_t pixels = (size_t)f->width * f->n_rows;
+    const size_t pixels = (size_t)f->width * f->n_rows;  // per frame
+    const size_t all_px = pixels * (size_t)n_frames;
     float* rgb = out ? out->rgb : nullptr;
     if (!rgb) {
-        if (ctx->rgb_cap < pixels) {
+        if (ctx->rgb_cap < all_px) {
             if (ctx->d_rgb_own) HIPC(hipFree(ctx->d_rgb_own));
             ctx->d_rgb_own = nullptr;
             ctx->rgb_cap = 0;
-            HIPC(hipMalloc((void**)&ctx->d_rgb_own, sizeof(float) * 3 * pixels));
-            ctx->rgb_cap = pixels;
+            HIPC(hipMalloc((void**)&ctx->d_rgb_own, sizeof(float) * 3 * all_px));
+            ctx->rgb_cap = all_px;
         }
         rgb = ctx->d_rgb_own;
     }
@@ -673,6 +702,45 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     if ((kernel == RT_KERNEL_WAVEFRONT || kernel == RT_KERNEL_WAVE) && (f->spp > 1 || (out && out->bounce_hit)))
         kernel = RT_KERNEL_FAST;  // spp > 1 and per-level hit dumps: the fused path kernels
     if ((f->bounces > rtd::WF_MAXB || ctx->n_lights > 32) && kernel == RT_KERNEL_WAVEFRONT) kernel = RT_KERNEL_FAST;
+    if (n_frames > 1 && kernel != RT_KERNEL_FAST) {  // one launch per frame, outputs at frame offsets
+        for (int i = 0; i < n_frames; i++) {
+            rt_outputs o{rgb + 3 * pixels * i, A.hit ? A.hit + pixels * i : nullptr, A.t ? A.t + pixels * i : nullptr,
+                         A.bounce_hit ? A.bounce_hit + pixels * f->bounces * i : nullptr};
+            ctx->batch_sum = i > 0;
+            const int rc = render_batch(ctx, cams + i, 1, f, &o);
+            ctx->batch_sum = false;
+            if (rc) return rc;
+        }
+        ctx->last_rgb = rgb;
+        ctx->last_hit = A.hit;
+        ctx->last_pixels = all_px;
+        ctx->last_frames = n_frames;
+        return RT_OK;
+    }
+    A.n_frames = n_frames;
+    A.frame_px = pixels;
+    if (n_frames > 1) {  // the batch's cameras, uploaded when they change (pinned staging, stream-ordered)
+        const size_t nf = 12 * (size_t)n_frames;
+        static_assert(sizeof(rt_camera) == 48, "rt_camera = 4 x rt_vec3");
+        if (ctx->cams_cap < n_frames) {
+            HIPC(hipStreamSynchronize(ctx->stream));
+            if (ctx->d_cams) HIPC(hipFree(ctx->d_cams));
+            if (ctx->h_cams) HIPC(hipHostFree(ctx->h_cams));
+            ctx->d_cams = nullptr;
+            ctx->h_cams = nullptr;
+            ctx->cams_cap = ctx->cams_n = 0;
+            HIPC(hipMalloc((void**)&ctx->d_cams, sizeof(float) * nf));
+            HIPC(hipHostMalloc((void**)&ctx->h_cams, sizeof(float) * nf, hipHostMallocDefault));
+            ctx->cams_cap = n_frames;
+        }
+        if (ctx->cams_n != n_frames || std::memcmp(ctx->h_cams, cams, sizeof(float) * nf) != 0) {
+            HIPC(hipStreamSynchronize(ctx->stream));  // an earlier copy from h_cams may still be queued
+            std::memcpy(ctx->h_cams, cams, sizeof(float) * nf);
+            HIPC(hipMemcpyAsync(ctx->d_cams, ctx->h_cams, sizeof(float) * nf, hipMemcpyHostToDevice, ctx->stream));
+            ctx->cams_n = n_frames;
+        }
+        A.cams = ctx->d_cams;
+    }
     A.refill_below = kernel == RT_KERNEL_WAVEFRONT ? 48 : 32;  // tuning knob, PRT_REFILL_BELOW overrides (0..64)
     if (const char* e = std::getenv("PRT_REFILL_BELOW")) A.refill_below = std::max(0, std::min(64, std::atoi(e)));
     const bool count = (ctx->flags & RT_FLAG_COUNTERS) != 0;
@@ -687,7 +755,7 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     // pixels); trace_n = the tiles of the configuration that ran.
     unsigned long long* d_trace = nullptr;
     size_t trace_n = (size_t)A.n_tiles;
-    if (trace_path && kernel == RT_KERNEL_FAST) {
+    if (trace_path && kernel == RT_KERNEL_FAST && n_frames == 1) {
         const size_t cap = (size_t)((f->width + 3) / 4) * (size_t)((f->n_rows + 1) / 2);
         HIPC(hipMalloc((void**)&d_trace, sizeof(unsigned long long) * 4 * cap));
         HIPC(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * 4 * cap, ctx->stream));
@@ -743,7 +811,8 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     const char* occa_env = std::getenv("PRT_SPLIT_OCC_A");
     const char* coop_env = std::getenv("PRT_COOP");
     const char* tune_env = std::getenv("PRT_TUNE");
-    const bool split_ok = kernel == RT_KERNEL_FAST && f->spp == 1 && ctx->n_lights <= 32 && !A.tile_trace;
+    const bool split_ok =
+        kernel == RT_KERNEL_FAST && f->spp == 1 && ctx->n_lights <= 32 && !A.tile_trace && n_frames == 1;
     const bool coop_ok = kernel == RT_KERNEL_FAST && ctx->wide_n > 0;
     const bool fan_ok = coop_ok && ctx->n_lights >= 1 && ctx->n_lights <= 7;
     const int fan_r = ctx->n_lights <= 1 ? 2 : ctx->n_lights <= 3 ? 4 : 8;  // lanes per pixel: 1 + lights
@@ -755,11 +824,29 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     int cap = mode == M_SPLIT ? env_cap("PRT_SPLIT_OCC_A", 2) : env_cap("PRT_PERSIST_CAP", 8);
     const bool tunable = kernel == RT_KERNEL_FAST && !A.tile_trace && !split_env && !cap_env && !occa_env &&
                          !coop_env && !fan_env && !(tune_env && std::atoi(tune_env) == 0);
-    rt_ctx::Tune& T = ctx->tune;
+    rt_ctx::Tune* Tp = nullptr;
+    for (auto& t : ctx->tunes)
+        if (t.scene == ctx->scene_gen && t.W == f->width && t.rows == f->n_rows && t.bounces == f->bounces &&
+            t.spp == f->spp && t.frames == n_frames)
+            Tp = &t;
+    if (!Tp && tunable) {
+        if (ctx->tunes.size() >= 16) {  // bounded: drop the oldest decision (its events with it)
+            for (int i = 0; i < rt_ctx::TUNE_MAX * rt_ctx::TUNE_REPS; i++) {
+                if (ctx->tunes.front().e0[i]) HIPC(hipEventDestroy(ctx->tunes.front().e0[i]));
+                if (ctx->tunes.front().e1[i]) HIPC(hipEventDestroy(ctx->tunes.front().e1[i]));
+            }
+            ctx->tunes.erase(ctx->tunes.begin());
+        }
+        ctx->tunes.emplace_back();
+        Tp = &ctx->tunes.back();
+    }
+    rt_ctx::Tune dummy;
+    rt_ctx::Tune& T = Tp ? *Tp : dummy;
     bool trial = false;
     if (tunable) {
         if (T.scene != ctx->scene_gen || T.W != f->width || T.rows != f->n_rows || T.bounces != f->bounces ||
-            T.spp != f->spp) {
+            T.spp != f->spp || T.frames != n_frames) {
+            T.frames = n_frames;
             T.scene = ctx->scene_gen;
             T.W = f->width;
             T.rows = f->n_rows;
@@ -768,9 +855,10 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
             T.n = 0;
             T.choice = -1;
             T.pending = false;
-            const int md[7] = {M_PERSIST, M_PERSIST, M_SPLIT, 4, 2, 8, M_FAN};  // (no trial with PRT_TILE_TRACE)
-            const int cp[7] = {8, 2, 2, 8, 8, 8, 8};
-            for (int i = 0; i < 7 && T.n < rt_ctx::TUNE_MAX; i++)
+            // (coop8 is 3x slower than coop4 everywhere measured: a knob, PRT_COOP=8, not a candidate)
+            const int md[6] = {M_PERSIST, M_PERSIST, M_SPLIT, 4, 2, M_FAN};
+            const int cp[6] = {8, 2, 2, 8, 8, 8};
+            for (int i = 0; i < 6 && T.n < rt_ctx::TUNE_MAX; i++)
                 if ((md[i] != M_SPLIT || (split_ok && ctx->n_lights >= 1)) && (md[i] != M_FAN || fan_ok) &&
                     (md[i] < 2 || md[i] == M_FAN || coop_ok)) {
                     T.mode[T.n] = md[i];
@@ -794,7 +882,7 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
             T.choice = best;
             T.pending = false;
             if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1) {
-                std::fprintf(stderr, "[prt tune] %dx%d b%d spp%d:", T.W, T.rows, T.bounces, T.spp);
+                std::fprintf(stderr, "[prt tune] %dx%d b%d spp%d f%d:", T.W, T.rows, T.bounces, T.spp, T.frames);
                 for (int c = 0; c < T.n; c++) {
                     const int m = T.mode[c];
                     std::fprintf(stderr, " %s%s/%d %.3f ms",
@@ -815,7 +903,8 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     // one frame of configuration (mode, cap); d_work holds the persistent grids' work counters, and the
     // ray counters restart with every launch (rt_get_stats reports the frame, not the trial launches)
     auto dispatch = [&](int md, int cp) -> int {
-        HIPC(hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT, ctx->stream));
+        if (!ctx->batch_sum)  // a per-frame loop of a batch keeps adding to the batch's counters
+            HIPC(hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT, ctx->stream));
         HIPC(hipMemsetAsync(ctx->d_work, 0, 1024, ctx->stream));
         if (md == M_SPLIT) return f->bounces <= 4 ? launch_split<4>(ctx, A, count, cp) : launch_split<8>(ctx, A, count, cp);
         if (md >= 2) {
@@ -874,7 +963,8 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     ctx->launches++;
     ctx->last_rgb = rgb;
     ctx->last_hit = A.hit;
-    ctx->last_pixels = pixels;
+    ctx->last_pixels = all_px;
+    ctx->last_frames = n_frames;
     ctx->last_W = f->width;
     ctx->last_H = f->height;
     ctx->last_off = f->row_offset;
@@ -882,6 +972,16 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
     ctx->last_rows = f->n_rows;
     ctx->rendered = true;
     return RT_OK;
+}
+}  // namespace
+
+extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, const rt_outputs* out) {
+    return render_batch(ctx, cam, 1, f, out);
+}
+
+extern "C" int rt_render_frames(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_frame* f,
+                                const rt_outputs* out) {
+    return render_batch(ctx, cams, n_frames, f, out);
 }
 
 extern "C" int rt_sync(rt_ctx* ctx, float* kernel_ms) {
@@ -981,6 +1081,7 @@ extern "C" int rt_gather(rt_ctx* const* ctxs, int n, int root) {
         rt_ctx* c = ctxs[i];
         if (!c || !c->rendered) return arg_err(ctx, "rt_gather: a context has not rendered");
         if (c->last_W != W || c->last_H != H) return arg_err(ctx, "rt_gather: frame sizes differ");
+        if (c->last_frames != 1) return arg_err(ctx, "rt_gather: the last render was a frame batch");
         for (int k = 0; k < c->last_rows; k++) {
             const long long y = c->last_off + (long long)k * c->last_stride;
             if (y < 0 || y >= H || cover[y]) return arg_err(ctx, "rt_gather: row sets do not partition the frame");
@@ -1047,6 +1148,7 @@ extern "C" int rt_download_bmp(rt_ctx* ctx, unsigned char* h_bmp, size_t cap) {
         ctx->err = "rt_download_bmp: nothing rendered";
         return RT_E_STATE;
     }
+    if (ctx->last_frames != 1) return arg_err(ctx, "rt_download_bmp: the last render was a frame batch");
     const int W = ctx->last_W, H = ctx->last_H;
     if (ctx->last_off != 0 || ctx->last_stride != 1 || ctx->last_rows != H) {
         ctx->err = "rt_download_bmp: the last frame is not a full frame (gather it first)";
@@ -1105,6 +1207,8 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     free_scene(ctx);
     if (ctx->wf_mem) (void)hipFree(ctx->wf_mem);
     if (ctx->d_rgb_own) (void)hipFree(ctx->d_rgb_own);
+    if (ctx->d_cams) (void)hipFree(ctx->d_cams);
+    if (ctx->h_cams) (void)hipHostFree(ctx->h_cams);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     for (auto& o : ctx->orders) (void)hipFree(o.second);
     for (void* p : {(void*)ctx->d_full, (void*)ctx->d_full_hit, (void*)ctx->d_stage, (void*)ctx->d_bmp,
@@ -1115,10 +1219,11 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
         if (ctx->ev0s[i]) (void)hipEventDestroy(ctx->ev0s[i]);
         if (ctx->ev1s[i]) (void)hipEventDestroy(ctx->ev1s[i]);
     }
-    for (int i = 0; i < rt_ctx::TUNE_MAX * rt_ctx::TUNE_REPS; i++) {
-        if (ctx->tune.e0[i]) (void)hipEventDestroy(ctx->tune.e0[i]);
-        if (ctx->tune.e1[i]) (void)hipEventDestroy(ctx->tune.e1[i]);
-    }
+    for (auto& t : ctx->tunes)
+        for (int i = 0; i < rt_ctx::TUNE_MAX * rt_ctx::TUNE_REPS; i++) {
+            if (t.e0[i]) (void)hipEventDestroy(t.e0[i]);
+            if (t.e1[i]) (void)hipEventDestroy(t.e1[i]);
+        }
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -706,9 +706,8 @@ __device__ __forceinline__ v3 fold_path(const DScene& s, const v3 (&cols)[MAXB],
 }
 
 template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1>
-__device__ v3 trace_path(const KArgs& A, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0, int bh_pix,
+__device__ v3 trace_path(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0, int bh_pix,
                          unsigned q = 0) {
-    v3 o = mk(A.pos[0], A.pos[1], A.pos[2]);
     v3 cols[MAXB];
     int mats[MAXB];
 #pragma unroll
@@ -730,27 +729,51 @@ __device__ __forceinline__ v3 clamp01(v3 c) {  // vec_constrain(col, 0, 1), vec.
     return mk(fminf(fmaxf(c.x, 0.0f), 1.0f), fminf(fmaxf(c.y, 0.0f), 1.0f), fminf(fmaxf(c.z, 0.0f), 1.0f));
 }
 
+// one frame's camera constants (main.c:243-250)
+struct Cam {
+    v3 pos, ul, ix, iy;
+};
+// frame f of a batch (A.cams; BATCH kernels), or the launch's single camera (kernel arguments: a
+// camera read from memory stays live in registers across the spp loop and costs the single-frame
+// kernels spills, so they never read A.cams)
+template <bool BATCH = false>
+__device__ __forceinline__ Cam cam_of(const KArgs& A, int f) {
+    if (!BATCH || !A.cams) return Cam{mk(A.pos[0], A.pos[1], A.pos[2]), mk(A.ul[0], A.ul[1], A.ul[2]),
+                                      mk(A.ix[0], A.ix[1], A.ix[2]), mk(A.iy[0], A.iy[1], A.iy[2])};
+    // f is wave-uniform: three vector loads, then every value moved to a scalar register (readfirstlane),
+    // so the camera costs no vector registers while it stays live across the spp loop
+    const float4* c4 = reinterpret_cast<const float4*>(A.cams) + 3 * f;
+    const float4 a = c4[0], b = c4[1], e = c4[2];
+    float c[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, e.x, e.y, e.z, e.w};
+#pragma unroll
+    for (int i = 0; i < 12; i++) c[i] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(c[i])));
+    return Cam{mk(c[0], c[1], c[2]), mk(c[3], c[4], c[5]), mk(c[6], c[7], c[8]), mk(c[9], c[10], c[11])};
+}
 // primary direction, main.c:229-233: ((ul - pos) + inc_x * x) + inc_y * y
-__device__ __forceinline__ v3 primary_dir(const KArgs& A, float fx, float fy) {
-    v3 d = sub(mk(A.ul[0], A.ul[1], A.ul[2]), mk(A.pos[0], A.pos[1], A.pos[2]));
-    d = add(d, mul(mk(A.ix[0], A.ix[1], A.ix[2]), fx));
-    d = add(d, mul(mk(A.iy[0], A.iy[1], A.iy[2]), fy));
+__device__ __forceinline__ v3 primary_dir(const Cam& C, float fx, float fy) {
+    v3 d = sub(C.ul, C.pos);
+    d = add(d, mul(C.ix, fx));
+    d = add(d, mul(C.iy, fy));
     return d;
 }
+__device__ __forceinline__ v3 primary_dir(const KArgs& A, float fx, float fy) {
+    return primary_dir(cam_of(A, 0), fx, fy);
+}
 
+// Pixel (x, compact row k) of frame `frame` of the launch (outputs at frame * frame_px).
 template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1>
-__device__ __forceinline__ void render_pixel(const KArgs& A, int x, int k, int* __restrict__ stk, Ctr& c,
-                                             unsigned q = 0) {
+__device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int frame, int x, int k,
+                                             int* __restrict__ stk, Ctr& c, unsigned q = 0) {
     const int y = A.row_offset + k * A.row_stride;
-    const size_t o = (size_t)k * A.W + x;
+    const size_t o = (size_t)frame * A.frame_px + (size_t)k * A.W + x;
     int hit0 = -1;
     float t0 = FMAX;
     v3 col;
     if (A.bounce_hit)
         for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
     if (A.spp <= 1) {
-        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G>(A, primary_dir(A, (float)x, (float)y), stk, c, hit0,
-                                                              t0, (int)o, q));
+        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G>(A, C.pos, primary_dir(C, (float)x, (float)y), stk, c,
+                                                              hit0, t0, (int)o, q));
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples
         const int g = A.spp_grid;
         v3 acc = mk(0.0f, 0.0f, 0.0f);
@@ -761,7 +784,7 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, int x, int k, int* 
                 int h;
                 float tt;
                 const v3 cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G>(
-                    A, primary_dir(A, fx, fy), stk, c, h, tt, si == 0 && sj == 0 ? (int)o : -1, q));
+                    A, C.pos, primary_dir(C, fx, fy), stk, c, h, tt, si == 0 && sj == 0 ? (int)o : -1, q));
                 acc = add(acc, cs);
                 if (si == 0 && sj == 0) {
                     hit0 = h;
@@ -791,7 +814,7 @@ __global__ __launch_bounds__(BLOCK) void k_tiles(KArgs A) {
     const int x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7);
     const int k = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
     Ctr c = {};
-    if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT>(A, x, k, stk, c);
+    if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT>(A, cam_of(A, 0), 0, x, k, stk, c);
     flush<COUNT>(c, A.counters);
 }
 
@@ -802,25 +825,30 @@ __global__ __launch_bounds__(BLOCK) void k_tiles(KArgs A) {
 // OCC: waves per SIMD the register allocation must allow: 3 caps VGPRs at 168 (512 / 3 in 8-register
 // granules; one register more halves nothing but drops a whole wave per SIMD), 4 at 128 (the LDS
 // stack allows 4 workgroups per CU).
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int OCC = 3, bool TRACE = false>
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int OCC = 3, bool TRACE = false, bool BATCH = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(OCC > 0 ? OCC : 1)))
 void k_persist(KArgs A) {
     __shared__ int lds[STACK * BLOCK];
     int* stk = lds + threadIdx.x;
     const int lane = threadIdx.x & 63;
     Ctr c = {};
+    // frame batches: dealt item t = (tile t / n_frames of the dealing order, frame t % n_frames), so the
+    // expensive (central) tiles of every frame of the batch start first
+    const unsigned items = (unsigned)A.n_tiles * (unsigned)A.n_frames;
     for (;;) {
-        unsigned tile = 0;
-        if (lane == 0) tile = atomicAdd(A.work, 1u);
-        tile = __shfl(tile, 0, 64);
-        if (tile >= (unsigned)A.n_tiles) break;
+        unsigned t = 0;
+        if (lane == 0) t = atomicAdd(A.work, 1u);
+        t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+        if (t >= items) break;
+        const int frame = (int)(t % (unsigned)A.n_frames);
+        unsigned tile = t / (unsigned)A.n_frames;
         if (A.tile_order) tile = (unsigned)A.tile_order[tile];
         const int tx = (int)(tile % (unsigned)A.tiles_x), ty = (int)(tile / (unsigned)A.tiles_x);
         const int x = tx * 8 + (lane & 7), k = ty * 8 + (lane >> 3);
         unsigned long long t0 = 0;
         const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
         if (TRACE) t0 = __builtin_amdgcn_s_memrealtime();
-        if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT, REG>(A, x, k, stk, c);
+        if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT, REG>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c);
         if (TRACE) {  // {begin, end, wave | fallbacks << 32, wave steps | lane node visits << 32} (COUNT)
             const unsigned fb = wave_sum(c.fb - fb0), ws = wave_sum(c.ws - ws0), nv = wave_sum(c.chi + c.shi - nd0);
             if (lane == 0) {

@@ -74,13 +74,8 @@ __device__ __forceinline__ unsigned wave_append(unsigned* cnt, bool want) {
 __global__ __launch_bounds__(WF_BLOCK) void k_wf_primary(WfArgs A) {
     const unsigned n_ids = (unsigned)A.n_tiles * 64u;
     if (blockIdx.x == 0 && threadIdx.x == 0) A.q[Q_C0] = n_ids;
-    KArgs K;  // primary_dir reads only the camera fields
-    for (int i = 0; i < 3; i++) {
-        K.pos[i] = A.pos[i];
-        K.ul[i] = A.ul[i];
-        K.ix[i] = A.ix[i];
-        K.iy[i] = A.iy[i];
-    }
+    const Cam K{mk(A.pos[0], A.pos[1], A.pos[2]), mk(A.ul[0], A.ul[1], A.ul[2]), mk(A.ix[0], A.ix[1], A.ix[2]),
+                mk(A.iy[0], A.iy[1], A.iy[2])};
     Ctr c = {};
     for (unsigned id = blockIdx.x * WF_BLOCK + threadIdx.x; id < n_ids; id += gridDim.x * WF_BLOCK) {
         const int tile = (int)(id >> 6), w = (int)(id & 63u);

@@ -122,6 +122,7 @@ def hip():
         L.rt_create.argtypes = [P(Opts), P(ctypes.c_void_p)]
         L.rt_upload_scene.argtypes = [ctypes.c_void_p, P(SceneDesc)]
         L.rt_render.argtypes = [ctypes.c_void_p, P(Camera), P(Frame), ctypes.c_void_p]
+        L.rt_render_frames.argtypes = [ctypes.c_void_p, P(Camera), ctypes.c_int, P(Frame), ctypes.c_void_p]
         L.rt_download.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.rt_sync.argtypes = [ctypes.c_void_p, P(ctypes.c_float)]
         L.rt_kernel_times.argtypes = [ctypes.c_void_p, P(ctypes.c_float), ctypes.c_int]

@@ -101,6 +101,21 @@ class Renderer:
         self._chk(_L.rt_render(self._ctx, ctypes.byref(cam), ctypes.byref(f), ctypes.byref(out)), "rt_render")
         self._last = (width, nr)
         self._size = (width, height)
+        self._frames = 1
+
+    def render_frames(self, cams, width, height, rows=None, bounces=4, spp=1, kernel="auto", rgb=None, hit=None,
+                      t=None, bounce_hit=None):
+        """rt_render_frames(): a batch of len(cams) frames of one shape (one persistent launch on the fast
+        kernel); outputs [n_frames, n_rows, W, ...]. Asynchronous."""
+        ro, rs, nr = rows if rows is not None else (0, 1, height)
+        f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel))
+        out = Outputs(_ptr(rgb), _ptr(hit), _ptr(t), _ptr(bounce_hit))
+        arr = (Camera * len(cams))(*cams)
+        self._chk(_L.rt_render_frames(self._ctx, arr, len(cams), ctypes.byref(f), ctypes.byref(out)),
+                  "rt_render_frames")
+        self._last = (width, nr)
+        self._size = (width, height)
+        self._frames = len(cams)
 
     def sync(self):
         ms = ctypes.c_float()
@@ -118,8 +133,10 @@ class Renderer:
     def download(self, hit=False):
         """load_from_gpu(): the last frame's compact rows -> (rgb[n_rows, W, 3], hit or None)"""
         W, nr = self._last
-        rgb = np.zeros((nr, W, 3), np.float32)
-        h = np.zeros((nr, W), np.int32) if hit else None
+        nf = getattr(self, "_frames", 1)
+        shp = (nr, W) if nf == 1 else (nf, nr, W)
+        rgb = np.zeros(shp + (3,), np.float32)
+        h = np.zeros(shp, np.int32) if hit else None
         self._chk(_L.rt_download(self._ctx, rgb.ctypes.data, h.ctypes.data if hit else None), "rt_download")
         return rgb, h
 

@@ -21,27 +21,65 @@ def padded_rows(H, world):
 
 
 class FrameGather:
-    """Gather per-rank compact row blocks [padded_rows, W, C] into the full frame on rank 0."""
+    """Gather per-rank compact row blocks [padded_rows, W, C] into the full frame on rank 0.
 
-    def __init__(self, H, W, C, rank, world, dist, like):
+    frames > 1: a frame batch (rt_render_frames) — blocks [frames, padded_rows, W, C] -> frames
+    [frames, H, W, C], one collective for the whole batch. buffers > 1: ping-pong blocks, so that the
+    gather of batch k (start(k % buffers), asynchronous on the collective's stream) overlaps the render of
+    batch k + 1 into the other block; finish(i) makes the current stream wait for it and un-interleaves.
+    World 1: the block IS the frame (no collective, no copy)."""
+
+    def __init__(self, H, W, C, rank, world, dist, like, frames=1, buffers=1):
         import torch
-        self.H, self.W, self.rank, self.world, self.dist = H, W, rank, world, dist
+        self.H, self.W, self.C, self.rank, self.world, self.dist = H, W, C, rank, world, dist
+        self.frames = frames
         self.n_max = padded_rows(H, world)
-        self.block = torch.zeros((self.n_max, W, C), dtype=like.dtype, device=like.device)
-        self.frame = torch.zeros((H, W, C), dtype=like.dtype, device=like.device) if rank == 0 else None
-        self.parts = [torch.empty_like(self.block) for _ in range(world)] if (rank == 0 and world > 1) else None
+        shape = (self.n_max, W, C) if frames == 1 else (frames, self.n_max, W, C)
+        self.blocks = [torch.zeros(shape, dtype=like.dtype, device=like.device) for _ in range(buffers)]
+        self.block = self.blocks[0]
+        many = rank == 0 and world > 1
+        fshape = (H, W, C) if frames == 1 else (frames, H, W, C)
+        self.frame = torch.zeros(fshape, dtype=like.dtype, device=like.device) if many else None
+        self.parts = [torch.empty((world,) + shape, dtype=like.dtype, device=like.device) for _ in range(buffers)] \
+            if many else None
+        self._work = [None] * buffers
 
     def rows(self):
         return cyclic_rows(self.H, self.rank, self.world)
 
-    def gather(self):
-        """collective: every rank calls it after rendering into self.block"""
+    def start(self, i=0):
+        """collective (every rank): begin gathering blocks[i] to rank 0"""
         if self.world == 1:
-            self.frame.copy_(self.block)
-            return self.frame
-        self.dist.gather(self.block, self.parts if self.rank == 0 else None, dst=0)
-        if self.rank == 0:
+            return
+        dst = list(self.parts[i]) if self.rank == 0 else None
+        self._work[i] = self.dist.gather(self.blocks[i], dst, dst=0, async_op=True)
+
+    def pending(self, i=0):
+        return self._work[i] is not None
+
+    def finish(self, i=0):
+        """wait for start(i)'s gather; rank 0: un-interleave it into self.frame and return it"""
+        if self.world == 1:
+            return self.blocks[i]
+        w, self._work[i] = self._work[i], None
+        if w is not None:
+            w.wait()
+        if self.rank != 0:
+            return None
+        P = self.parts[i]
+        frame = self.frame
+        if self.frames == 1:
+            P, frame = P.unsqueeze(1), frame.unsqueeze(0)
+        F, n = P.shape[1], self.n_max
+        if self.H % self.world == 0:  # one copy: frame row k * world + q <- rank q's compact row k
+            frame.view(F, n, self.world, self.W, self.C).copy_(P.permute(1, 2, 0, 3, 4))
+        else:
             for q in range(self.world):
                 nq = cyclic_rows(self.H, q, self.world)[2]
-                self.frame[q::self.world] = self.parts[q][:nq]
+                frame[:, q::self.world] = P[q, :, :nq]
         return self.frame
+
+    def gather(self, i=0):
+        """collective: every rank calls it after rendering into blocks[i]"""
+        self.start(i)
+        return self.finish(i)

@@ -48,6 +48,61 @@ def _worker(rank, world, port, W, H, out_path):
     dist.destroy_process_group()
 
 
+def _batch_worker(rank, world, port, W, H, out_path):
+    """two ping-pong batches of 2 frames (the bench's pattern): start(0), render batch 1 while batch 0's
+    gather runs, finish(0), start(1), finish(1); the frames of both batches must be the single frame"""
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "parallel-ray-tracer_amd"))
+    import torch
+    import torch.distributed as dist
+
+    from prt.dist import FrameGather
+    from tests.oracle_bind import OracleScene
+    from tests.scenes import scene_paths
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    o = OracleScene.load(*scene_paths("car_only"))
+    o.build_bvh(3)
+    g = FrameGather(H, W, 3, rank, world, dist, torch.zeros(1), frames=2, buffers=2)
+    ro, rs, nr = g.rows()
+    mine = torch.from_numpy(o.render(W, H, rows=(ro, rs, nr), threads=2)["rgb"][ro::rs][:nr])
+    out = []
+    for b in range(2):
+        for f in range(2):
+            g.blocks[b][f, :nr] = mine
+        g.start(b)
+        if b == 1:
+            out.append(g.finish(0).clone() if rank == 0 else None)
+    out.append(g.finish(1).clone() if rank == 0 else None)
+    if rank == 0:
+        np.save(out_path, torch.stack(out).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,H", [(2, 36), (3, 37)])
+def test_batched_pingpong_gather_equals_single_frame(tmp_path, world, H):
+    import torch.multiprocessing as mp
+
+    from tests.oracle_bind import OracleScene
+    from tests.scenes import scene_paths
+
+    W = 64  # H % world == 0: one permuted copy; else per-rank strided copies
+    out = str(tmp_path / "frames.npy")
+    mp.start_processes(_batch_worker, args=(world, _free_port(), W, H, out), nprocs=world, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    o = OracleScene.load(*scene_paths("car_only"))
+    o.build_bvh(3)
+    ref = o.render(W, H)["rgb"]
+    assert got.shape == (2, 2, H, W, 3)
+    for b in range(2):
+        for f in range(2):
+            assert np.array_equal(got[b, f].view(np.int32), ref.view(np.int32)), (b, f)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_cyclic_rows_gather_equals_single_frame(tmp_path, world):
     import torch.multiprocessing as mp

@@ -20,9 +20,10 @@ def main():
     ap.add_argument("--scene", default="dragon")
     ap.add_argument("--W", type=int, default=1920)
     ap.add_argument("--H", type=int, default=1080)
-    ap.add_argument("--frames", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--kernel", default="fast")
+    ap.add_argument("--frames", default="1", help="frames per launch (rt_render_frames), comma list")
     a = ap.parse_args()
     import torch
     from prt import device, host
@@ -30,28 +31,29 @@ def main():
     s = host.Scene.named(a.scene).build_bvh(3)
     cam = host.camera(a.W, a.H)
     out = {}
-    base = None
-    for n in [int(x) for x in a.ns.split(",")]:
-        per_rank = []
-        for q in range(n):
-            r = device.Renderer(0)
-            r.upload(s)
-            ro, rs, nr = cyclic_rows(a.H, q, n)
-            rgb = torch.empty((padded_rows(a.H, n), a.W, 3), dtype=torch.float32, device="cuda")
-            for _ in range(2):  # tuning frame + warm-up
-                r.render(cam, a.W, a.H, rows=(ro, rs, nr), kernel=a.kernel, rgb=rgb)
-                r.sync()
-            for _ in range(a.frames):
-                r.render(cam, a.W, a.H, rows=(ro, rs, nr), kernel=a.kernel, rgb=rgb)
-            ts = sorted(r.kernel_times(a.frames))
-            per_rank.append(ts[len(ts) // 2])
-            r.close()
-        mx = max(per_rank)
-        if base is None:
-            base = mx * n
-        out[n] = {"max_ms": mx, "ranks_ms": per_rank, "kernel_scaling": base / mx}
-        print(f"N={n}: max over ranks {mx:.4f} ms  ranks {['%.3f' % t for t in per_rank]}  "
-              f"kernel-only scaling {base / mx:.2f}x", flush=True)
+    for F in [int(x) for x in a.frames.split(",")]:
+        base = None
+        for n in [int(x) for x in a.ns.split(",")]:
+            per_rank = []
+            for q in range(n):
+                r = device.Renderer(0)
+                r.upload(s)
+                ro, rs, nr = cyclic_rows(a.H, q, n)
+                rgb = torch.empty((F, padded_rows(a.H, n), a.W, 3), dtype=torch.float32, device="cuda")
+                for _ in range(2):  # tuning launch + warm-up
+                    r.render_frames([cam] * F, a.W, a.H, rows=(ro, rs, nr), kernel=a.kernel, rgb=rgb)
+                    r.sync()
+                for _ in range(a.reps):
+                    r.render_frames([cam] * F, a.W, a.H, rows=(ro, rs, nr), kernel=a.kernel, rgb=rgb)
+                ts = sorted(r.kernel_times(a.reps))
+                per_rank.append(ts[len(ts) // 2] / F)
+                r.close()
+            mx = max(per_rank)
+            if base is None:
+                base = mx * n
+            out[f"F{F}_N{n}"] = {"max_ms_per_frame": mx, "ranks_ms": per_rank, "kernel_scaling": base / mx}
+            print(f"F={F} N={n}: max over ranks {mx:.4f} ms/frame  ranks {['%.3f' % t for t in per_rank]}  "
+                  f"kernel-only scaling {base / mx:.2f}x (vs N=1 at the same F)", flush=True)
     print(json.dumps({"scene": a.scene, "W": a.W, "H": a.H, "results": out}))
 
 
