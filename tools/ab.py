@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--reupload", action="store_true", help="rebuild the scene per variant (knobs read at upload)")
     ap.add_argument("--world", type=int, default=1, help="render rank --rank's cyclic rows of a --world split")
     ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=1, help="frames per launch (rt_render_frames); times are per frame")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
@@ -33,7 +34,7 @@ def main():
     cam = host.camera(a.W, a.H)
     from prt.dist import cyclic_rows
     rows = cyclic_rows(a.H, a.rank, a.world)
-    rgb = torch.empty((rows[2], a.W, 3), dtype=torch.float32, device="cuda")
+    rgb = torch.empty((a.batch, rows[2], a.W, 3), dtype=torch.float32, device="cuda")
     res = {v: [] for v in a.variants}
     rays = {}
     pixels = {}
@@ -59,13 +60,13 @@ def main():
             if a.reupload:
                 r.upload(s)
             for _ in range(a.frames):
-                r.render(cam, a.W, a.H, rows=rows, kernel=kern, rgb=rgb)
-            ts = r.kernel_times(a.frames)
+                r.render_frames([cam] * a.batch, a.W, a.H, rows=rows, kernel=kern, rgb=rgb)
+            ts = [t / a.batch for t in r.kernel_times(a.frames)]
             if rnd > 0:  # round 0 = warm-up
                 res[v] += ts
             st = r.stats()
-            rays[v] = st["rays"]
-            pixels[v] = st["pixels"]
+            rays[v] = st["rays"] // a.batch
+            pixels[v] = st["pixels"] // a.batch
             if rnd == 0:  # every variant must render the first variant's frame bit for bit
                 frame = rgb.view(torch.int32).clone()
                 if ref is None:

@@ -15,7 +15,8 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PROD = "k_persist<4, false, false, true"  # production instantiation (no counters, no trace)
+# production instantiation of the bench: k_persist, no counters, no trace, frame batch (BATCH = true)
+PROD = "k_persist<4, false, false, true, 3, false, true>"
 
 
 def rows(path):
@@ -46,7 +47,8 @@ def main():
     # kernel trace stats
     stats = rows(os.path.join(prof, "trace", "run_kernel_stats.csv"))
     lines = [f"# rocprofv3 --kernel-trace --stats ({tag})", "",
-             f"command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline`",
+             f"command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 64 --warmup 16 --no-cpu-baseline`"
+             f" (16 frames per launch: one launch = 16 frames)",
              "", "| kernel | calls | total ms | avg ms | min ms | max ms | % |", "|---|---|---|---|---|---|---|"]
     for r in stats:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "

@@ -17,7 +17,7 @@ step() {  # name timeout cmd...
     echo "=== $name rc=$rc" | tee -a $out/session.log
     if [ $rc -ne 0 ]; then tail -20 $out/$name.log; exit $rc; fi
 }
-B="python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline $args"
+B="python3 bench.py --steps 64 --warmup 16 --no-cpu-baseline $args"
 step trace 600 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- $B
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d $out/pmc_fetch -o run --output-format csv -- $B
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d $out/pmc_write -o run --output-format csv -- $B
