@@ -130,12 +130,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-rank flow on a one-GPU box (never set by the driver): PRT_DIST_ONE_GPU=1 puts
+    # every rank on device 0, PRT_DIST_BACKEND=gloo replaces RCCL (which refuses two ranks on one GPU)
+    if os.environ.get("PRT_DIST_ONE_GPU") == "1":
+        local = 0
+    backend = os.environ.get("PRT_DIST_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from prt import device, host
     from prt.dist import FrameGather

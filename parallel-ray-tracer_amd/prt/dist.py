@@ -27,7 +27,9 @@ class FrameGather:
     [frames, H, W, C], one collective for the whole batch. buffers > 1: ping-pong blocks, so that the
     gather of batch k (start(k % buffers), asynchronous on the collective's stream) overlaps the render of
     batch k + 1 into the other block; finish(i) makes the current stream wait for it and un-interleaves.
-    World 1: the block IS the frame (no collective, no copy)."""
+    World 1: the block IS the frame (no collective, no copy). On a GPU, rank 0 un-interleaves on a side
+    stream, so the copy (F frames of H x W x C) does not delay rank 0's next render — which every rank's
+    next gather would wait for."""
 
     def __init__(self, H, W, C, rank, world, dist, like, frames=1, buffers=1):
         import torch
@@ -43,6 +45,9 @@ class FrameGather:
         self.parts = [torch.empty((world,) + shape, dtype=like.dtype, device=like.device) for _ in range(buffers)] \
             if many else None
         self._work = [None] * buffers
+        cuda = like.device.type == "cuda" and many
+        self._side = torch.cuda.Stream(device=like.device) if cuda else None
+        self._copied = [None] * buffers  # side-stream event: parts[i] read by the un-interleave
 
     def rows(self):
         return cyclic_rows(self.H, self.rank, self.world)
@@ -51,6 +56,10 @@ class FrameGather:
         """collective (every rank): begin gathering blocks[i] to rank 0"""
         if self.world == 1:
             return
+        if self._copied[i] is not None:  # parts[i] is still being read by the last un-interleave
+            import torch
+            torch.cuda.current_stream().wait_event(self._copied[i])
+            self._copied[i] = None
         dst = list(self.parts[i]) if self.rank == 0 else None
         self._work[i] = self.dist.gather(self.blocks[i], dst, dst=0, async_op=True)
 
@@ -63,9 +72,20 @@ class FrameGather:
             return self.blocks[i]
         w, self._work[i] = self._work[i], None
         if w is not None:
-            w.wait()
+            w.wait()  # the current stream waits for the gather (blocks[i] may be rendered into again)
         if self.rank != 0:
             return None
+        if self._side is not None:
+            import torch
+            self._side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self._side):
+                self._uninterleave(i)
+            self._copied[i] = self._side.record_event()
+        else:
+            self._uninterleave(i)
+        return self.frame
+
+    def _uninterleave(self, i):
         P = self.parts[i]
         frame = self.frame
         if self.frames == 1:
@@ -77,9 +97,13 @@ class FrameGather:
             for q in range(self.world):
                 nq = cyclic_rows(self.H, q, self.world)[2]
                 frame[:, q::self.world] = P[q, :, :nq]
-        return self.frame
 
     def gather(self, i=0):
-        """collective: every rank calls it after rendering into blocks[i]"""
+        """collective: every rank calls it after rendering into blocks[i]; the returned frame is ready on
+        the current stream"""
         self.start(i)
-        return self.finish(i)
+        out = self.finish(i)
+        if self._side is not None:
+            import torch
+            torch.cuda.current_stream().wait_event(self._copied[i])
+        return out
