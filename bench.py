@@ -108,7 +108,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=64, help="timed frames")
     ap.add_argument("--warmup", type=int, default=16, help="untimed frames (after the tuning launches)")
-    ap.add_argument("--frames", type=int, default=0, help="frames per launch (0: 16 x world size, at most --steps)")
+    ap.add_argument("--frames", type=int, default=16, help="frames per launch (at most --steps)")
+    ap.add_argument("--streams", type=int, default=0, help="contexts on their own streams, launches alternating "
+                    "(0: 1 at N = 1, 2 at N > 1)")
+    ap.add_argument("--row-block", type=int, default=0,
+                    help="N > 1: rows dealt to ranks in blocks of this many (0: 8, so 8x8 tiles stay 8x8 in the image)")
     ap.add_argument("--scene", default="dragon")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -153,40 +157,53 @@ def main():
     files = scene_paths(args.scene)
     scene = host.Scene.load(*files).build_bvh(args.bvh)
     stream = torch.cuda.current_stream().cuda_stream
-    r = device.Renderer(local, stream=stream)
-    r.upload(scene, accel=args.accel)
+    # N > 1: two contexts on two streams, launches alternating: a launch's tail (its longest reflection
+    # chains) overlaps the next launch's work (tools/rank_rows.py --streams 2: 8-GPU rank rows 0.191 ->
+    # 0.160 ms per frame; a whole frame at N = 1 gains ~1 %, and one stream keeps its launch durations —
+    # the roofline's denominator — unshared)
+    n_streams = args.streams or (1 if world == 1 else 2)
+    streams = [torch.cuda.Stream() for _ in range(n_streams)]
+    rends = [device.Renderer(local, stream=s.cuda_stream) for s in streams]
+    for rr_ in rends:
+        rr_.upload(scene, accel=args.accel)
     cam = host.camera(W, H)
     K = args.steps
-    F = max(1, min(args.frames or 16 * world, K))
+    F = max(1, min(args.frames, K))
     plan = [F] * (K // F) + ([K % F] if K % F else [])  # launches covering exactly K frames
-    # cyclic rows y = rank + k * world, gathered to rank 0 with one RCCL collective per batch (prt/dist.py,
-    # tested with gloo in tests/test_multi.py); two ping-pong blocks so a batch's gather overlaps the next
-    # batch's render
+    # rows: 8-row blocks dealt cyclically to the ranks (an 8x8 tile of a rank's rows is an 8x8 tile of the
+    # image; costs average out over the blocks), gathered to rank 0 with one RCCL collective per batch
+    # (prt/dist.py, tested with gloo in tests/test_multi.py); two ping-pong blocks so a batch's gather
+    # overlaps the next batch's render
+    B = args.row_block if args.row_block > 0 else (8 if world > 1 else 1)
     fg = FrameGather(H, W, 3, rank, world, dist, like=torch.empty(0, dtype=torch.float32, device="cuda"),
-                     frames=F, buffers=2)
-    _, _, n_r = fg.rows()
+                     frames=F, buffers=2, block=B)
+    my_rows = fg.rows()
+    n_r = my_rows[2]
     launch_no = [0]
 
     def launch(nf):
         b = launch_no[0] % 2
+        c = launch_no[0] % n_streams
         launch_no[0] += 1
-        if fg.pending(b):
-            fg.finish(b)
-        r.render_frames([cam] * nf, W, H, rows=(rank, world, n_r), bounces=args.bounces, spp=args.spp,
-                        kernel=args.kernel, rgb=fg.blocks[b])
-        fg.start(b)
+        with torch.cuda.stream(streams[c]):  # block b is rendered by context c on its stream
+            if fg.pending(b):
+                fg.finish(b)
+            rends[c].render_frames([cam] * nf, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
+                                   kernel=args.kernel, rgb=fg.blocks[b])
+            fg.start(b)
 
     def drain():
         for b in range(2):
-            if fg.pending(b):
-                fg.finish(b)
+            with torch.cuda.stream(streams[b % n_streams]):
+                if fg.pending(b):
+                    fg.finish(b)
 
     # setup, like the upload: the first launch of a scene and batch shape is rt_render's launch-autotuning
     # launch (every candidate configuration timed, rt_hip.hip); the next launch of that shape reads the
     # timings. Each batch size of the plan is tuned here, then `warmup` frames run untimed.
     for nf in sorted(set(plan)):
-        launch(nf)
-        launch(nf)
+        for _ in range(2 * n_streams):  # per context: the tuning launch, then the launch reading its timings
+            launch(nf)
     for _ in range(max(1, -(-args.warmup // F))):
         launch(F)
     drain()
@@ -195,7 +212,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    timed = []  # (context, frames) of every timed launch
     for nf in plan:
+        timed.append((launch_no[0] % n_streams, nf))
         launch(nf)
     drain()
     torch.cuda.synchronize()
@@ -203,9 +222,16 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    ktimes = r.kernel_times(min(len(plan), 64))
-    kfull = [t for t, nf in zip(ktimes, plan[-len(ktimes):]) if nf == F] or ktimes
-    st = r.stats()
+    # per-launch kernel times of both contexts (HIP events on each launch's stream; overlapping launches
+    # share the chip, so each one's duration is longer than its share of the wall time)
+    kfull = []
+    for b, rr_ in enumerate(rends):
+        mine = [nf for (c, nf) in timed if c == b][-64:]  # this context's timed launches (the last ones)
+        ts_ = rr_.kernel_times(len(mine)) if mine else []
+        kfull += [t for t, nf in zip(ts_, mine) if nf == F]
+    kfull = kfull or [float("nan")]
+    last = rends[timed[-1][0]]
+    st = last.stats()
     # whole-job ray count per frame (identical every frame: the render is deterministic), from the last
     # launch's counters (a batch: the sum over its frames)
     rays_local = st["rays"] // plan[-1]
@@ -220,7 +246,7 @@ def main():
     # algorithmic bytes of this rank's full-batch launch: one extra untimed launch with traversal counters
     rc = device.Renderer(local, counters=True, stream=stream)
     rc.upload(scene, accel=args.accel)
-    rc.render_frames([cam] * F, W, H, rows=(rank, world, n_r), bounces=args.bounces, spp=args.spp,
+    rc.render_frames([cam] * F, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
                      kernel=args.kernel, rgb=fg.blocks[0])
     stc = rc.stats()
     rc.close()
@@ -230,7 +256,7 @@ def main():
     rl = device.Renderer(local, stream=stream)
     rl.upload(scene, accel=args.accel)
     for _ in range(3):
-        rl.render(cam, W, H, rows=(rank, world, n_r), bounces=args.bounces, spp=args.spp, kernel=args.kernel,
+        rl.render(cam, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp, kernel=args.kernel,
                   rgb=fg.blocks[0])
     lat_ms = sorted(rl.kernel_times(2))[0]
     rl.close()
@@ -268,14 +294,17 @@ def main():
                                    f"traversal+intersect+shade persistent launch per batch of {F} frames",
                        "scene": args.scene, "triangles": scene.n_triangles, "lights": len(scene.lights),
                        "width": W, "height": H, "bvh": args.bvh, "accel": args.accel, "kernel": args.kernel,
-                       "rays_per_frame": rays_frame, "parallelism": f"rows-cyclic x{world} + RCCL gather"
+                       "rays_per_frame": rays_frame, "parallelism": f"{B}-row blocks cyclic x{world} + RCCL gather"
                        if world > 1 else "single GPU", "frames_per_launch": F},
             "frame_latency_ms": lat.item(),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": k_avg_ms, "alg_bytes_per_launch": bytes_launch, "frames_per_launch": F,
-                         "note": "algorithmic bytes (node/triangle/shading records the kernel reads) / HIP-event "
-                                 "kernel time; the ~10 MB scene stays L2/MALL-resident, so HBM traffic is far lower"},
+                         "achieved_steady": bytes_launch / F * K / elapsed / 1e9, "streams": n_streams,
+                         "note": "algorithmic bytes (node/triangle/shading records the kernel reads) of one launch / "
+                                 "its HIP-event duration (two launches overlap on two streams, so this is "
+                                 "conservative; achieved_steady = the same bytes per frame x frames / wall time); "
+                                 "the ~6 MB scene stays L2/MALL-resident, so HBM traffic is far lower"},
         }
         if world == 1 and not args.no_cpu_baseline:
             def gpu_rays_for_rows(stride):
@@ -292,7 +321,8 @@ def main():
             except Exception as e:  # reported, never silently replaced
                 result["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(result), flush=True)
-    r.close()
+    for rr_ in rends:
+        rr_.close()
     if dist:
         dist.barrier()
         dist.destroy_process_group()

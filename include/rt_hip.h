@@ -69,14 +69,18 @@ enum {
     RT_KERNEL_WAVE = 4    /* persistent per-lane ray state machine in one kernel (k_wave); A/B only */
 };
 
-/* Rows rendered: y = row_offset + k * row_stride for k in [0, n_rows). Output rows are compact:
- * row k of the output holds image row y. A full frame is {W, H, 0, 1, H, ...}. */
+/* Rows rendered: y = row_offset + (k / B) * row_stride + k % B for k in [0, n_rows), B = max(1, row_block)
+ * (B = 1: y = row_offset + k * row_stride). Output rows are compact: row k of the output holds image
+ * row y. A full frame is {W, H, 0, 1, H, ...}. Rank q of N, cyclic rows: {.., q, N, ..}; block-cyclic
+ * rows (blocks of B rows dealt cyclically, so a rank's 8x8 pixel tiles stay 8x8 in the image):
+ * {.., q * B, N * B, .., row_block = B}. */
 typedef struct rt_frame {
     int width, height;
     int row_offset, row_stride, n_rows;
     int bounces; /* BOUNCES (cpu/include/options.h:52), 1..8; the reference uses 4 */
     int spp;     /* 1 = the reference's pixel-corner ray; s*s = s x s stratified grid, mean of clamped samples */
     int kernel;  /* RT_KERNEL_* */
+    int row_block; /* 0 or 1: single rows; B > 1: rows in blocks of B (row_stride >= B) */
 } rt_frame;
 
 /* Device output pointers (all nullable). rgb: [n_rows][width][3] f32 in [0,1] = vec_t pixels

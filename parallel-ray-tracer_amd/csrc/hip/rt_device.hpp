@@ -86,7 +86,7 @@ struct KArgs {
     // its outputs at pixel offset f * frame_px (frame_px = n_rows * W)
     const float* cams;
     int n_frames;
-    int frames_pad;
+    int row_block;  // rows in blocks of row_block (>= 1): image row of compact row k = image_row()
     unsigned long long frame_px;
 };
 

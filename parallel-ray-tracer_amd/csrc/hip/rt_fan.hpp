@@ -129,7 +129,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         unsigned long long tr0 = 0;
         const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
         if (TRACE) tr0 = __builtin_amdgcn_s_memrealtime();
-        const int y = A.row_offset + k * A.row_stride;
+        const int y = image_row(A, k);
         const size_t po = (size_t)frame * A.frame_px + (size_t)k * A.W + x;
         if (valid && role == 0 && A.bounce_hit)
             for (int i = 0; i < A.bounces; i++) A.bounce_hit[po * (size_t)A.bounces + i] = -2;

@@ -70,7 +70,7 @@ struct rt_ctx {
     float* last_rgb = nullptr;
     int* last_hit = nullptr;
     size_t last_pixels = 0;
-    int last_W = 0, last_H = 0, last_off = 0, last_stride = 1, last_rows = 0;  // the last frame's rows
+    int last_W = 0, last_H = 0, last_off = 0, last_stride = 1, last_rows = 0, last_block = 1;  // the last frame's rows
     int last_frames = 1;     // frames of the last render (rt_render_frames)
     bool batch_sum = false;  // set while rt_render_frames launches frames one by one (counters add up)
     // frame batches: the cameras on the device (d_cams) and the host copy they were uploaded from
@@ -639,8 +639,10 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     if (!cams || !f) return arg_err(ctx, "rt_render: null camera/frame");
     if (n_frames < 1 || n_frames > 4096) return arg_err(ctx, "rt_render_frames: n_frames must be 1..4096");
     const rt_camera* cam = cams;
+    const int rb = f->row_block > 1 ? f->row_block : 1;
     if (f->width <= 0 || f->height <= 0 || f->row_stride <= 0 || f->n_rows <= 0 || f->row_offset < 0 ||
-        (long long)f->row_offset + (long long)(f->n_rows - 1) * f->row_stride >= f->height)
+        f->row_block < 0 || (f->n_rows > rb && f->row_stride < rb) ||
+        (long long)f->row_offset + (long long)((f->n_rows - 1) / rb) * f->row_stride + (f->n_rows - 1) % rb >= f->height)
         return arg_err(ctx, "rt_render: rows outside the frame");
     if (f->bounces < 1 || f->bounces > 8) return arg_err(ctx, "rt_render: bounces must be 1..8");
     int g = 1;
@@ -685,6 +687,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     A.H = f->height;
     A.row_offset = f->row_offset;
     A.row_stride = f->row_stride;
+    A.row_block = rb;
     A.n_rows = f->n_rows;
     A.bounces = f->bounces;
     A.spp = f->spp;
@@ -701,7 +704,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     // the wavefront pipeline and k_wave render 1 spp; spp > 1 goes to the per-pixel path kernel
     if ((kernel == RT_KERNEL_WAVEFRONT || kernel == RT_KERNEL_WAVE) && (f->spp > 1 || (out && out->bounce_hit)))
         kernel = RT_KERNEL_FAST;  // spp > 1 and per-level hit dumps: the fused path kernels
-    if ((f->bounces > rtd::WF_MAXB || ctx->n_lights > 32) && kernel == RT_KERNEL_WAVEFRONT) kernel = RT_KERNEL_FAST;
+    if ((f->bounces > rtd::WF_MAXB || ctx->n_lights > 32 || rb > 1) && kernel == RT_KERNEL_WAVEFRONT)
+        kernel = RT_KERNEL_FAST;  // (the wavefront pipeline's primary-ray stage takes single rows only)
     if (n_frames > 1 && kernel != RT_KERNEL_FAST) {  // one launch per frame, outputs at frame offsets
         for (int i = 0; i < n_frames; i++) {
             rt_outputs o{rgb + 3 * pixels * i, A.hit ? A.hit + pixels * i : nullptr, A.t ? A.t + pixels * i : nullptr,
@@ -970,6 +974,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     ctx->last_off = f->row_offset;
     ctx->last_stride = f->row_stride;
     ctx->last_rows = f->n_rows;
+    ctx->last_block = rb;
     ctx->rendered = true;
     return RT_OK;
 }
@@ -1083,7 +1088,7 @@ extern "C" int rt_gather(rt_ctx* const* ctxs, int n, int root) {
         if (c->last_W != W || c->last_H != H) return arg_err(ctx, "rt_gather: frame sizes differ");
         if (c->last_frames != 1) return arg_err(ctx, "rt_gather: the last render was a frame batch");
         for (int k = 0; k < c->last_rows; k++) {
-            const long long y = c->last_off + (long long)k * c->last_stride;
+            const long long y = c->last_off + (long long)(k / c->last_block) * c->last_stride + k % c->last_block;
             if (y < 0 || y >= H || cover[y]) return arg_err(ctx, "rt_gather: row sets do not partition the frame");
             cover[y] = 1;
         }
@@ -1129,7 +1134,7 @@ extern "C" int rt_gather(rt_ctx* const* ctxs, int n, int root) {
         const int grid = (int)std::max<size_t>(1, std::min<size_t>((cpx + 255) / 256, 4096));
         rtd::k_unshuffle<<<grid, 256, 0, ctx->stream>>>(src, all_hit ? src_hit : nullptr, ctx->d_full,
                                                          all_hit ? ctx->d_full_hit : nullptr, W, c->last_off,
-                                                         c->last_stride, c->last_rows);
+                                                         c->last_stride, c->last_rows, c->last_block);
         HIPC(hipGetLastError());
     }
     HIPC(hipEventRecord(ctx->ev1, ctx->stream));
@@ -1139,6 +1144,7 @@ extern "C" int rt_gather(rt_ctx* const* ctxs, int n, int root) {
     ctx->last_off = 0;
     ctx->last_stride = 1;
     ctx->last_rows = H;
+    ctx->last_block = 1;
     return RT_OK;
 }
 
@@ -1150,7 +1156,7 @@ extern "C" int rt_download_bmp(rt_ctx* ctx, unsigned char* h_bmp, size_t cap) {
     }
     if (ctx->last_frames != 1) return arg_err(ctx, "rt_download_bmp: the last render was a frame batch");
     const int W = ctx->last_W, H = ctx->last_H;
-    if (ctx->last_off != 0 || ctx->last_stride != 1 || ctx->last_rows != H) {
+    if (ctx->last_off != 0 || ctx->last_stride != ctx->last_block || ctx->last_rows != H) {
         ctx->err = "rt_download_bmp: the last frame is not a full frame (gather it first)";
         return RT_E_STATE;
     }

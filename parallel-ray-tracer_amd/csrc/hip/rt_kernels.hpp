@@ -729,6 +729,11 @@ __device__ __forceinline__ v3 clamp01(v3 c) {  // vec_constrain(col, 0, 1), vec.
     return mk(fminf(fmaxf(c.x, 0.0f), 1.0f), fminf(fmaxf(c.y, 0.0f), 1.0f), fminf(fmaxf(c.z, 0.0f), 1.0f));
 }
 
+// image row of compact output row k (rt_frame: rows in blocks of row_block, blocks row_stride apart)
+__device__ __forceinline__ int image_row(const KArgs& A, int k) {
+    return A.row_offset + (k / A.row_block) * A.row_stride + k % A.row_block;
+}
+
 // one frame's camera constants (main.c:243-250)
 struct Cam {
     v3 pos, ul, ix, iy;
@@ -764,7 +769,7 @@ __device__ __forceinline__ v3 primary_dir(const KArgs& A, float fx, float fy) {
 template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1>
 __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int frame, int x, int k,
                                              int* __restrict__ stk, Ctr& c, unsigned q = 0) {
-    const int y = A.row_offset + k * A.row_stride;
+    const int y = image_row(A, k);
     const size_t o = (size_t)frame * A.frame_px + (size_t)k * A.W + x;
     int hit0 = -1;
     float t0 = FMAX;
@@ -919,7 +924,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                     if (A.bounce_hit)
                         for (int i = 0; i < A.bounces; i++) A.bounce_hit[((size_t)k * A.W + x) * A.bounces + i] = -2;
                     o = mk(A.pos[0], A.pos[1], A.pos[2]);
-                    d = primary_dir(A, (float)x, (float)(A.row_offset + k * A.row_stride));
+                    d = primary_dir(A, (float)x, (float)image_row(A, k));
                 }
             }
             nxt += take;

@@ -4,15 +4,16 @@
 
 namespace rtd {
 
-// Compact rows of one context's frame (row k = image row off + k * stride) into the full frame.
-// One thread per float4 of a row would need W % 4 == 0; rows are f32 x 3, so one thread per pixel.
+// Compact rows of one context's frame (row k = image row off + (k / block) * stride + k % block, rt_frame)
+// into the full frame. One thread per float4 of a row would need W % 4 == 0; rows are f32 x 3, so one
+// thread per pixel.
 __global__ __launch_bounds__(256) void k_unshuffle(const float* __restrict__ src, const int* __restrict__ src_hit,
                                                    float* __restrict__ dst, int* __restrict__ dst_hit, int W,
-                                                   int off, int stride, int rows) {
+                                                   int off, int stride, int rows, int block) {
     const size_t n = (size_t)W * rows;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const size_t k = i / W, x = i % W;
-        const size_t o = ((size_t)off + k * stride) * W + x;
+        const size_t o = ((size_t)off + (k / block) * stride + k % block) * W + x;
         dst[3 * o] = src[3 * i];
         dst[3 * o + 1] = src[3 * i + 1];
         dst[3 * o + 2] = src[3 * i + 2];

@@ -51,7 +51,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
             c.pix++;
             const size_t px = (size_t)k * A.W + x;
             v3 o = mk(A.pos[0], A.pos[1], A.pos[2]);
-            v3 d = primary_dir(A, (float)x, (float)(A.row_offset + k * A.row_stride));
+            v3 d = primary_dir(A, (float)x, (float)image_row(A, k));
             if (A.bounce_hit)
                 for (int i = 0; i < A.bounces; i++) A.bounce_hit[px * A.bounces + i] = -2;
             for (int it = 0; it < A.bounces; ++it) {

@@ -108,7 +108,7 @@ __device__ __forceinline__ void wave_body(const KArgs& A, int* __restrict__ stk)
 
             if (ph == PH_START) {  // render_pixel, main.c:228-239: primary ray
                 const int k = pix / A.W, x = pix - k * A.W;
-                const int y = A.row_offset + k * A.row_stride;
+                const int y = image_row(A, k);
                 o = mk(A.pos[0], A.pos[1], A.pos[2]);
                 d = primary_dir(A, (float)x, (float)y);
                 it = 0;

@@ -57,6 +57,13 @@ def _ptr(x):
     return x.data_ptr()
 
 
+def _rows(rows, height):
+    """rows tuple (offset, stride, n) or (offset, stride, n, block) -> rt_frame fields; None = full frame"""
+    if rows is None:
+        return 0, 1, height, 1
+    return (tuple(rows) + (1,))[:4]
+
+
 class Renderer:
     """One rt_ctx on one device (gpu.cuh:23-26 seam, explicit instead of global)."""
 
@@ -93,10 +100,11 @@ class Renderer:
 
     def render(self, cam, width, height, rows=None, bounces=4, spp=1, kernel="auto", rgb=None, hit=None, t=None,
                bounce_hit=None):
-        """render_frame(): asynchronous. rows = (offset, stride, n) or None for the full frame.
+        """render_frame(): asynchronous. rows = (offset, stride, n[, block]) (rt_frame; prt.dist) or None for
+        the full frame.
         rgb / hit / t / bounce_hit ([n, W, bounces] int32): optional device tensors (torch) or raw pointers."""
-        ro, rs, nr = rows if rows is not None else (0, 1, height)
-        f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel))
+        ro, rs, nr, rb = _rows(rows, height)
+        f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel), rb)
         out = Outputs(_ptr(rgb), _ptr(hit), _ptr(t), _ptr(bounce_hit))
         self._chk(_L.rt_render(self._ctx, ctypes.byref(cam), ctypes.byref(f), ctypes.byref(out)), "rt_render")
         self._last = (width, nr)
@@ -107,8 +115,8 @@ class Renderer:
                       t=None, bounce_hit=None):
         """rt_render_frames(): a batch of len(cams) frames of one shape (one persistent launch on the fast
         kernel); outputs [n_frames, n_rows, W, ...]. Asynchronous."""
-        ro, rs, nr = rows if rows is not None else (0, 1, height)
-        f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel))
+        ro, rs, nr, rb = _rows(rows, height)
+        f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel), rb)
         out = Outputs(_ptr(rgb), _ptr(hit), _ptr(t), _ptr(bounce_hit))
         arr = (Camera * len(cams))(*cams)
         self._chk(_L.rt_render_frames(self._ctx, arr, len(cams), ctypes.byref(f), ctypes.byref(out)),

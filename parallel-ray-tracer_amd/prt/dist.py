@@ -16,8 +16,29 @@ def cyclic_rows(H, rank, world):
     return rank, world, (H - rank + world - 1) // world
 
 
-def padded_rows(H, world):
-    return (H + world - 1) // world
+def padded_rows(H, world, block=1):
+    """rows of the largest rank block (every rank's block is padded to it for the gather)"""
+    return max(rank_rows(H, q, world, block)[2] for q in range(world)) if block > 1 else (H + world - 1) // world
+
+
+def rank_rows(H, rank, world, block=1):
+    """rt_frame rows of rank `rank`: (row_offset, row_stride, n_rows, row_block). block = 1: cyclic rows
+    (y = rank + k * world); block = B: blocks of B consecutive rows dealt cyclically (block j on rank
+    j % world), so an 8x8 pixel tile of a rank's compact rows is an 8x8 tile of the image (B = 8) while
+    the ranks' costs still average out over the ~H / (B * world) blocks each."""
+    if block <= 1:
+        return cyclic_rows(H, rank, world) + (1,)
+    if not (0 <= rank < world) or H <= 0:
+        raise ValueError("bad rank/world/height")
+    nb = (H + block - 1) // block
+    n = sum(min(block, H - j * block) for j in range(rank, nb, world))
+    return rank * block, world * block, n, block
+
+
+def image_rows(H, rank, world, block=1):
+    """image row of each of rank `rank`'s compact rows (rt_frame: off + (k // B) * stride + k % B)"""
+    off, stride, n, b = rank_rows(H, rank, world, block)
+    return [off + (k // b) * stride + k % b for k in range(n)]
 
 
 class FrameGather:
@@ -31,11 +52,12 @@ class FrameGather:
     stream, so the copy (F frames of H x W x C) does not delay rank 0's next render — which every rank's
     next gather would wait for."""
 
-    def __init__(self, H, W, C, rank, world, dist, like, frames=1, buffers=1):
+    def __init__(self, H, W, C, rank, world, dist, like, frames=1, buffers=1, block=1):
         import torch
         self.H, self.W, self.C, self.rank, self.world, self.dist = H, W, C, rank, world, dist
         self.frames = frames
-        self.n_max = padded_rows(H, world)
+        self.bk = max(1, block)
+        self.n_max = padded_rows(H, world, self.bk)
         shape = (self.n_max, W, C) if frames == 1 else (frames, self.n_max, W, C)
         self.blocks = [torch.zeros(shape, dtype=like.dtype, device=like.device) for _ in range(buffers)]
         self.block = self.blocks[0]
@@ -48,9 +70,15 @@ class FrameGather:
         cuda = like.device.type == "cuda" and many
         self._side = torch.cuda.Stream(device=like.device) if cuda else None
         self._copied = [None] * buffers  # side-stream event: parts[i] read by the un-interleave
+        self._idx = None
+        if many and self.bk > 1 and H % (world * self.bk) != 0:  # general block layout: index copies
+            self._idx = [torch.tensor(image_rows(H, q, world, self.bk), dtype=torch.long, device=like.device)
+                         for q in range(world)]
 
     def rows(self):
-        return cyclic_rows(self.H, self.rank, self.world)
+        """this rank's rt_frame rows: (offset, stride, n) for single rows, (offset, stride, n, block)"""
+        r = rank_rows(self.H, self.rank, self.world, self.bk)
+        return r if self.bk > 1 else r[:3]
 
     def start(self, i=0):
         """collective (every rank): begin gathering blocks[i] to rank 0"""
@@ -91,7 +119,15 @@ class FrameGather:
         if self.frames == 1:
             P, frame = P.unsqueeze(1), frame.unsqueeze(0)
         F, n = P.shape[1], self.n_max
-        if self.H % self.world == 0:  # one copy: frame row k * world + q <- rank q's compact row k
+        if self.bk > 1:
+            if self._idx is None:  # one copy: frame row (m * world + q) * B + r <- rank q's row m * B + r
+                M, B = self.H // (self.world * self.bk), self.bk
+                frame.view(F, M, self.world, B, self.W, self.C).copy_(
+                    P.view(self.world, F, M, B, self.W, self.C).permute(1, 2, 0, 3, 4, 5))
+            else:
+                for q in range(self.world):
+                    frame.index_copy_(1, self._idx[q], P[q, :, :len(self._idx[q])])
+        elif self.H % self.world == 0:  # one copy: frame row k * world + q <- rank q's compact row k
             frame.view(F, n, self.world, self.W, self.C).copy_(P.permute(1, 2, 0, 3, 4))
         else:
             for q in range(self.world):

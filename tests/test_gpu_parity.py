@@ -109,10 +109,16 @@ def test_1080p_vs_reference_sample(dev, scenes, kernel, scene):
 
 @pytest.mark.parametrize("kernel", KERNELS)
 def test_row_subset_equals_full_frame(dev, scenes, kernel):
+    """compact row sets (rt_frame rows): cyclic single rows, and blocks of rows (row_block; the last
+    block partial) — every row equal to the full frame's"""
     full = render(dev, scenes["car_boxed"], 320, 180, kernel)
     part = render(dev, scenes["car_boxed"], 320, 180, kernel, rows=(5, 8, 22))
     rows = [5 + 8 * k for k in range(22)]
     assert same_bits(part["rgb"], full["rgb"][rows])
+    np.testing.assert_array_equal(part["hit"], full["hit"][rows])
+    part = render(dev, scenes["car_boxed"], 320, 180, kernel, rows=(8, 24, 37, 8))
+    rows = [8 + (k // 8) * 24 + k % 8 for k in range(37)]
+    assert same_bits(part["rgb"], full["rgb"][rows]), kernel
     np.testing.assert_array_equal(part["hit"], full["hit"][rows])
 
 
@@ -294,17 +300,19 @@ def test_gather_rows_of_several_contexts(dev, scenes, n):
     full = render(dev, scenes["car_boxed"], W, H, "fast")
     rs = [dev.Renderer(0) for _ in range(n)]
     bufs = []
-    for g, r in enumerate(rs):
-        r.upload(scenes["car_boxed"])
-        nr = (H - g + n - 1) // n
-        hit = torch.empty((nr, W), dtype=torch.int32, device="cuda")
-        r.render(host.camera(W, H), W, H, rows=(g, n, nr), hit=hit)
-        bufs.append(hit)
-    dev.gather(rs, root=1)
-    rgb, hit = rs[1].download(hit=True)
-    assert same_bits(rgb, full["rgb"])
-    np.testing.assert_array_equal(hit, full["hit"])
-    assert rs[1].download_bmp() == host.bmp_encode(full["rgb"])
+    from prt.dist import rank_rows
+    for block in (1, 8):  # cyclic rows, then 8-row blocks dealt cyclically (the bench's N > 1 layout)
+        for g, r in enumerate(rs):
+            r.upload(scenes["car_boxed"])
+            rows = rank_rows(H, g, n, block)
+            hit = torch.empty((rows[2], W), dtype=torch.int32, device="cuda")
+            r.render(host.camera(W, H), W, H, rows=rows, hit=hit)
+            bufs.append(hit)
+        dev.gather(rs, root=1)
+        rgb, hit = rs[1].download(hit=True)
+        assert same_bits(rgb, full["rgb"]), block
+        np.testing.assert_array_equal(hit, full["hit"])
+        assert rs[1].download_bmp() == host.bmp_encode(full["rgb"])
     bad = dev.Renderer(0)
     bad.upload(scenes["car_boxed"])
     bad.render(host.camera(W, H), W, H, rows=(0, 2, 57))

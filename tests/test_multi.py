@@ -48,7 +48,7 @@ def _worker(rank, world, port, W, H, out_path):
     dist.destroy_process_group()
 
 
-def _batch_worker(rank, world, port, W, H, out_path):
+def _batch_worker(rank, world, port, W, H, out_path, block):
     """two ping-pong batches of 2 frames (the bench's pattern): start(0), render batch 1 while batch 0's
     gather runs, finish(0), start(1), finish(1); the frames of both batches must be the single frame"""
     import sys
@@ -65,9 +65,11 @@ def _batch_worker(rank, world, port, W, H, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     o = OracleScene.load(*scene_paths("car_only"))
     o.build_bvh(3)
-    g = FrameGather(H, W, 3, rank, world, dist, torch.zeros(1), frames=2, buffers=2)
-    ro, rs, nr = g.rows()
-    mine = torch.from_numpy(o.render(W, H, rows=(ro, rs, nr), threads=2)["rgb"][ro::rs][:nr])
+    g = FrameGather(H, W, 3, rank, world, dist, torch.zeros(1), frames=2, buffers=2, block=block)
+    from prt.dist import image_rows
+    rows = image_rows(H, rank, world, block)
+    nr = len(rows)
+    mine = torch.from_numpy(o.render(W, H, threads=2)["rgb"][rows])
     out = []
     for b in range(2):
         for f in range(2):
@@ -82,8 +84,8 @@ def _batch_worker(rank, world, port, W, H, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,H", [(2, 36), (3, 37)])
-def test_batched_pingpong_gather_equals_single_frame(tmp_path, world, H):
+@pytest.mark.parametrize("world,H,block", [(2, 36, 1), (3, 37, 1), (2, 32, 8), (3, 37, 4)])
+def test_batched_pingpong_gather_equals_single_frame(tmp_path, world, H, block):
     import torch.multiprocessing as mp
 
     from tests.oracle_bind import OracleScene
@@ -91,7 +93,7 @@ def test_batched_pingpong_gather_equals_single_frame(tmp_path, world, H):
 
     W = 64  # H % world == 0: one permuted copy; else per-rank strided copies
     out = str(tmp_path / "frames.npy")
-    mp.start_processes(_batch_worker, args=(world, _free_port(), W, H, out), nprocs=world, join=True,
+    mp.start_processes(_batch_worker, args=(world, _free_port(), W, H, out, block), nprocs=world, join=True,
                        start_method="spawn")
     got = np.load(out)
     o = OracleScene.load(*scene_paths("car_only"))
@@ -119,6 +121,22 @@ def test_cyclic_rows_gather_equals_single_frame(tmp_path, world):
     o.build_bvh(3)
     ref = o.render(W, H)["rgb"]
     assert np.array_equal(got.view(np.int32), ref.view(np.int32))
+
+
+def test_block_cyclic_partition_covers_every_row_once():
+    from prt.dist import image_rows, padded_rows, rank_rows
+    for H in (1, 7, 37, 1080, 2160):
+        for N in (1, 2, 3, 4, 8):
+            for B in (2, 4, 8):
+                seen = []
+                for r in range(N):
+                    off, stride, n, b = rank_rows(H, r, N, B)
+                    assert n <= padded_rows(H, N, B) and b == B
+                    rows = image_rows(H, r, N, B)
+                    assert len(rows) == n and all(0 <= y < H for y in rows)
+                    assert rows == sorted(rows)
+                    seen += rows
+                assert sorted(seen) == list(range(H)), (H, N, B)
 
 
 def test_cyclic_partition_covers_every_row_once():

@@ -24,10 +24,13 @@ def main():
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--kernel", default="fast")
     ap.add_argument("--frames", default="1", help="frames per launch (rt_render_frames), comma list")
+    ap.add_argument("--block", type=int, default=1, help="rows dealt in blocks of this many (prt.dist.rank_rows)")
+    ap.add_argument("--streams", type=int, default=1, help="contexts on separate streams, launches alternate "
+                    "(consecutive launches overlap); the time is then wall clock per frame")
     a = ap.parse_args()
     import torch
     from prt import device, host
-    from prt.dist import cyclic_rows, padded_rows
+    from prt.dist import padded_rows, rank_rows
     s = host.Scene.named(a.scene).build_bvh(3)
     cam = host.camera(a.W, a.H)
     out = {}
@@ -36,18 +39,40 @@ def main():
         for n in [int(x) for x in a.ns.split(",")]:
             per_rank = []
             for q in range(n):
-                r = device.Renderer(0)
-                r.upload(s)
-                ro, rs, nr = cyclic_rows(a.H, q, n)
-                rgb = torch.empty((F, padded_rows(a.H, n), a.W, 3), dtype=torch.float32, device="cuda")
-                for _ in range(2):  # tuning launch + warm-up
-                    r.render_frames([cam] * F, a.W, a.H, rows=(ro, rs, nr), kernel=a.kernel, rgb=rgb)
-                    r.sync()
-                for _ in range(a.reps):
-                    r.render_frames([cam] * F, a.W, a.H, rows=(ro, rs, nr), kernel=a.kernel, rgb=rgb)
-                ts = sorted(r.kernel_times(a.reps))
-                per_rank.append(ts[len(ts) // 2] / F)
-                r.close()
+                rows = rank_rows(a.H, q, n, a.block)
+                nr = rows[2]
+                if a.streams == 1:
+                    r = device.Renderer(0)
+                    r.upload(s)
+                    rgb = torch.empty((F, padded_rows(a.H, n, a.block), a.W, 3), dtype=torch.float32, device="cuda")
+                    for _ in range(2):  # tuning launch + warm-up
+                        r.render_frames([cam] * F, a.W, a.H, rows=rows, kernel=a.kernel, rgb=rgb)
+                        r.sync()
+                    for _ in range(a.reps):
+                        r.render_frames([cam] * F, a.W, a.H, rows=rows, kernel=a.kernel, rgb=rgb)
+                    ts = sorted(r.kernel_times(a.reps))
+                    per_rank.append(ts[len(ts) // 2] / F)
+                    r.close()
+                    continue
+                import time
+                strs = [torch.cuda.Stream() for _ in range(a.streams)]
+                rs_ = [device.Renderer(0, stream=st.cuda_stream) for st in strs]
+                bufs = [torch.empty((F, padded_rows(a.H, n, a.block), a.W, 3), dtype=torch.float32, device="cuda")
+                        for _ in strs]
+                for r, b in zip(rs_, bufs):
+                    r.upload(s)
+                    for _ in range(2):
+                        r.render_frames([cam] * F, a.W, a.H, rows=rows, kernel=a.kernel, rgb=b)
+                        r.sync()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for j in range(a.reps * a.streams):
+                    k = j % a.streams
+                    rs_[k].render_frames([cam] * F, a.W, a.H, rows=rows, kernel=a.kernel, rgb=bufs[k])
+                torch.cuda.synchronize()
+                per_rank.append((time.perf_counter() - t0) * 1e3 / (a.reps * a.streams * F))
+                for r in rs_:
+                    r.close()
             mx = max(per_rank)
             if base is None:
                 base = mx * n
