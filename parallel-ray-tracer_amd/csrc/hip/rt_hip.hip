@@ -430,7 +430,8 @@ int env_cap(const char* name, int def) {
 }
 
 template <int MAXB>
-void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int device, hipStream_t s, int cap) {
+void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int device, hipStream_t s, int cap,
+            int occ = 3) {
     if (kernel == RT_KERNEL_STRICT) {
         if (count) rtd::k_tiles<MAXB, true, true><<<grid_tiles, rtd::BLOCK, 0, s>>>(A);
         else rtd::k_tiles<MAXB, true, false><<<grid_tiles, rtd::BLOCK, 0, s>>>(A);
@@ -439,13 +440,18 @@ void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int de
         auto k = count ? rtd::k_persist<MAXB, false, true> : rtd::k_persist<MAXB, false, false>;
         if (const char* e = std::getenv("PRT_PERSIST_REG"); e && std::atoi(e) == 0)  // A/B: stack-only walk
             k = count ? rtd::k_persist<MAXB, false, true, false> : rtd::k_persist<MAXB, false, false, false>;
-        if (const char* e = std::getenv("PRT_PERSIST_OCC"); e && std::atoi(e) == 4)  // A/B: <= 128 VGPRs
+        if (const char* e = std::getenv("PRT_PERSIST_OCC"); e && std::atoi(e) == 4) occ = 4;  // A/B knob
+        if (occ == 4)  // <= 128 VGPRs: 4 waves per SIMD (spills; wins in batches, where the chip stays full)
             k = count ? rtd::k_persist<MAXB, false, true, true, 4> : rtd::k_persist<MAXB, false, false, true, 4>;
         if (A.tile_trace)  // diagnostics (PRT_TILE_TRACE)
             k = count ? rtd::k_persist<MAXB, false, true, true, 3, true> : rtd::k_persist<MAXB, false, false, true, 3, true>;
-        if (A.n_frames > 1)  // frame batch: cameras from A.cams
+        if (A.n_frames > 1) {  // frame batch: cameras from A.cams
             k = count ? rtd::k_persist<MAXB, false, true, true, 3, false, true>
                       : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
+            if (occ == 4)
+                k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true>
+                          : rtd::k_persist<MAXB, false, false, true, 4, false, true>;
+        }
         if (const char* e = std::getenv("PRT_REGEN"); e && std::atoi(e) == 1 && A.spp <= 1) {  // A/B: path regeneration
             auto kr = count ? rtd::k_regen<MAXB, true> : rtd::k_regen<MAXB, false>;
             int blocks = std::max(1, std::min(resident(kr, device), (A.n_tiles + 3) / 4));
@@ -809,7 +815,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     // (scene, frame shape) runs each candidate TUNE_REPS times (all into the same outputs), the next
     // frame reads the timings and keeps the fastest. PRT_TUNE=0 (or forcing a configuration through
     // PRT_SPLIT / PRT_PERSIST_CAP / PRT_SPLIT_OCC_A / PRT_COOP) disables it; PRT_TUNE_LOG=1 prints the timings.
-    enum { M_PERSIST = 0, M_SPLIT = 1, M_FAN = 3 };  // 2, 4, 8: k_coop with G = mode
+    enum { M_PERSIST = 0, M_SPLIT = 1, M_FAN = 3, M_PERSIST4 = 6 };  // 2, 4, 8: k_coop with G = mode
     const char* split_env = std::getenv("PRT_SPLIT");
     const char* cap_env = std::getenv("PRT_PERSIST_CAP");
     const char* occa_env = std::getenv("PRT_SPLIT_OCC_A");
@@ -822,6 +828,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     const int fan_r = ctx->n_lights <= 1 ? 2 : ctx->n_lights <= 3 ? 4 : 8;  // lanes per pixel: 1 + lights
     const char* fan_env = std::getenv("PRT_FAN");
     int mode = split_ok && (split_env ? std::atoi(split_env) == 1 : ctx->n_lights >= 3) ? M_SPLIT : M_PERSIST;
+    if (mode == M_PERSIST && n_frames > 1) mode = M_PERSIST4;  // untuned batches: 4 waves/SIMD (-8 %)
     if (coop_ok && coop_env && (std::atoi(coop_env) == 2 || std::atoi(coop_env) == 4 || std::atoi(coop_env) == 8))
         mode = std::atoi(coop_env);
     if (fan_ok && fan_env && std::atoi(fan_env) == 1) mode = M_FAN;
@@ -860,9 +867,9 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             T.choice = -1;
             T.pending = false;
             // (coop8 is 3x slower than coop4 everywhere measured: a knob, PRT_COOP=8, not a candidate)
-            const int md[6] = {M_PERSIST, M_PERSIST, M_SPLIT, 4, 2, M_FAN};
-            const int cp[6] = {8, 2, 2, 8, 8, 8};
-            for (int i = 0; i < 6 && T.n < rt_ctx::TUNE_MAX; i++)
+            const int md[7] = {M_PERSIST, M_PERSIST4, M_PERSIST, M_SPLIT, 4, 2, M_FAN};
+            const int cp[7] = {8, 8, 2, 2, 8, 8, 8};
+            for (int i = 0; i < 7 && T.n < rt_ctx::TUNE_MAX; i++)
                 if ((md[i] != M_SPLIT || (split_ok && ctx->n_lights >= 1)) && (md[i] != M_FAN || fan_ok) &&
                     (md[i] < 2 || md[i] == M_FAN || coop_ok)) {
                     T.mode[T.n] = md[i];
@@ -890,8 +897,10 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 for (int c = 0; c < T.n; c++) {
                     const int m = T.mode[c];
                     std::fprintf(stderr, " %s%s/%d %.3f ms",
-                                 m == M_PERSIST ? "persist" : m == M_SPLIT ? "split" : m == M_FAN ? "fan" : "coop",
-                                 m == M_FAN ? std::to_string(fan_r).c_str() : m >= 2 ? std::to_string(m).c_str() : "",
+                                 m == M_PERSIST ? "persist" : m == M_PERSIST4 ? "persist-occ4" : m == M_SPLIT ? "split"
+                                 : m == M_FAN ? "fan" : "coop",
+                                 m == M_FAN ? std::to_string(fan_r).c_str()
+                                 : (m >= 2 && m != M_PERSIST4) ? std::to_string(m).c_str() : "",
                                  T.cap[c], T.ms[c]);
                 }
                 std::fprintf(stderr, " -> %d\n", best);
@@ -911,7 +920,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             HIPC(hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT, ctx->stream));
         HIPC(hipMemsetAsync(ctx->d_work, 0, 1024, ctx->stream));
         if (md == M_SPLIT) return f->bounces <= 4 ? launch_split<4>(ctx, A, count, cp) : launch_split<8>(ctx, A, count, cp);
-        if (md >= 2) {
+        if (md >= 2 && md != M_PERSIST4) {
             rtd::KArgs B = A;
             const int gr = md == M_FAN ? fan_r : md;  // lanes per pixel
             const int tw = gr == 2 ? 8 : 4, th = gr == 8 ? 2 : 4;  // rtd::GTile<gr>
@@ -927,8 +936,9 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                                    : launch_coop<8>(B, md, count, ctx->device, ctx->stream, cp);
         }
         if (kernel == RT_KERNEL_WAVEFRONT) return launch_wf(ctx, A, count);
-        if (f->bounces <= 4) launch<4>(A, kernel, count, grid, ctx->device, ctx->stream, cp);
-        else launch<8>(A, kernel, count, grid, ctx->device, ctx->stream, cp);
+        const int occ = md == M_PERSIST4 ? 4 : 3;
+        if (f->bounces <= 4) launch<4>(A, kernel, count, grid, ctx->device, ctx->stream, cp, occ);
+        else launch<8>(A, kernel, count, grid, ctx->device, ctx->stream, cp, occ);
         return RT_OK;
     };
     if (trial) {
