@@ -630,21 +630,18 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
     const float4 sh0 = s.shade[2 * orig], sh1 = s.shade[2 * orig + 1];
     const int m = __float_as_int(sh0.w);
     const v3 n = nd ? xyz(sh1) : xyz(sh0);
-    const v3 ks = xyz(s.mats[3 * m]), kd = xyz(s.mats[3 * m + 1]), kr = xyz(s.mats[3 * m + 2]);
-    v3 col = mk(0.0f + kd.x * amb.x, 0.0f + kd.y * amb.y, 0.0f + kd.z * amb.z);  // :144-146
+    const v3 kd0 = xyz(s.mats[3 * m + 1]);
+    v3 col = mk(0.0f + kd0.x * amb.x, 0.0f + kd0.y * amb.y, 0.0f + kd0.z * amb.z);  // :144-146
     const v3 v = mul(d, -1.0f);                                                      // :147
     for (int j = 0; j < s.n_lights; ++j) {                                           // :149-160
-        const v3 Lp = xyz(s.lights[2 * j]), kl = xyz(s.lights[2 * j + 1]);
+        // the shadow ray first (light_v, raytracer.c:62-99), then the Lambert/Blinn terms: the same
+        // values (pure functions of ip, n, d, the material and the light), fewer of them live across the walk
+        const v3 Lp = xyz(s.lights[2 * j]);
         v3 l = sub(Lp, ip);
         float mg = mag(l);
         l = dvs(l, mg);
         mg *= mg;
-        const float ndl = dot(n, l);
-        const v3 h = normalize(add(l, v));  // lambert_blinn, raytracer.c:21-33
-        const float coeff = fmaxf(0.0f, dot(n, h));
-        const v3 cr = mk(kd.x * fmaxf(0.0f, ndl) + ks.x * coeff, kd.y * fmaxf(0.0f, ndl) + ks.y * coeff,
-                         kd.z * fmaxf(0.0f, ndl) + ks.z * coeff);
-        const v3 tmp = sub(ip, Lp), tmp2 = sub(Lp, ip);  // light_v, raytracer.c:62-99
+        const v3 tmp = sub(ip, Lp), tmp2 = sub(Lp, ip);
         const float ld2 = dot(tmp, tmp);
         int V;
         if (dot(tmp2, n) < 0) {
@@ -655,6 +652,13 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
             if constexpr (G > 1) V = visible_g<G, COUNT>(s, ip, l, ld2, stk, c, q) ? 1 : 0;
             else V = visible<STRICT, COUNT, REG>(s, ip, l, ld2, stk, c) ? 1 : 0;
         }
+        const v3 kl = xyz(s.lights[2 * j + 1]);
+        const v3 ks = xyz(s.mats[3 * m]), kd = xyz(s.mats[3 * m + 1]);
+        const float ndl = dot(n, l);
+        const v3 h = normalize(add(l, v));  // lambert_blinn, raytracer.c:21-33
+        const float coeff = fmaxf(0.0f, dot(n, h));
+        const v3 cr = mk(kd.x * fmaxf(0.0f, ndl) + ks.x * coeff, kd.y * fmaxf(0.0f, ndl) + ks.y * coeff,
+                         kd.z * fmaxf(0.0f, ndl) + ks.z * coeff);
         const float fV = (float)V;
         col.x = col.x + fV * kl.x * cr.x / mg;
         col.y = col.y + fV * kl.y * cr.y / mg;
@@ -665,6 +669,7 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
     const v3 r = normalize(add(dd, ns));
     set3<MAXB>(cols, it, col);
     seti<MAXB>(mats, it, m);
+    const v3 kr = xyz(s.mats[3 * m + 2]);
     if (!(mag(kr) > 0.0f)) {  // raytracer.c:168
         L = it + 1;
         tail = false;
