@@ -88,13 +88,20 @@ struct KArgs {
     int n_frames;
     int row_block;  // rows in blocks of row_block (>= 1): image row of compact row k = image_row()
     unsigned long long frame_px;
+    // PB kernels: each level's colour + material of a lane's path, [wave][level][lane] (rt_kernels.hpp)
+    float4* pathbuf;
+    // DYN kernels: the wide walk's stack in dynamic LDS (wcap 2-int entries per lane = the scene's wide
+    // depth), the binary walks' stacks in global memory (gstack: [block][STACK][256] ints)
+    int* gstack;
+    int wcap;
+    int dyn_pad;
 };
 
 // Kernel arguments are laid out by the host compiler and read by the device compiler: both passes must
 // agree on every offset (an LDS pointer, 32-bit on gfx950 but 64-bit on the host, once shifted every
 // later field and hung a kernel). Pinned sizes catch such drift at compile time in whichever pass
 // disagrees; never put address-space-qualified pointers in these structs.
-static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 144 && sizeof(KArgs) == 368,
+static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 144 && sizeof(KArgs) == 392,
               "kernel-argument layout changed: update the pinned sizes only after checking both passes agree");
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

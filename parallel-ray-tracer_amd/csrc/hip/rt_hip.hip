@@ -75,6 +75,8 @@ struct rt_ctx {
     bool batch_sum = false;  // set while rt_render_frames launches frames one by one (counters add up)
     // frame batches: the cameras on the device (d_cams) and the host copy they were uploaded from
     float* d_cams = nullptr;
+    float4* d_pathbuf = nullptr;  // PB kernels: per-wave path levels (rtd::KArgs::pathbuf)
+    int* d_gstack = nullptr;      // DYN kernels: the binary walks' stacks (rtd::KArgs::gstack)
     float* h_cams = nullptr;  // pinned
     int cams_cap = 0, cams_n = 0;
     // output stage (rt_gather, rt_download_bmp)
@@ -414,9 +416,9 @@ namespace {
 
 // resident workgroups per CU of a persistent kernel (occupancy API, capped at 8)
 template <class K>
-int resident(K kernel, int device, int cap = 8) {
+int resident(K kernel, int device, int cap = 8, size_t dyn_lds = 0) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, rtd::BLOCK, 0) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, rtd::BLOCK, dyn_lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -441,16 +443,28 @@ void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int de
         if (const char* e = std::getenv("PRT_PERSIST_REG"); e && std::atoi(e) == 0)  // A/B: stack-only walk
             k = count ? rtd::k_persist<MAXB, false, true, false> : rtd::k_persist<MAXB, false, false, false>;
         if (const char* e = std::getenv("PRT_PERSIST_OCC"); e && std::atoi(e) == 4) occ = 4;  // A/B knob
-        if (occ == 4)  // <= 128 VGPRs: 4 waves per SIMD (spills; wins in batches, where the chip stays full)
-            k = count ? rtd::k_persist<MAXB, false, true, true, 4> : rtd::k_persist<MAXB, false, false, true, 4>;
+        if (occ == 4)  // <= 128 VGPRs: 4 waves per SIMD (path buffer + spills; wins where the chip stays full)
+            k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, false, true>
+                      : rtd::k_persist<MAXB, false, false, true, 4, false, false, true>;
         if (A.tile_trace)  // diagnostics (PRT_TILE_TRACE)
             k = count ? rtd::k_persist<MAXB, false, true, true, 3, true> : rtd::k_persist<MAXB, false, false, true, 3, true>;
+        size_t dyn = 0;
         if (A.n_frames > 1) {  // frame batch: cameras from A.cams
             k = count ? rtd::k_persist<MAXB, false, true, true, 3, false, true>
                       : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
             if (occ == 4)
-                k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true>
-                          : rtd::k_persist<MAXB, false, false, true, 4, false, true>;
+                k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, true>
+                          : rtd::k_persist<MAXB, false, false, true, 4, false, true, true>;
+            if (const char* e = std::getenv("PRT_PERSIST_OCC"); e && A.gstack && A.wcap > 0) {  // DYN A/B knob
+                const int o = std::atoi(e);
+                if (o == 5) k = count ? rtd::k_persist<MAXB, false, true, true, 5, false, true, true, true>
+                                      : rtd::k_persist<MAXB, false, false, true, 5, false, true, true, true>;
+                if (o == 6) k = count ? rtd::k_persist<MAXB, false, true, true, 6, false, true, true, true>
+                                      : rtd::k_persist<MAXB, false, false, true, 6, false, true, true, true>;
+                if (o == 8) k = count ? rtd::k_persist<MAXB, false, true, true, 8, false, true, true, true>
+                                      : rtd::k_persist<MAXB, false, false, true, 8, false, true, true, true>;
+                if (o == 5 || o == 6 || o == 8) dyn = sizeof(int) * 2 * (size_t)A.wcap * rtd::BLOCK;
+            }
         }
         if (const char* e = std::getenv("PRT_REGEN"); e && std::atoi(e) == 1 && A.spp <= 1) {  // A/B: path regeneration
             auto kr = count ? rtd::k_regen<MAXB, true> : rtd::k_regen<MAXB, false>;
@@ -458,8 +472,8 @@ void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int de
             kr<<<blocks, rtd::BLOCK, 0, s>>>(A);
             return;
         }
-        int blocks = std::max(1, std::min(resident(k, device, cap), (A.n_tiles + 3) / 4));
-        k<<<blocks, rtd::BLOCK, 0, s>>>(A);
+        int blocks = std::max(1, std::min(resident(k, device, cap, dyn), (A.n_tiles + 3) / 4));
+        k<<<blocks, rtd::BLOCK, dyn, s>>>(A);
     } else {
         const char* ev = std::getenv("PRT_WAVE_VARIANT");  // "4": the 128-VGPR build (A/B knob)
         const int variant = ev ? std::atoi(ev) : 0;
@@ -729,6 +743,17 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     }
     A.n_frames = n_frames;
     A.frame_px = pixels;
+    if (kernel == RT_KERNEL_FAST && !ctx->d_pathbuf) {  // path buffer of the PB kernels: every resident wave
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
+        const size_t waves = (size_t)cus * 8 * (rtd::BLOCK / 64);  // <= 8 workgroups per CU (resident() cap)
+        HIPC(hipMalloc((void**)&ctx->d_pathbuf, sizeof(float4) * waves * 8 * 64));  // MAXB <= 8 levels
+        // DYN kernels' binary-walk stacks: STACK ints per lane of every resident workgroup (<= 8 per CU)
+        HIPC(hipMalloc((void**)&ctx->d_gstack, sizeof(int) * (size_t)cus * 8 * rtd::STACK * rtd::BLOCK));
+    }
+    A.pathbuf = ctx->d_pathbuf;
+    A.gstack = ctx->d_gstack;
+    A.wcap = ctx->wide_n > 0 ? std::max(1, ctx->wide_depth) : 0;
     if (n_frames > 1) {  // the batch's cameras, uploaded when they change (pinned staging, stream-ordered)
         const size_t nf = 12 * (size_t)n_frames;
         static_assert(sizeof(rt_camera) == 48, "rt_camera = 4 x rt_vec3");
@@ -1224,6 +1249,8 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     if (ctx->wf_mem) (void)hipFree(ctx->wf_mem);
     if (ctx->d_rgb_own) (void)hipFree(ctx->d_rgb_own);
     if (ctx->d_cams) (void)hipFree(ctx->d_cams);
+    if (ctx->d_pathbuf) (void)hipFree(ctx->d_pathbuf);
+    if (ctx->d_gstack) (void)hipFree(ctx->d_gstack);
     if (ctx->h_cams) (void)hipHostFree(ctx->h_cams);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     for (auto& o : ctx->orders) (void)hipFree(o.second);

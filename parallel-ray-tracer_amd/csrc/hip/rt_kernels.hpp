@@ -355,7 +355,7 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
 // the walks issue its loads BEFORE those tests and their latency overlaps them. -1: walk done; -2: stack
 // overflow (reported, never silent).
 __device__ __forceinline__ int wide_next(unsigned nh, int cb, unsigned imask, unsigned oct, int& sp,
-                                         int* __restrict__ stk) {
+                                         int* __restrict__ stk, int wcap = WSTACK) {
     if (!nh) {
         if (sp == 0) return -1;
         --sp;
@@ -367,7 +367,7 @@ __device__ __forceinline__ int wide_next(unsigned nh, int cb, unsigned imask, un
     const unsigned slot = (unsigned)__builtin_ctz(nh) ^ oct;
     nh &= nh - 1u;
     if (nh) {
-        if (sp >= WSTACK) return -2;
+        if (sp >= wcap) return -2;
         stk[(2 * sp) * BLOCK] = cb;
         stk[(2 * sp + 1) * BLOCK] = (int)((imask << 8) | nh);
         ++sp;
@@ -379,7 +379,7 @@ __device__ __forceinline__ int wide_next(unsigned nh, int cb, unsigned imask, un
 // pays where registers allow (the split kernels), not in k_persist (spills at its 168-VGPR cap).
 template <bool COUNT, bool PIPE = false>
 __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& best, int& hp, int& nd, bool& tie,
-                                             int* __restrict__ stk, Ctr& c) {
+                                             int* __restrict__ stk, Ctr& c, int wcap = WSTACK) {
     const RayPre p = ray_pre(o, d);
     const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
     int sp = 0;
@@ -394,7 +394,7 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
             c.nb += 10;
             c.ws += first_active_lane();
         }
-        const int next = wide_next(nh, cb, imask, oct, sp, stk);
+        const int next = wide_next(nh, cb, imask, oct, sp, stk, wcap);
         if (next >= 0) N = wload(W, next);
         if (!PIPE) {
             while (th) {
@@ -453,7 +453,8 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
 }
 
 template <bool COUNT, bool PIPE = false>
-__device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c) {
+__device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c,
+                                             int wcap = WSTACK) {
     const RayPre p = ray_pre(o, d);
     const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
     float best = FMAX;
@@ -470,7 +471,7 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
             c.nb += 10;
             c.ws += first_active_lane();
         }
-        const int next = wide_next(nh, cb, imask, oct, sp, stk);
+        const int next = wide_next(nh, cb, imask, oct, sp, stk, wcap);
         if (next >= 0) N = wload(W, next);
         if (!PIPE) {
             while (th) {
@@ -524,19 +525,21 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
 }
 
 // Closest hit with the kernel's policy; returns the ORIGINAL triangle index (-1 = miss).
+// sstk (nullable): the binary walks' stack when the wide walk's `stk` holds only wcap entries (DYN kernels)
 template <bool STRICT, bool COUNT, bool REG = true, bool PIPE = false>
 __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best, int& nd, int* __restrict__ stk,
-                                       Ctr& c) {
+                                       Ctr& c, int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
+    int* __restrict__ bstk = sstk ? sstk : stk;
     int hp = -1;
     bool tie = false;
     best = FMAX;
     nd = 0;
     if (!STRICT && !degenerate(d)) {
         if (s.wide.nodes) {
-            closest_wide<COUNT, PIPE>(s.wide, o, d, best, hp, nd, tie, stk, c);
+            closest_wide<COUNT, PIPE>(s.wide, o, d, best, hp, nd, tie, stk, c, wcap);
             if (!tie) return hp >= 0 ? s.wide.tri_orig[hp] : -1;
         } else {
-            closest_walk<false, COUNT, REG>(s.acc, o, d, best, hp, nd, tie, stk, c);
+            closest_walk<false, COUNT, REG>(s.acc, o, d, best, hp, nd, tie, bstk, c);
             if (!tie) return hp >= 0 ? s.acc.tri_orig[hp] : -1;
         }
         c.fb++;
@@ -546,18 +549,20 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
     } else if (!STRICT) {
         c.fb++;
     }
-    closest_walk<true, COUNT, REG>(s.ref, o, d, best, hp, nd, tie, stk, c);
+    closest_walk<true, COUNT, REG>(s.ref, o, d, best, hp, nd, tie, bstk, c);
     return hp >= 0 ? s.ref.tri_orig[hp] : -1;
 }
 
 template <bool STRICT, bool COUNT, bool REG = true, bool PIPE = false>
-__device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c) {
+__device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c,
+                                        int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
+    int* __restrict__ bstk = sstk ? sstk : stk;
     if (!STRICT && !degenerate(d)) {
-        if (s.wide.nodes) return visible_wide<COUNT, PIPE>(s.wide, o, d, ld2, stk, c);
-        return visible_walk<false, COUNT, REG>(s.acc, o, d, ld2, stk, c);
+        if (s.wide.nodes) return visible_wide<COUNT, PIPE>(s.wide, o, d, ld2, stk, c, wcap);
+        return visible_walk<false, COUNT, REG>(s.acc, o, d, ld2, bstk, c);
     }
     if (!STRICT) c.fb++;
-    return visible_walk<true, COUNT, REG>(s.ref, o, d, ld2, stk, c);
+    return visible_walk<true, COUNT, REG>(s.ref, o, d, ld2, bstk, c);
 }
 
 // group-cooperative walks (rt_coop.hpp): G lanes per ray
@@ -601,11 +606,15 @@ __device__ __forceinline__ void seti(int (&a)[MAXB], int i, int v) {
 // colour and material; returns true when the path ends (L = levels kept, tail = the reference's
 // raytrace(.., BOUNCES) returned {0,0,0}), otherwise leaves the reflection ray in (o, d).
 // G > 1: the traversals are group-cooperative (rt_coop.hpp), q = the lane's place in its group.
-template <int MAXB, bool STRICT, bool COUNT, bool REG, int G = 1>
+// PB: the level's colour and material go to this lane's path buffer slot pb[it * 64] instead of the
+// register arrays (cold values: written once per level, read once by the fold), which frees 4 * MAXB
+// registers across the walks for the kernels with the tightest register budget.
+template <int MAXB, bool STRICT, bool COUNT, bool REG, int G = 1, bool PB = false>
 __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, v3& o, v3& d, v3 (&cols)[MAXB],
                                           int (&mats)[MAXB], int& L, bool& tail, int& hit0, float& t0,
                                           int* __restrict__ bh, int bh_pix, int* __restrict__ stk, Ctr& c,
-                                          unsigned q = 0) {
+                                          unsigned q = 0, float4* __restrict__ pb = nullptr,
+                                          int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
     const v3 amb = mk(s.amb_x, s.amb_y, s.amb_z);
     float best;
     int nd;
@@ -613,14 +622,15 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
     else c.refl++;
     int orig;
     if constexpr (G > 1) orig = closest_g<G, COUNT>(s, o, d, best, nd, stk, c, q);
-    else orig = closest<STRICT, COUNT, REG>(s, o, d, best, nd, stk, c);
+    else orig = closest<STRICT, COUNT, REG>(s, o, d, best, nd, stk, c, sstk, wcap);
     if (it == 0) {
         hit0 = orig;
         t0 = best;
     }
     if (bh && bh_pix >= 0) bh[(size_t)bh_pix * bounces + it] = orig;  // per-level dump (uniform base, nullable)
     if (orig < 0) {  // raytracer.c:132-135
-        set3<MAXB>(cols, it, mk(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z));
+        if constexpr (PB) pb[it * 64] = make_float4(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z, __int_as_float(0));
+        else set3<MAXB>(cols, it, mk(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z));
         L = it + 1;
         tail = false;
         return true;
@@ -650,7 +660,7 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
         } else {
             c.shad++;
             if constexpr (G > 1) V = visible_g<G, COUNT>(s, ip, l, ld2, stk, c, q) ? 1 : 0;
-            else V = visible<STRICT, COUNT, REG>(s, ip, l, ld2, stk, c) ? 1 : 0;
+            else V = visible<STRICT, COUNT, REG>(s, ip, l, ld2, stk, c, sstk, wcap) ? 1 : 0;
         }
         const v3 kl = xyz(s.lights[2 * j + 1]);
         const v3 ks = xyz(s.mats[3 * m]), kd = xyz(s.mats[3 * m + 1]);
@@ -667,8 +677,12 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
     const v3 dd = mul(v, -1.0f);  // raytracer.c:163-166
     const v3 ns = mul(n, 2.0f * __builtin_fabsf(dot(dd, n)));
     const v3 r = normalize(add(dd, ns));
-    set3<MAXB>(cols, it, col);
-    seti<MAXB>(mats, it, m);
+    if constexpr (PB) {
+        pb[it * 64] = make_float4(col.x, col.y, col.z, __int_as_float(m));
+    } else {
+        set3<MAXB>(cols, it, col);
+        seti<MAXB>(mats, it, m);
+    }
     const v3 kr = xyz(s.mats[3 * m + 2]);
     if (!(mag(kr) > 0.0f)) {  // raytracer.c:168
         L = it + 1;
@@ -710,24 +724,53 @@ __device__ __forceinline__ v3 fold_path(const DScene& s, const v3 (&cols)[MAXB],
     return acc;
 }
 
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1>
+// fold_path over a path buffer (PB kernels): the same sums in the same order
+template <int MAXB>
+__device__ __forceinline__ v3 fold_pb(const DScene& s, const float4* __restrict__ pb, int L, bool tail) {
+    v3 acc = mk(0.0f, 0.0f, 0.0f);
+    bool have = false;
+#pragma unroll
+    for (int i = MAXB - 1; i >= 0; --i) {
+        if (i < L) {
+            const float4 e = pb[i * 64];
+            const v3 ci = mk(e.x, e.y, e.z);
+            const v3 kr = xyz(s.mats[3 * __float_as_int(e.w) + 2]);
+            if (!have) {
+                acc = ci;
+                if (tail) acc = mk(acc.x + kr.x * 0.0f, acc.y + kr.y * 0.0f, acc.z + kr.z * 0.0f);
+                have = true;
+            } else {
+                acc = mk(ci.x + kr.x * acc.x, ci.y + kr.y * acc.y, ci.z + kr.z * acc.z);
+            }
+        }
+    }
+    return acc;
+}
+
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, bool PB = false>
 __device__ v3 trace_path(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0, int bh_pix,
-                         unsigned q = 0) {
+                         unsigned q = 0, int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
     v3 cols[MAXB];
     int mats[MAXB];
+    float4* pb = nullptr;
+    if constexpr (PB) {  // [wave][level][lane] (persistent grids: a wave's slot is its own for the launch)
+        pb = A.pathbuf + ((size_t)(blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6)) * MAXB) * 64 + (threadIdx.x & 63);
+    } else {
 #pragma unroll
-    for (int k = 0; k < MAXB; k++) {
-        cols[k] = mk(0.0f, 0.0f, 0.0f);
-        mats[k] = 0;
+        for (int k = 0; k < MAXB; k++) {
+            cols[k] = mk(0.0f, 0.0f, 0.0f);
+            mats[k] = 0;
+        }
     }
     int L = 0;
     bool tail = false;
     for (int it = 0; it < A.bounces; ++it) {
-        if (path_step<MAXB, STRICT, COUNT, REG, G>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0,
-                                                   A.bounce_hit, bh_pix, stk, c, q))
+        if (path_step<MAXB, STRICT, COUNT, REG, G, PB>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0,
+                                                       A.bounce_hit, bh_pix, stk, c, q, pb, sstk, wcap))
             break;
     }
-    return fold_path<MAXB>(A.s, cols, mats, L, tail);
+    if constexpr (PB) return fold_pb<MAXB>(A.s, pb, L, tail);
+    else return fold_path<MAXB>(A.s, cols, mats, L, tail);
 }
 
 __device__ __forceinline__ v3 clamp01(v3 c) {  // vec_constrain(col, 0, 1), vec.c:47-54
@@ -771,9 +814,10 @@ __device__ __forceinline__ v3 primary_dir(const KArgs& A, float fx, float fy) {
 }
 
 // Pixel (x, compact row k) of frame `frame` of the launch (outputs at frame * frame_px).
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1>
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, bool PB = false>
 __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int frame, int x, int k,
-                                             int* __restrict__ stk, Ctr& c, unsigned q = 0) {
+                                             int* __restrict__ stk, Ctr& c, unsigned q = 0,
+                                             int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
     const int y = image_row(A, k);
     const size_t o = (size_t)frame * A.frame_px + (size_t)k * A.W + x;
     int hit0 = -1;
@@ -782,8 +826,8 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
     if (A.bounce_hit)
         for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
     if (A.spp <= 1) {
-        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G>(A, C.pos, primary_dir(C, (float)x, (float)y), stk, c,
-                                                              hit0, t0, (int)o, q));
+        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB>(A, C.pos, primary_dir(C, (float)x, (float)y), stk,
+                                                                  c, hit0, t0, (int)o, q, sstk, wcap));
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples
         const int g = A.spp_grid;
         v3 acc = mk(0.0f, 0.0f, 0.0f);
@@ -793,8 +837,8 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
                 const float fy = (float)y + ((float)sj + 0.5f) / (float)g;
                 int h;
                 float tt;
-                const v3 cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G>(
-                    A, C.pos, primary_dir(C, fx, fy), stk, c, h, tt, si == 0 && sj == 0 ? (int)o : -1, q));
+                const v3 cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB>(
+                    A, C.pos, primary_dir(C, fx, fy), stk, c, h, tt, si == 0 && sj == 0 ? (int)o : -1, q, sstk, wcap));
                 acc = add(acc, cs);
                 if (si == 0 && sj == 0) {
                     hit0 = h;
@@ -835,11 +879,25 @@ __global__ __launch_bounds__(BLOCK) void k_tiles(KArgs A) {
 // OCC: waves per SIMD the register allocation must allow: 3 caps VGPRs at 168 (512 / 3 in 8-register
 // granules; one register more halves nothing but drops a whole wave per SIMD), 4 at 128 (the LDS
 // stack allows 4 workgroups per CU).
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int OCC = 3, bool TRACE = false, bool BATCH = false>
+// DYN: the wide walk's stack in dynamic LDS sized to the scene's wide depth (2 * wcap ints per lane instead
+// of STACK = 34) and the binary walks' (rare strict fallbacks) in global memory, so that more workgroups
+// fit a CU's LDS: the kernels with OCC > 4 waves per SIMD.
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int OCC = 3, bool TRACE = false, bool BATCH = false,
+          bool PB = false, bool DYN = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(OCC > 0 ? OCC : 1)))
 void k_persist(KArgs A) {
-    __shared__ int lds[STACK * BLOCK];
-    int* stk = lds + threadIdx.x;
+    int* stk;
+    int* sstk = nullptr;
+    int wcap = WSTACK;
+    if constexpr (DYN) {
+        extern __shared__ int lds_dyn[];
+        stk = lds_dyn + threadIdx.x;
+        sstk = A.gstack + (size_t)blockIdx.x * STACK * BLOCK + threadIdx.x;
+        wcap = A.wcap;
+    } else {
+        __shared__ int lds[STACK * BLOCK];
+        stk = lds + threadIdx.x;
+    }
     const int lane = threadIdx.x & 63;
     Ctr c = {};
     // frame batches: dealt item t = (tile t / n_frames of the dealing order, frame t % n_frames), so the
@@ -858,7 +916,8 @@ void k_persist(KArgs A) {
         unsigned long long t0 = 0;
         const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
         if (TRACE) t0 = __builtin_amdgcn_s_memrealtime();
-        if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT, REG>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c);
+        if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT, REG, 1, PB>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, 0u,
+                                                                              sstk, wcap);
         if (TRACE) {  // {begin, end, wave | fallbacks << 32, wave steps | lane node visits << 32} (COUNT)
             const unsigned fb = wave_sum(c.fb - fb0), ws = wave_sum(c.ws - ws0), nv = wave_sum(c.chi + c.shi - nd0);
             if (lane == 0) {

@@ -15,8 +15,8 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# production instantiation of the bench: k_persist, no counters, no trace, frame batch (BATCH = true)
-PROD = "k_persist<4, false, false, true, 3, false, true>"
+# production instantiation of the bench: k_persist, no counters, 4 waves/SIMD, no trace, frame batch
+PROD = "k_persist<4, false, false, true, 4, false, true>"
 
 
 def rows(path):
