@@ -166,8 +166,12 @@ int main(int argc, char** argv) {
         std::vector<int> status(G, 0);
         for (int g = 0; g < G; g++)
             th.emplace_back([&, g] {
-                int nr = (a.H - g + G - 1) / G;
-                rt_frame f{a.W, a.H, g, G, nr, a.bounces, a.spp, kern};
+                // 8-row blocks dealt cyclically to the GPUs (prt/dist.py::rank_rows): a GPU's 8x8 tiles stay
+                // 8x8 image tiles; one GPU renders the frame as single rows
+                const int B = G > 1 ? 8 : 1, nb = (a.H + B - 1) / B;
+                int nr = 0;
+                for (int j = g; j < nb; j += G) nr += std::min(B, a.H - j * B);
+                rt_frame f{a.W, a.H, g * B, G * B, nr, a.bounces, a.spp, kern, B};
                 int s = rt_render(ctx[g], &cam, &f, nullptr);
                 if (s == RT_OK) s = rt_sync(ctx[g], nullptr);
                 status[g] = s;
