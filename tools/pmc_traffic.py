@@ -16,7 +16,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # production instantiation of the bench: k_persist, no counters, 4 waves/SIMD, no trace, frame batch
-PROD = "k_persist<4, false, false, true, 4, false, true>"
+PROD = "k_persist<4, false, false, true, 4, false, true, true, false>"
 
 
 def rows(path):
