@@ -95,13 +95,16 @@ struct KArgs {
     int* gstack;
     int wcap;
     int dyn_pad;
+    // XCD-aware dealing (nullable): tile_order holds 8 spatial regions' tiles, region r at
+    // [region_off[r], region_off[r + 1]); workgroup b (on XCD b % 8) drains region b % 8 first
+    const int* region_off;
 };
 
 // Kernel arguments are laid out by the host compiler and read by the device compiler: both passes must
 // agree on every offset (an LDS pointer, 32-bit on gfx950 but 64-bit on the host, once shifted every
 // later field and hung a kernel). Pinned sizes catch such drift at compile time in whichever pass
 // disagrees; never put address-space-qualified pointers in these structs.
-static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 144 && sizeof(KArgs) == 392,
+static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 144 && sizeof(KArgs) == 400,
               "kernel-argument layout changed: update the pinned sizes only after checking both passes agree");
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

@@ -879,6 +879,39 @@ __global__ __launch_bounds__(BLOCK) void k_tiles(KArgs A) {
 // OCC: waves per SIMD the register allocation must allow: 3 caps VGPRs at 168 (512 / 3 in 8-register
 // granules; one register more halves nothing but drops a whole wave per SIMD), 4 at 128 (the LDS
 // stack allows 4 workgroups per CU).
+// The next (frame, tile) item of a persistent wave. Default: one counter over items t = (tile t / F of
+// the dealing order, frame t % F). XCD-aware (A.region_off): the workgroups on XCD x (blockIdx % 8, the
+// dispatcher's round-robin) drain spatial region x first — its rays touch a smaller part of the scene,
+// which that XCD's own 4 MB L2 then holds — and then the other regions in turn (load balance); `reg` is
+// the wave's current region offset from its home region.
+__device__ __forceinline__ bool next_item(const KArgs& A, int lane, int& reg, int& frame, unsigned& tile) {
+    const unsigned F = (unsigned)A.n_frames;
+    if (!A.region_off) {
+        unsigned t = 0;
+        if (lane == 0) t = atomicAdd(A.work, 1u);
+        t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+        if (t >= (unsigned)A.n_tiles * F) return false;
+        frame = (int)(t % F);
+        tile = t / F;
+        if (A.tile_order) tile = (unsigned)A.tile_order[tile];
+        return true;
+    }
+    while (reg < 8) {
+        const int r = (int)((blockIdx.x + (unsigned)reg) & 7u);
+        const unsigned base = (unsigned)A.region_off[r], n = (unsigned)A.region_off[r + 1] - base;
+        unsigned t = 0;
+        if (lane == 0) t = atomicAdd(A.work + 16 * r, 1u);
+        t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+        if (t < n * F) {
+            frame = (int)(t % F);
+            tile = (unsigned)A.tile_order[base + t / F];
+            return true;
+        }
+        ++reg;
+    }
+    return false;
+}
+
 // DYN: the wide walk's stack in dynamic LDS sized to the scene's wide depth (2 * wcap ints per lane instead
 // of STACK = 34) and the binary walks' (rare strict fallbacks) in global memory, so that more workgroups
 // fit a CU's LDS: the kernels with OCC > 4 waves per SIMD.
@@ -902,15 +935,11 @@ void k_persist(KArgs A) {
     Ctr c = {};
     // frame batches: dealt item t = (tile t / n_frames of the dealing order, frame t % n_frames), so the
     // expensive (central) tiles of every frame of the batch start first
-    const unsigned items = (unsigned)A.n_tiles * (unsigned)A.n_frames;
+    int reg = 0;
     for (;;) {
-        unsigned t = 0;
-        if (lane == 0) t = atomicAdd(A.work, 1u);
-        t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
-        if (t >= items) break;
-        const int frame = (int)(t % (unsigned)A.n_frames);
-        unsigned tile = t / (unsigned)A.n_frames;
-        if (A.tile_order) tile = (unsigned)A.tile_order[tile];
+        int frame;
+        unsigned tile;
+        if (!next_item(A, lane, reg, frame, tile)) break;
         const int tx = (int)(tile % (unsigned)A.tiles_x), ty = (int)(tile / (unsigned)A.tiles_x);
         const int x = tx * 8 + (lane & 7), k = ty * 8 + (lane >> 3);
         unsigned long long t0 = 0;

@@ -445,3 +445,32 @@ def test_frame_batch_equals_single_frames(dev, name, kernel):
         if rows is None and name != "car_boxed":
             ref = np.load(os.path.join(GOLD, f"{name}_96x54_strict.npz"))
             assert same_bits(rgb[0].cpu().numpy(), ref["rgb"])
+
+
+@pytest.mark.parametrize("xcd", ["0", "1", "2"])
+def test_xcd_aware_dealing_renders_the_same_frames(dev, xcd, monkeypatch):
+    """k_persist's tile dealing (rt_hip.hip, rtd::next_item): one global counter (PRT_XCD=0), 8 row
+    bands, 8 column bands, and the default 4 x 2 blocks drained first by their own XCD — the same bits
+    for a frame, a row subset and a frame batch, and the same ray counts"""
+    import torch
+    s = host.Scene.named("dragon").build_bvh(3)
+    W, H = 200, 120
+    outs = {}
+    for v in ("3", xcd):
+        monkeypatch.setenv("PRT_XCD", v)
+        monkeypatch.setenv("PRT_TUNE", "0")
+        a = render(dev, s, W, H, "fast", counters=True)
+        b = render(dev, s, W, H, "fast", rows=(8, 24, 40, 8))
+        r = dev.Renderer(0)
+        r.upload(s)
+        rgb = torch.empty((3, H, W, 3), dtype=torch.float32, device="cuda")
+        r.render_frames([host.camera(W, H)] * 3, W, H, kernel="fast", rgb=rgb)
+        r.sync()
+        outs[v] = (a, b, rgb.cpu().numpy())
+        r.close()
+    (a0, b0, f0), (a1, b1, f1) = outs["3"], outs[xcd]
+    assert same_bits(a0["rgb"], a1["rgb"]) and same_bits(b0["rgb"], b1["rgb"]) and same_bits(f0, f1)
+    np.testing.assert_array_equal(a0["hit"], a1["hit"])
+    assert a0["stats"]["rays"] == a1["stats"]["rays"]
+    for i in range(3):
+        assert same_bits(f1[i], a0["rgb"])
