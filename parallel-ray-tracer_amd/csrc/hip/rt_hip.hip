@@ -830,28 +830,46 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     if (int rc = order_for(A.tiles_x, A.n_tiles / A.tiles_x, A.tile_order)) return rc;
     // XCD-aware dealing of k_persist: the centre-out order split into 8 spatial regions, region r drained
     // first by the workgroups on XCD r (rtd::next_item), so each XCD's L2 holds the part of the scene its
-    // region's rays touch. PRT_XCD: 3 = 4 x 2 blocks of tiles (default), 1 = 8 bands of tile rows,
-    // 2 = 8 bands of tile columns, 0 = one global counter. Same-box, 16-frame batches, ms per frame:
+    // region's rays touch. PRT_XCD: 3 = 4 x 2 blocks of tiles, 1 = 8 bands of tile rows, 2 = 8 bands of
+    // tile columns, 0 = one global counter. Same-box, ms per frame: 16-frame batches of the full frame,
     // dragon 1.060 / 0.938 (blocks) / 0.980 (rows) / 0.942 (columns), sportscar 0.599 / 0.504, car_boxed
-    // 1.067 / 1.041. Device layout: 9 region offsets, then the concatenated regions' tiles.
+    // 1.067 / 1.041; a single frame 1.862 / 1.871 (blocks) / 1.732 (rows); an 8-GPU rank's rows, batched,
+    // 0.220 / 0.208 (blocks) / 0.202 (rows). Default: blocks for batches of the full frame, row bands
+    // otherwise. Device layout: 9 region offsets, then the concatenated regions' tiles.
     const char* xcd_env = std::getenv("PRT_XCD");
     const int* region_off = nullptr;
     const int* region_order = nullptr;
-    const int xcd_mode = xcd_env ? std::atoi(xcd_env) : 3;
+    const bool full_frame = f->row_offset == 0 && f->n_rows == f->height;
+    const int xcd_mode = xcd_env ? std::atoi(xcd_env) : (n_frames > 1 && full_frame ? 3 : 1);
     if (centre_out && xcd_mode >= 1 && xcd_mode <= 3) {
         const int tx = A.tiles_x, ty = A.n_tiles / A.tiles_x;
-        const long long key = ((long long)xcd_mode << 60) | ((long long)tx << 32) | (unsigned)ty;
+        // order inside a region: centre-out (default) or Z-order (PRT_XCD_ORDER=z: consecutive tiles are
+        // neighbours; A/B: batches dragon -2 %, sportscar +2 %, car_boxed +1 %, a single frame +5 %)
+        const char* zo = std::getenv("PRT_XCD_ORDER");
+        const bool zorder = zo && zo[0] == 'z';
+        const long long key = ((long long)(xcd_mode + (zorder ? 4 : 0)) << 58) | ((long long)tx << 32) | (unsigned)ty;
         auto it = ctx->orders.find(key);
         if (it == ctx->orders.end()) {
             const int n = tx * ty;
             std::vector<int> ord(n);
             for (int i = 0; i < n; i++) ord[i] = i;
             const float cx = 0.5f * tx, cy = 0.5f * ty;
-            std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
-                const float ax = a % tx + 0.5f - cx, ay = a / tx + 0.5f - cy;
-                const float bx = b % tx + 0.5f - cx, by = b / tx + 0.5f - cy;
-                return ax * ax + ay * ay < bx * bx + by * by;
-            });
+            auto morton = [](unsigned x, unsigned y) {
+                unsigned long long m = 0;
+                for (int i = 0; i < 16; i++)
+                    m |= (unsigned long long)((x >> i) & 1u) << (2 * i) | (unsigned long long)((y >> i) & 1u) << (2 * i + 1);
+                return m;
+            };
+            if (zorder)
+                std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+                    return morton(a % tx, a / tx) < morton(b % tx, b / tx);
+                });
+            else
+                std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+                    const float ax = a % tx + 0.5f - cx, ay = a / tx + 0.5f - cy;
+                    const float bx = b % tx + 0.5f - cx, by = b / tx + 0.5f - cy;
+                    return ax * ax + ay * ay < bx * bx + by * by;
+                });
             std::vector<int> dev(9 + n);
             int at = 9;
             for (int r = 0; r < 8; r++) {
