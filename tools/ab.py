@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--world", type=int, default=1, help="render rank --rank's cyclic rows of a --world split")
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--batch", type=int, default=1, help="frames per launch (rt_render_frames); times are per frame")
+    ap.add_argument("--orbit", type=float, default=0.0,
+                    help="batch frames from a camera path: frame i's camera moved by i * ORBIT along x "
+                         "(0: the reference's fixed camera)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
@@ -32,6 +35,12 @@ def main():
     r = device.Renderer(0)
     r.upload(s)
     cam = host.camera(a.W, a.H)
+    cams = []
+    for i in range(a.batch):
+        c = host.camera(a.W, a.H)
+        for v in (c.pos, c.ul):
+            v.x += i * a.orbit
+        cams.append(c)
     from prt.dist import cyclic_rows
     rows = cyclic_rows(a.H, a.rank, a.world)
     rgb = torch.empty((a.batch, rows[2], a.W, 3), dtype=torch.float32, device="cuda")
@@ -60,7 +69,7 @@ def main():
             if a.reupload:
                 r.upload(s)
             for _ in range(a.frames):
-                r.render_frames([cam] * a.batch, a.W, a.H, rows=rows, kernel=kern, rgb=rgb)
+                r.render_frames(cams, a.W, a.H, rows=rows, kernel=kern, rgb=rgb)
             ts = [t / a.batch for t in r.kernel_times(a.frames)]
             if rnd > 0:  # round 0 = warm-up
                 res[v] += ts
