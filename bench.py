@@ -2,9 +2,11 @@
 """bench.py — BASELINE.json metric: Mrays/s (primary + secondary) on dragon at 1920x1080, 1/2/4/8 MI355X.
 
 One step = one full frame of the hot path (ray generation, BVH traversal, ray-triangle intersection,
-shading with shadow rays, 4 reflection bounces, clamp) for the workload below, with the scene resident
-in HBM before timing starts; for N > 1 the frame's rows are dealt cyclically over the ranks (row y on
-rank y % N: cost-balanced) and gathered to rank 0 over RCCL inside the timed region.
+shading with shadow rays, 4 reflection bounces, clamp, and the BMP writer's BGRA8 quantisation written by
+the kernel itself: --output bgra8) for the workload below, with the scene resident in HBM
+before timing starts; for N > 1 the frame's rows are dealt over the ranks in 8-row blocks (block j on
+rank j % N: cost-balanced) and gathered to rank 0 over RCCL inside the timed region (4 bytes
+per pixel; --output rgb writes and gathers the 12-byte f32 pixels instead).
 
 Frames in flight: the K timed frames (the reference's ITERATIONS loop of one camera, main.c) are traced
 in batches of F frames per launch (rt_render_frames: one persistent launch whose tile dealing interleaves
@@ -37,15 +39,15 @@ METRIC = "Mrays/sec (primary+secondary) on dragon at 1920×1080, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def alg_bytes(st, pixels, n_lights):
+def alg_bytes(st, pixels, n_lights, px_bytes=12):
     """Algorithmic bytes of one launch from the kernel's traversal counters:
     BVH records read (node_bytes, counted on the device: 80 B per wide-node visit of the fast walk,
     64 B per child-pair node + 8 B per leaf record of the strict fallback walk), 48 B per triangle
     test (v0, e1, e2, n), per closest hit 4 + 32 + 48 B (tri_orig, normals + material id, material),
-    32 B per light per hit, 12 B per pixel written (rgb)."""
+    32 B per light per hit, px_bytes per pixel written (4: the BGRA8 pixel, 12: f32 rgb)."""
     tri = st["ch_tri"] + st["sh_tri"]
     nodes = st.get("node_bytes") or (64 * (st["ch_inner"] + st["sh_inner"]) + 8 * (st["ch_leaf"] + st["sh_leaf"]))
-    return nodes + 48 * tri + (84 + 32 * n_lights) * st["hits"] + 12 * pixels
+    return nodes + 48 * tri + (84 + 32 * n_lights) * st["hits"] + px_bytes * pixels
 
 
 def cpu_baseline(scene_files, W, H, gpu_rays_for_rows, args):
@@ -113,6 +115,9 @@ def main():
                     "(0: 1 at N = 1, 2 at N > 1)")
     ap.add_argument("--row-block", type=int, default=0,
                     help="N > 1: rows dealt to ranks in blocks of this many (0: 8, so 8x8 tiles stay 8x8 in the image)")
+    ap.add_argument("--output", choices=("bgra8", "rgb"), default="bgra8",
+                    help="what each frame's kernel writes and the gather moves: bgra8 = the BMP writer's quantised "
+                         "pixel (rt_outputs.bgra, 4 B), rgb = the f32 vec_t pixel (12 B)")
     ap.add_argument("--scene", default="dragon")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -175,8 +180,13 @@ def main():
     # (prt/dist.py, tested with gloo in tests/test_multi.py); two ping-pong blocks so a batch's gather
     # overlaps the next batch's render
     B = args.row_block if args.row_block > 0 else (8 if world > 1 else 1)
-    fg = FrameGather(H, W, 3, rank, world, dist, like=torch.empty(0, dtype=torch.float32, device="cuda"),
+    bgra = args.output == "bgra8"
+    fg = FrameGather(H, W, 1 if bgra else 3, rank, world, dist,
+                     like=torch.empty(0, dtype=torch.int32 if bgra else torch.float32, device="cuda"),
                      frames=F, buffers=2, block=B)
+
+    def out(blk):  # the kernel's output argument for a gather block
+        return {"bgra": blk} if bgra else {"rgb": blk}
     my_rows = fg.rows()
     n_r = my_rows[2]
     launch_no = [0]
@@ -189,7 +199,7 @@ def main():
             if fg.pending(b):
                 fg.finish(b)
             rends[c].render_frames([cam] * nf, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
-                                   kernel=args.kernel, rgb=fg.blocks[b])
+                                   kernel=args.kernel, **out(fg.blocks[b]))
             fg.start(b)
 
     def drain():
@@ -247,17 +257,17 @@ def main():
     rc = device.Renderer(local, counters=True, stream=stream)
     rc.upload(scene, accel=args.accel)
     rc.render_frames([cam] * F, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
-                     kernel=args.kernel, rgb=fg.blocks[0])
+                     kernel=args.kernel, **out(fg.blocks[0]))
     stc = rc.stats()
     rc.close()
-    bytes_launch = alg_bytes(stc, F * W * n_r, len(scene.lights))
+    bytes_launch = alg_bytes(stc, F * W * n_r, len(scene.lights), 4 if bgra else 12)
     k_avg_ms = sum(kfull) / len(kfull)
     # single-frame latency of this rank's rows (one launch, one frame; its own tuning launch first)
     rl = device.Renderer(local, stream=stream)
     rl.upload(scene, accel=args.accel)
     for _ in range(3):
         rl.render(cam, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp, kernel=args.kernel,
-                  rgb=fg.blocks[0])
+                  **out(fg.blocks[0][0] if F > 1 else fg.blocks[0]))
     lat_ms = sorted(rl.kernel_times(2))[0]
     rl.close()
     lat = torch.tensor([lat_ms], dtype=torch.float64, device="cuda")
@@ -269,7 +279,7 @@ def main():
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
-                key = f"{args.scene}_{W}x{H}_{args.kernel}_{args.bvh}"
+                key = f"{args.scene}_{W}x{H}_{args.kernel}_{args.bvh}" + ("_bgra8" if bgra else "")
                 if key in tj:
                     traffic = tj[key]["hbm_bytes_per_launch"]
             except Exception:
@@ -291,10 +301,11 @@ def main():
                      "(.MISSING_LARGE_BLOBS); prt/scenes.py generates a Cornell room + 98,304-tri knot with the "
                      "real dragon .mtl and lights.obj" if is_standin(args.scene) else "reference asset"),
             "config": {"workload": f"{args.scene} {W}x{H}, {args.spp} spp, {args.bounces} bounces, one fused "
-                                   f"traversal+intersect+shade persistent launch per batch of {F} frames",
+                                   f"traversal+intersect+shade persistent launch per batch of {F} frames, "
+                                   f"output {args.output}",
                        "scene": args.scene, "triangles": scene.n_triangles, "lights": len(scene.lights),
                        "width": W, "height": H, "bvh": args.bvh, "accel": args.accel, "kernel": args.kernel,
-                       "rays_per_frame": rays_frame, "parallelism": f"{B}-row blocks cyclic x{world} + RCCL gather"
+                       "rays_per_frame": rays_frame, "output": args.output, "parallelism": f"{B}-row blocks cyclic x{world} + RCCL gather"
                        if world > 1 else "single GPU", "frames_per_launch": F},
             "frame_latency_ms": lat.item(),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

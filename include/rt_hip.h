@@ -87,12 +87,18 @@ typedef struct rt_frame {
  * (main.c:39); NULL -> a buffer owned by the context (read it with rt_download).
  * hit: [n_rows][width] int32 primary closest-hit triangle index (-1 = miss); t: its distance.
  * bounce_hit: [n_rows][width][bounces] int32 closest-hit triangle index of every recursion level
- * (raytrace(.., iter), raytracer.c:101-135): -1 = miss, -2 = level not reached (first sample when spp > 1). */
+ * (raytrace(.., iter), raytracer.c:101-135): -1 = miss, -2 = level not reached (first sample when spp > 1).
+ * bgra: [n_rows][width] uint32, the pixel quantised as the BMP writer does (vec_to_bgra,
+ * cpu/src/bmp_writer.c:88-95: B | G << 8 | R << 16 | 255 << 24, little-endian bytes B,G,R,A) in the frame's
+ * top-down row order (the BMP file stores rows bottom-up); written by the kernel itself, so a frame bound for
+ * a gather or a file moves 4 bytes per pixel instead of 12. With bgra set and rgb NULL no f32 pixels are
+ * written (rt_download of rgb, rt_gather and rt_download_bmp then refuse the frame). */
 typedef struct rt_outputs {
     float* rgb;
     int* hit;
     float* t;
     int* bounce_hit;
+    unsigned int* bgra;
 } rt_outputs;
 
 typedef struct rt_stats {

@@ -98,13 +98,15 @@ struct KArgs {
     // XCD-aware dealing (nullable): tile_order holds 8 spatial regions' tiles, region r at
     // [region_off[r], region_off[r + 1]); workgroup b (on XCD b % 8) drains region b % 8 first
     const int* region_off;
+    // nullable: the frame quantised on the fly (rt_outputs.bgra), one packed B|G<<8|R<<16|255<<24 per pixel
+    unsigned* bgra;
 };
 
 // Kernel arguments are laid out by the host compiler and read by the device compiler: both passes must
 // agree on every offset (an LDS pointer, 32-bit on gfx950 but 64-bit on the host, once shifted every
 // later field and hung a kernel). Pinned sizes catch such drift at compile time in whichever pass
 // disagrees; never put address-space-qualified pointers in these structs.
-static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 144 && sizeof(KArgs) == 400,
+static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 144 && sizeof(KArgs) == 408,
               "kernel-argument layout changed: update the pinned sizes only after checking both passes agree");
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)
@@ -123,6 +125,22 @@ __device__ __forceinline__ v3 cross(v3 a, v3 b) {
 }
 __device__ __forceinline__ v3 normalize(v3 a) { return dvs(a, mag(a)); }
 __device__ __forceinline__ v3 xyz(float4 f) { return mk(f.x, f.y, f.z); }
+
+// One finished pixel (o = frame-relative output index) to the frame's outputs: the f32 vec_t pixel
+// (main.c:39) and/or its BMP quantisation vec_to_bgra (cpu/src/bmp_writer.c:88-95; as k_bgra, but in
+// the frame's top-down row order), so that a quantised frame never takes a second pass over HBM.
+__device__ __forceinline__ void store_px(float* __restrict__ rgb, unsigned* __restrict__ bgra, size_t o, v3 col) {
+    if (rgb) {
+        rgb[3 * o] = col.x;
+        rgb[3 * o + 1] = col.y;
+        rgb[3 * o + 2] = col.z;
+    }
+    if (bgra) {
+        const unsigned r = (unsigned char)(col.x * 255.0f), g = (unsigned char)(col.y * 255.0f),
+                       b = (unsigned char)(col.z * 255.0f);
+        bgra[o] = b | (g << 8) | (r << 16) | (255u << 24);
+    }
+}
 
 // ---------------------------------------------------------------- ray-triangle (raytracer.c:35-59)
 // v0, e1, e2, n precomputed on the host with the reference's own roundings.

@@ -302,11 +302,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                 const float nn = (float)(g * g);
                 col = mk(acc.x / nn, acc.y / nn, acc.z / nn);
             }
-            if (A.rgb) {
-                A.rgb[3 * po] = col.x;
-                A.rgb[3 * po + 1] = col.y;
-                A.rgb[3 * po + 2] = col.z;
-            }
+            store_px(A.rgb, A.bgra, po, col);
             if (A.hit) A.hit[po] = hit0;
             if (A.t) A.t[po] = t0;
         }

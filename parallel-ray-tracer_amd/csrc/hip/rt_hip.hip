@@ -673,7 +673,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     const size_t pixels = (size_t)f->width * f->n_rows;  // per frame
     const size_t all_px = pixels * (size_t)n_frames;
     float* rgb = out ? out->rgb : nullptr;
-    if (!rgb) {
+    unsigned* bgra = out ? out->bgra : nullptr;
+    if (!rgb && !bgra) {  // a quantised-only frame writes no f32 pixels at all
         if (ctx->rgb_cap < all_px) {
             if (ctx->d_rgb_own) HIPC(hipFree(ctx->d_rgb_own));
             ctx->d_rgb_own = nullptr;
@@ -713,6 +714,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     A.spp = f->spp;
     A.spp_grid = g;
     A.rgb = rgb;
+    A.bgra = bgra;
     A.hit = out ? out->hit : nullptr;
     A.t = out ? out->t : nullptr;
     A.bounce_hit = out ? out->bounce_hit : nullptr;
@@ -724,12 +726,15 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     // the wavefront pipeline and k_wave render 1 spp; spp > 1 goes to the per-pixel path kernel
     if ((kernel == RT_KERNEL_WAVEFRONT || kernel == RT_KERNEL_WAVE) && (f->spp > 1 || (out && out->bounce_hit)))
         kernel = RT_KERNEL_FAST;  // spp > 1 and per-level hit dumps: the fused path kernels
-    if ((f->bounces > rtd::WF_MAXB || ctx->n_lights > 32 || rb > 1) && kernel == RT_KERNEL_WAVEFRONT)
-        kernel = RT_KERNEL_FAST;  // (the wavefront pipeline's primary-ray stage takes single rows only)
+    if ((f->bounces > rtd::WF_MAXB || ctx->n_lights > 32 || rb > 1 || bgra) && kernel == RT_KERNEL_WAVEFRONT)
+        kernel = RT_KERNEL_FAST;  // (the wavefront pipeline's primary-ray stage takes single rows only and
+                                  // its fold stage writes f32 pixels only)
     if (n_frames > 1 && kernel != RT_KERNEL_FAST) {  // one launch per frame, outputs at frame offsets
         for (int i = 0; i < n_frames; i++) {
-            rt_outputs o{rgb + 3 * pixels * i, A.hit ? A.hit + pixels * i : nullptr, A.t ? A.t + pixels * i : nullptr,
-                         A.bounce_hit ? A.bounce_hit + pixels * f->bounces * i : nullptr};
+            rt_outputs o{rgb ? rgb + 3 * pixels * i : nullptr, A.hit ? A.hit + pixels * i : nullptr,
+                         A.t ? A.t + pixels * i : nullptr,
+                         A.bounce_hit ? A.bounce_hit + pixels * f->bounces * i : nullptr,
+                         bgra ? bgra + pixels * i : nullptr};
             ctx->batch_sum = i > 0;
             const int rc = render_batch(ctx, cams + i, 1, f, &o);
             ctx->batch_sum = false;
@@ -1124,6 +1129,10 @@ extern "C" int rt_download(rt_ctx* ctx, float* h_rgb, int* h_hit) {
     }
     HIPC(hipSetDevice(ctx->device));
     HIPC(hipStreamSynchronize(ctx->stream));
+    if (h_rgb && !ctx->last_rgb) {
+        ctx->err = "rt_download: last frame was rendered to a bgra output only";
+        return RT_E_STATE;
+    }
     if (h_rgb)
         HIPC(hipMemcpy(h_rgb, ctx->last_rgb, sizeof(float) * 3 * ctx->last_pixels, hipMemcpyDeviceToHost));
     if (h_hit) {
@@ -1190,6 +1199,7 @@ extern "C" int rt_gather(rt_ctx* const* ctxs, int n, int root) {
         if (!c || !c->rendered) return arg_err(ctx, "rt_gather: a context has not rendered");
         if (c->last_W != W || c->last_H != H) return arg_err(ctx, "rt_gather: frame sizes differ");
         if (c->last_frames != 1) return arg_err(ctx, "rt_gather: the last render was a frame batch");
+        if (!c->last_rgb) return arg_err(ctx, "rt_gather: the last render had a bgra output only");
         for (int k = 0; k < c->last_rows; k++) {
             const long long y = c->last_off + (long long)(k / c->last_block) * c->last_stride + k % c->last_block;
             if (y < 0 || y >= H || cover[y]) return arg_err(ctx, "rt_gather: row sets do not partition the frame");
@@ -1258,6 +1268,7 @@ extern "C" int rt_download_bmp(rt_ctx* ctx, unsigned char* h_bmp, size_t cap) {
         return RT_E_STATE;
     }
     if (ctx->last_frames != 1) return arg_err(ctx, "rt_download_bmp: the last render was a frame batch");
+    if (!ctx->last_rgb) return arg_err(ctx, "rt_download_bmp: the last render had a bgra output only");
     const int W = ctx->last_W, H = ctx->last_H;
     if (ctx->last_off != 0 || ctx->last_stride != ctx->last_block || ctx->last_rows != H) {
         ctx->err = "rt_download_bmp: the last frame is not a full frame (gather it first)";

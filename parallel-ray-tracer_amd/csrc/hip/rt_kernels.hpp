@@ -850,11 +850,7 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
     }
     c.pix++;
     if (q != 0) return;  // a group's pixel is written once
-    if (A.rgb) {
-        A.rgb[3 * o] = col.x;
-        A.rgb[3 * o + 1] = col.y;
-        A.rgb[3 * o + 2] = col.z;
-    }
+    store_px(A.rgb, A.bgra, o, col);
     if (A.hit) A.hit[o] = hit0;
     if (A.t) A.t[o] = t0;
 }
@@ -1030,11 +1026,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                 const v3 col = clamp01(fold_path<MAXB>(A.s, cols, mats, L, tail));
                 const size_t w = (size_t)pk * A.W + px;
                 c.pix++;
-                if (A.rgb) {
-                    A.rgb[3 * w] = col.x;
-                    A.rgb[3 * w + 1] = col.y;
-                    A.rgb[3 * w + 2] = col.z;
-                }
+                store_px(A.rgb, A.bgra, w, col);
                 if (A.hit) A.hit[w] = hit0;
                 if (A.t) A.t[w] = t0;
                 px = -1;

@@ -204,12 +204,7 @@ __global__ __launch_bounds__(256) void k_split_resolve(KArgs A) {
         seti<MAXB>(mats, it, m);
     }
     const v3 col = clamp01(fold_path<MAXB>(s, cols, mats, L, (info & SPLIT_TAIL) != 0));
-    if (A.rgb) {
-        const size_t px = (size_t)k * A.W + x;
-        A.rgb[3 * px] = col.x;
-        A.rgb[3 * px + 1] = col.y;
-        A.rgb[3 * px + 2] = col.z;
-    }
+    store_px(A.rgb, A.bgra, (size_t)k * A.W + x, col);
 }
 
 }  // namespace rtd

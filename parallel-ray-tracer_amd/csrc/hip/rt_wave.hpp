@@ -150,11 +150,7 @@ __device__ __forceinline__ void wave_body(const KArgs& A, int* __restrict__ stk)
                             }
                         }
                     const v3 cl = clamp01(accum);
-                    if (A.rgb) {
-                        A.rgb[3 * (size_t)pix] = cl.x;
-                        A.rgb[3 * (size_t)pix + 1] = cl.y;
-                        A.rgb[3 * (size_t)pix + 2] = cl.z;
-                    }
+                    store_px(A.rgb, A.bgra, (size_t)pix, cl);
                     c.pix++;
                     ph = PH_NONE;
                     continue;
@@ -255,11 +251,7 @@ __device__ __forceinline__ void wave_body(const KArgs& A, int* __restrict__ stk)
                             }
                         }
                     const v3 cl = clamp01(accum);
-                    if (A.rgb) {
-                        A.rgb[3 * (size_t)pix] = cl.x;
-                        A.rgb[3 * (size_t)pix + 1] = cl.y;
-                        A.rgb[3 * (size_t)pix + 2] = cl.z;
-                    }
+                    store_px(A.rgb, A.bgra, (size_t)pix, cl);
                     c.pix++;
                     ph = PH_NONE;
                     continue;

@@ -23,7 +23,7 @@ class RtError(RuntimeError):
 
 class Outputs(ctypes.Structure):
     _fields_ = [("rgb", ctypes.c_void_p), ("hit", ctypes.c_void_p), ("t", ctypes.c_void_p),
-                ("bounce_hit", ctypes.c_void_p)]
+                ("bounce_hit", ctypes.c_void_p), ("bgra", ctypes.c_void_p)]
 
 
 _lib.hip()  # fail loudly at import if the HIP library is absent
@@ -99,25 +99,26 @@ class Renderer:
         return self
 
     def render(self, cam, width, height, rows=None, bounces=4, spp=1, kernel="auto", rgb=None, hit=None, t=None,
-               bounce_hit=None):
+               bounce_hit=None, bgra=None):
         """render_frame(): asynchronous. rows = (offset, stride, n[, block]) (rt_frame; prt.dist) or None for
         the full frame.
-        rgb / hit / t / bounce_hit ([n, W, bounces] int32): optional device tensors (torch) or raw pointers."""
+        rgb / hit / t / bounce_hit ([n, W, bounces] int32) / bgra ([n, W] int32: the BMP-quantised pixel in
+        top-down rows, rt_outputs.bgra): optional device tensors (torch) or raw pointers."""
         ro, rs, nr, rb = _rows(rows, height)
         f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel), rb)
-        out = Outputs(_ptr(rgb), _ptr(hit), _ptr(t), _ptr(bounce_hit))
+        out = Outputs(_ptr(rgb), _ptr(hit), _ptr(t), _ptr(bounce_hit), _ptr(bgra))
         self._chk(_L.rt_render(self._ctx, ctypes.byref(cam), ctypes.byref(f), ctypes.byref(out)), "rt_render")
         self._last = (width, nr)
         self._size = (width, height)
         self._frames = 1
 
     def render_frames(self, cams, width, height, rows=None, bounces=4, spp=1, kernel="auto", rgb=None, hit=None,
-                      t=None, bounce_hit=None):
+                      t=None, bounce_hit=None, bgra=None):
         """rt_render_frames(): a batch of len(cams) frames of one shape (one persistent launch on the fast
         kernel); outputs [n_frames, n_rows, W, ...]. Asynchronous."""
         ro, rs, nr, rb = _rows(rows, height)
         f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel), rb)
-        out = Outputs(_ptr(rgb), _ptr(hit), _ptr(t), _ptr(bounce_hit))
+        out = Outputs(_ptr(rgb), _ptr(hit), _ptr(t), _ptr(bounce_hit), _ptr(bgra))
         arr = (Camera * len(cams))(*cams)
         self._chk(_L.rt_render_frames(self._ctx, arr, len(cams), ctypes.byref(f), ctypes.byref(out)),
                   "rt_render_frames")

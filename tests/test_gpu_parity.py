@@ -474,3 +474,49 @@ def test_xcd_aware_dealing_renders_the_same_frames(dev, xcd, monkeypatch):
     assert a0["stats"]["rays"] == a1["stats"]["rays"]
     for i in range(3):
         assert same_bits(f1[i], a0["rgb"])
+
+
+def quantise(rgb):
+    """vec_to_bgra (cpu/src/bmp_writer.c:88-95) of f32 pixels -> packed uint32 B | G << 8 | R << 16 | 255 << 24"""
+    q = (np.asarray(rgb, np.float32) * np.float32(255.0)).astype(np.uint8).astype(np.uint32)
+    return q[..., 2] | (q[..., 1] << 8) | (q[..., 0] << 16) | np.uint32(255 << 24)
+
+
+@pytest.mark.parametrize("kernel", KERNELS + ["split"])
+def test_bgra_output_is_the_bmp_writers_quantisation(dev, scenes, kernel, monkeypatch):
+    """rt_outputs.bgra (the kernels quantise as they store): equal to vec_to_bgra of the same
+    frame's f32 pixels, with or without an rgb output, for a frame, a row-block subset and a frame batch;
+    the full frame's rows bottom-up are bmp_write_file's pixel bytes of the reference fixture"""
+    import torch
+    if kernel == "split":  # the fast kernel's closest/shadow/resolve pipeline
+        monkeypatch.setenv("PRT_SPLIT", "1")
+        kernel = "fast"
+    W, H = 160, 90
+    s = scenes["car_boxed"]
+    ref = np.load(os.path.join(GOLD, "car_boxed_160x90_strict.npz"))
+    for rows in (None, (8, 24, 24, 8)):
+        nr = rows[2] if rows else H
+        r = dev.Renderer(0)
+        r.upload(s)
+        rgb = torch.empty((nr, W, 3), dtype=torch.float32, device="cuda")
+        both = torch.zeros((nr, W), dtype=torch.int32, device="cuda")
+        only = torch.zeros((nr, W), dtype=torch.int32, device="cuda")
+        r.render(host.camera(W, H), W, H, rows=rows, kernel=select(kernel), rgb=rgb, bgra=both)
+        r.render(host.camera(W, H), W, H, rows=rows, kernel=select(kernel), bgra=only)
+        r.sync()
+        q = quantise(rgb.cpu().numpy())
+        np.testing.assert_array_equal(both.cpu().numpy().view(np.uint32), q)
+        np.testing.assert_array_equal(only.cpu().numpy().view(np.uint32), q)
+        with pytest.raises(dev.RtError):  # a bgra-only frame has no f32 pixels to download
+            r.download()
+        if rows is None:
+            bmp = host.bmp_encode(ref["rgb"])
+            assert only.cpu().numpy()[::-1].tobytes() == bmp[54:]
+        batch = torch.zeros((2, nr, W), dtype=torch.int32, device="cuda")
+        r.render_frames([host.camera(W, H), moved_camera(W, H, 0.25, 0.0)], W, H, rows=rows,
+                        kernel=select(kernel), bgra=batch)
+        r.sync()
+        unforce()
+        np.testing.assert_array_equal(batch[0].cpu().numpy().view(np.uint32), q)
+        assert not np.array_equal(batch[1].cpu().numpy(), batch[0].cpu().numpy())
+        r.close()

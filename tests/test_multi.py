@@ -48,7 +48,13 @@ def _worker(rank, world, port, W, H, out_path):
     dist.destroy_process_group()
 
 
-def _batch_worker(rank, world, port, W, H, out_path, block):
+def _bgra(rgb):
+    """vec_to_bgra (bmp_writer.c:88-95) packed as the kernels' rt_outputs.bgra: [..., W] -> int32 [..., W, 1]"""
+    q = (np.asarray(rgb, np.float32) * np.float32(255.0)).astype(np.uint8).astype(np.uint32)
+    return (q[..., 2] | (q[..., 1] << 8) | (q[..., 0] << 16) | np.uint32(255 << 24)).view(np.int32)[..., None]
+
+
+def _batch_worker(rank, world, port, W, H, out_path, block, fmt="rgb"):
     """two ping-pong batches of 2 frames (the bench's pattern): start(0), render batch 1 while batch 0's
     gather runs, finish(0), start(1), finish(1); the frames of both batches must be the single frame"""
     import sys
@@ -65,11 +71,14 @@ def _batch_worker(rank, world, port, W, H, out_path, block):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     o = OracleScene.load(*scene_paths("car_only"))
     o.build_bvh(3)
-    g = FrameGather(H, W, 3, rank, world, dist, torch.zeros(1), frames=2, buffers=2, block=block)
+    bgra = fmt == "bgra8"  # the bench's default: 4-byte quantised pixels, C = 1
+    g = FrameGather(H, W, 1 if bgra else 3, rank, world, dist, torch.zeros(1, dtype=torch.int32 if bgra else
+                    torch.float32), frames=2, buffers=2, block=block)
     from prt.dist import image_rows
     rows = image_rows(H, rank, world, block)
     nr = len(rows)
-    mine = torch.from_numpy(o.render(W, H, threads=2)["rgb"][rows])
+    px = o.render(W, H, threads=2)["rgb"][rows]
+    mine = torch.from_numpy(_bgra(px) if bgra else px)
     out = []
     for b in range(2):
         for f in range(2):
@@ -84,8 +93,9 @@ def _batch_worker(rank, world, port, W, H, out_path, block):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,H,block", [(2, 36, 1), (3, 37, 1), (2, 32, 8), (3, 37, 4)])
-def test_batched_pingpong_gather_equals_single_frame(tmp_path, world, H, block):
+@pytest.mark.parametrize("world,H,block,fmt", [(2, 36, 1, "rgb"), (3, 37, 1, "rgb"), (2, 32, 8, "rgb"), (3, 37, 4, "rgb"),
+                                              (2, 32, 8, "bgra8"), (3, 37, 4, "bgra8")])
+def test_batched_pingpong_gather_equals_single_frame(tmp_path, world, H, block, fmt):
     import torch.multiprocessing as mp
 
     from tests.oracle_bind import OracleScene
@@ -93,13 +103,15 @@ def test_batched_pingpong_gather_equals_single_frame(tmp_path, world, H, block):
 
     W = 64  # H % world == 0: one permuted copy; else per-rank strided copies
     out = str(tmp_path / "frames.npy")
-    mp.start_processes(_batch_worker, args=(world, _free_port(), W, H, out, block), nprocs=world, join=True,
+    mp.start_processes(_batch_worker, args=(world, _free_port(), W, H, out, block, fmt), nprocs=world, join=True,
                        start_method="spawn")
     got = np.load(out)
     o = OracleScene.load(*scene_paths("car_only"))
     o.build_bvh(3)
     ref = o.render(W, H)["rgb"]
-    assert got.shape == (2, 2, H, W, 3)
+    if fmt == "bgra8":
+        ref = _bgra(ref)
+    assert got.shape == (2, 2, H, W, 1 if fmt == "bgra8" else 3)
     for b in range(2):
         for f in range(2):
             assert np.array_equal(got[b, f].view(np.int32), ref.view(np.int32)), (b, f)

@@ -41,7 +41,7 @@ def find(d, sub):
 
 def main():
     prof, tag = sys.argv[1], sys.argv[2]
-    key = sys.argv[3] if len(sys.argv) > 3 else "dragon_1920x1080_fast_random"
+    key = sys.argv[3] if len(sys.argv) > 3 else "dragon_1920x1080_fast_random_bgra8"
     pdir = os.path.join(ROOT, "profiles")
     os.makedirs(pdir, exist_ok=True)
     # kernel trace stats
