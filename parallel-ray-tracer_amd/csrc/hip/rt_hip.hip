@@ -443,18 +443,37 @@ void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int de
         if (const char* e = std::getenv("PRT_PERSIST_REG"); e && std::atoi(e) == 0)  // A/B: stack-only walk
             k = count ? rtd::k_persist<MAXB, false, true, false> : rtd::k_persist<MAXB, false, false, false>;
         if (const char* e = std::getenv("PRT_PERSIST_OCC"); e && std::atoi(e) == 4) occ = 4;  // A/B knob
-        if (occ == 4)  // <= 128 VGPRs: 4 waves per SIMD (path buffer + spills; wins where the chip stays full)
+        // occ 4: <= 128 VGPRs, 4 waves per SIMD, each path level's colour + material in a path buffer. The
+        // buffer lives in LDS (after the wide stack sized to the scene's wide depth; DYN kernels) when 4
+        // workgroups of that still fit a CU, else in global memory (where its 2 MB per XCD competes with
+        // the scene for L2: LDS measured 1.2 % faster on dragon, 2.3 % on car_boxed; PRT_PB_LDS=0 = A/B)
+        size_t dyn = 0;
+        const size_t pbl_dyn = sizeof(int) * 2 * (size_t)A.wcap * rtd::BLOCK + sizeof(float4) * rtd::BLOCK * MAXB;
+        bool pbl = occ == 4 && A.gstack && A.wcap > 0;
+        if (const char* e = std::getenv("PRT_PB_LDS"); e && std::atoi(e) == 0) pbl = false;
+        if (pbl) {
+            int per_cu = 0;
+            auto kp = rtd::k_persist<MAXB, false, false, true, 4, false, true, 2, true>;
+            pbl = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, rtd::BLOCK, pbl_dyn) == hipSuccess &&
+                  per_cu >= 4;
+        }
+        if (occ == 4) {
             k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, false, true>
                       : rtd::k_persist<MAXB, false, false, true, 4, false, false, true>;
-        if (A.tile_trace)  // diagnostics (PRT_TILE_TRACE)
-            k = count ? rtd::k_persist<MAXB, false, true, true, 3, true> : rtd::k_persist<MAXB, false, false, true, 3, true>;
-        size_t dyn = 0;
+            if (pbl)
+                k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, false, 2, true>
+                          : rtd::k_persist<MAXB, false, false, true, 4, false, false, 2, true>;
+        }
         if (A.n_frames > 1) {  // frame batch: cameras from A.cams
             k = count ? rtd::k_persist<MAXB, false, true, true, 3, false, true>
                       : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
-            if (occ == 4)
+            if (occ == 4) {
                 k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, true>
                           : rtd::k_persist<MAXB, false, false, true, 4, false, true, true>;
+                if (pbl)
+                    k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, 2, true>
+                              : rtd::k_persist<MAXB, false, false, true, 4, false, true, 2, true>;
+            }
             if (const char* e = std::getenv("PRT_PERSIST_OCC"); e && A.gstack && A.wcap > 0) {  // DYN A/B knob
                 const int o = std::atoi(e);
                 if (o == 5) k = count ? rtd::k_persist<MAXB, false, true, true, 5, false, true, true, true>
@@ -463,8 +482,16 @@ void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int de
                                       : rtd::k_persist<MAXB, false, false, true, 6, false, true, true, true>;
                 if (o == 8) k = count ? rtd::k_persist<MAXB, false, true, true, 8, false, true, true, true>
                                       : rtd::k_persist<MAXB, false, false, true, 8, false, true, true, true>;
-                if (o == 5 || o == 6 || o == 8) dyn = sizeof(int) * 2 * (size_t)A.wcap * rtd::BLOCK;
+                if (o == 5 || o == 6 || o == 8) {
+                    dyn = sizeof(int) * 2 * (size_t)A.wcap * rtd::BLOCK;
+                    pbl = false;
+                }
             }
+        }
+        if (pbl) dyn = pbl_dyn;
+        if (A.tile_trace) {  // diagnostics (PRT_TILE_TRACE)
+            k = count ? rtd::k_persist<MAXB, false, true, true, 3, true> : rtd::k_persist<MAXB, false, false, true, 3, true>;
+            dyn = 0;
         }
         if (const char* e = std::getenv("PRT_REGEN"); e && std::atoi(e) == 1 && A.spp <= 1) {  // A/B: path regeneration
             auto kr = count ? rtd::k_regen<MAXB, true> : rtd::k_regen<MAXB, false>;

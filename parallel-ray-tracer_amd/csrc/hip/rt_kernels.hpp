@@ -747,13 +747,18 @@ __device__ __forceinline__ v3 fold_pb(const DScene& s, const float4* __restrict_
     return acc;
 }
 
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, bool PB = false>
+// PB: 0 = levels in registers, 1 = path buffer in global memory (A.pathbuf), 2 = path buffer in dynamic LDS
+// after the DYN wide stack (2 * wcap ints per lane): [wave][level][lane] float4, the L2 left to the scene
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0>
 __device__ v3 trace_path(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0, int bh_pix,
                          unsigned q = 0, int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
     v3 cols[MAXB];
     int mats[MAXB];
     float4* pb = nullptr;
-    if constexpr (PB) {  // [wave][level][lane] (persistent grids: a wave's slot is its own for the launch)
+    if constexpr (PB == 2) {
+        extern __shared__ int lds_dyn[];
+        pb = (float4*)(lds_dyn + 2 * wcap * BLOCK) + (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
+    } else if constexpr (PB) {  // [wave][level][lane] (persistent grids: a wave's slot is its own for the launch)
         pb = A.pathbuf + ((size_t)(blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6)) * MAXB) * 64 + (threadIdx.x & 63);
     } else {
 #pragma unroll
@@ -765,11 +770,11 @@ __device__ v3 trace_path(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, Ctr&
     int L = 0;
     bool tail = false;
     for (int it = 0; it < A.bounces; ++it) {
-        if (path_step<MAXB, STRICT, COUNT, REG, G, PB>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0,
+        if (path_step<MAXB, STRICT, COUNT, REG, G, PB != 0>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0,
                                                        A.bounce_hit, bh_pix, stk, c, q, pb, sstk, wcap))
             break;
     }
-    if constexpr (PB) return fold_pb<MAXB>(A.s, pb, L, tail);
+    if constexpr (PB != 0) return fold_pb<MAXB>(A.s, pb, L, tail);
     else return fold_path<MAXB>(A.s, cols, mats, L, tail);
 }
 
@@ -814,7 +819,7 @@ __device__ __forceinline__ v3 primary_dir(const KArgs& A, float fx, float fy) {
 }
 
 // Pixel (x, compact row k) of frame `frame` of the launch (outputs at frame * frame_px).
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, bool PB = false>
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0>
 __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int frame, int x, int k,
                                              int* __restrict__ stk, Ctr& c, unsigned q = 0,
                                              int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
@@ -912,9 +917,10 @@ __device__ __forceinline__ bool next_item(const KArgs& A, int lane, int& reg, in
 // of STACK = 34) and the binary walks' (rare strict fallbacks) in global memory, so that more workgroups
 // fit a CU's LDS: the kernels with OCC > 4 waves per SIMD.
 template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int OCC = 3, bool TRACE = false, bool BATCH = false,
-          bool PB = false, bool DYN = false>
+          int PB = 0, bool DYN = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(OCC > 0 ? OCC : 1)))
 void k_persist(KArgs A) {
+    static_assert(PB != 2 || DYN, "an LDS path buffer lives in the DYN kernels' dynamic LDS");
     int* stk;
     int* sstk = nullptr;
     int wcap = WSTACK;

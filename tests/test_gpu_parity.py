@@ -520,3 +520,37 @@ def test_bgra_output_is_the_bmp_writers_quantisation(dev, scenes, kernel, monkey
         np.testing.assert_array_equal(batch[0].cpu().numpy().view(np.uint32), q)
         assert not np.array_equal(batch[1].cpu().numpy(), batch[0].cpu().numpy())
         r.close()
+
+
+@pytest.mark.parametrize("name", ["dragon", "car_boxed"])
+def test_path_buffer_placements_render_the_same_frames(dev, name, monkeypatch):
+    """k_persist at 4 waves per SIMD keeps each path level in a path buffer: in LDS after the wide stack
+    (default when 4 workgroups fit) or in global memory (PRT_PB_LDS=0); both equal the 3-wave register
+    kernel bit for bit — a frame, a frame batch, 4 spp — with the same ray counts"""
+    import torch
+    s = host.Scene.named(name).build_bvh(3)
+    W, H = 200, 120
+    outs = {}
+    monkeypatch.setenv("PRT_TUNE", "0")
+    for v in ("occ3", "lds", "global"):
+        monkeypatch.delenv("PRT_PERSIST_OCC", raising=False)
+        if v != "occ3":
+            monkeypatch.setenv("PRT_PERSIST_OCC", "4")
+            monkeypatch.setenv("PRT_PB_LDS", "1" if v == "lds" else "0")
+        a = render(dev, s, W, H, "fast", counters=True)
+        b = render(dev, s, W, H, "fast", spp=4)
+        r = dev.Renderer(0)
+        r.upload(s)
+        rgb = torch.empty((3, H, W, 3), dtype=torch.float32, device="cuda")
+        r.render_frames([host.camera(W, H), moved_camera(W, H, 0.25, 0.0), host.camera(W, H)], W, H,
+                        kernel="fast", rgb=rgb)
+        r.sync()
+        outs[v] = (a, b, rgb.cpu().numpy())
+        r.close()
+    a0, b0, f0 = outs["occ3"]
+    assert same_bits(f0[0], a0["rgb"]) and same_bits(f0[2], a0["rgb"])
+    for v in ("lds", "global"):
+        a1, b1, f1 = outs[v]
+        assert same_bits(a0["rgb"], a1["rgb"]) and same_bits(b0["rgb"], b1["rgb"]) and same_bits(f0, f1), v
+        np.testing.assert_array_equal(a0["hit"], a1["hit"])
+        assert a0["stats"]["rays"] == a1["stats"]["rays"], v

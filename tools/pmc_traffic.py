@@ -15,8 +15,9 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# production instantiation of the bench: k_persist, no counters, 4 waves/SIMD, no trace, frame batch
-PROD = "k_persist<4, false, false, true, 4, false, true, true, false>"
+# production instantiation of the bench: k_persist, no counters, 4 waves/SIMD, no trace, frame batch,
+# path buffer in LDS (PB = 2) after the DYN wide stack
+PROD = "k_persist<4, false, false, true, 4, false, true, 2, true>"
 
 
 def rows(path):
