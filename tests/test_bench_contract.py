@@ -1,0 +1,72 @@
+"""bench.py's output contract on the GPU, on a small frame: one JSON line with every key the task's
+contract names, the metric string of BASELINE.json, value = rays per frame / ms per step, the
+roofline's frac = achieved / peak, a plan that covers --steps exactly (6 frames in batches of 4: 4 + 2),
+and rays per frame equal to the oracle's count for the same frame (the reference's definition:
+primary + traced reflection + traced shadow rays)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("output", ["bgra8", "rgb"])
+def test_bench_prints_the_contract_line(output):
+    W, H = 320, 180
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "6", "--warmup", "2",
+                        "--frames", "4", "--width", str(W), "--height", str(H), "--no-cpu-baseline",
+                        "--output", output], capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    d = json.loads(lines[0])
+    base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    assert d["metric"] == base["metric"]
+    for k in ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in d, k
+    assert d["unit"] == "Mrays/s" and d["n_gpus"] == 1 and d["steps"] == 6 and d["warmup"] == 2
+    assert d["higher_is_better"] is True and d["vs_baseline"] is None
+    assert "workload" in d["config"] and d["config"]["output"] == output
+    rays = d["config"]["rays_per_frame"]
+    assert d["value"] == pytest.approx(rays / d["ms_per_step"] / 1e3, rel=1e-9)
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"], rel=1e-9) and rf["achieved"] > 0
+    assert rf["frames_per_launch"] == 4
+    from tests.oracle_bind import OracleScene
+    from tests.scenes import scene_paths
+    o = OracleScene.load(*scene_paths("dragon"))
+    o.build_bvh(3)
+    c = o.render(W, H, threads=16)["counters"]
+    assert rays == c["primary"] + c["reflection"] + c["shadow"]
+
+
+def test_bench_two_ranks_on_one_gpu_count_the_whole_frame():
+    """the N > 1 flow (8-row blocks per rank, two streams, ping-pong gathers) rehearsed with 2 gloo ranks
+    on the one GPU of the test box (PRT_DIST_ONE_GPU; RCCL refuses two ranks on one device): the ranks'
+    rays add up to the whole frame's, and rank 0 prints the only line"""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, PRT_DIST_ONE_GPU="1", PRT_DIST_BACKEND="gloo")
+    args = ["--steps", "4", "--warmup", "2", "--frames", "2", "--width", "320", "--height", "180"]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2"] + args, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 4
+    one = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline"] + args,
+                         capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert one.returncode == 0, one.stderr[-3000:]
+    d1 = json.loads([l for l in one.stdout.splitlines() if l.startswith("{")][0])
+    assert d["config"]["rays_per_frame"] == d1["config"]["rays_per_frame"]
