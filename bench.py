@@ -131,6 +131,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-row-stride", type=int, default=0)
     ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--bmp", default="", help="after timing, rank 0 writes the last frame (gathered) as a BMP "
+                    "(bmp_write_file's bytes; from the device-quantised pixels with --output bgra8)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -190,20 +192,22 @@ def main():
     my_rows = fg.rows()
     n_r = my_rows[2]
     launch_no = [0]
+    latest = [0, 0]  # (block, frames) of the latest launch
 
     def launch(nf):
         b = launch_no[0] % 2
         c = launch_no[0] % n_streams
         launch_no[0] += 1
+        latest[:] = [b, nf]
         with torch.cuda.stream(streams[c]):  # block b is rendered by context c on its stream
             if fg.pending(b):
                 fg.finish(b)
             rends[c].render_frames([cam] * nf, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
-                                   kernel=args.kernel, **out(fg.blocks[b]))
+                                   kernel=args.kernel, **out(fg.target(b)))
             fg.start(b)
 
     def drain():
-        for b in range(2):
+        for b in ((latest[0] + 1) % 2, latest[0]):  # launch order: rank 0's frame ends as the latest batch
             with torch.cuda.stream(streams[b % n_streams]):
                 if fg.pending(b):
                     fg.finish(b)
@@ -245,6 +249,12 @@ def main():
     # whole-job ray count per frame (identical every frame: the render is deterministic), from the last
     # launch's counters (a batch: the sum over its frames)
     rays_local = st["rays"] // plan[-1]
+    if args.bmp and rank == 0:  # the BMP written from the root rank (untimed)
+        frames = fg.frame if world > 1 else fg.target(latest[0])
+        px = (frames if frames.dim() == 3 else frames[latest[1] - 1]).cpu().numpy()
+        data = host.bmp_from_bgra(px) if bgra else host.bmp_encode(px)
+        with open(args.bmp, "wb") as fbmp:
+            fbmp.write(data)
     el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     rays_t = torch.tensor([rays_local], dtype=torch.float64, device="cuda")
     if dist:
@@ -257,7 +267,7 @@ def main():
     rc = device.Renderer(local, counters=True, stream=stream)
     rc.upload(scene, accel=args.accel)
     rc.render_frames([cam] * F, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
-                     kernel=args.kernel, **out(fg.blocks[0]))
+                     kernel=args.kernel, **out(fg.target(0)))
     stc = rc.stats()
     rc.close()
     bytes_launch = alg_bytes(stc, F * W * n_r, len(scene.lights), 4 if bgra else 12)
@@ -267,7 +277,7 @@ def main():
     rl.upload(scene, accel=args.accel)
     for _ in range(3):
         rl.render(cam, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp, kernel=args.kernel,
-                  **out(fg.blocks[0][0] if F > 1 else fg.blocks[0]))
+                  **out(fg.target(0)[0] if F > 1 else fg.target(0)))
     lat_ms = sorted(rl.kernel_times(2))[0]
     rl.close()
     lat = torch.tensor([lat_ms], dtype=torch.float64, device="cuda")

@@ -108,6 +108,7 @@ def host():
         L.rth_camera.argtypes = [ctypes.c_int, ctypes.c_int, P(Camera)]
         L.rth_bmp_write.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
         L.rth_bmp_encode.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
+        L.rth_bmp_header.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.rth_free.argtypes = [ctypes.c_void_p]
         L.rth_free.restype = None
         _host = L

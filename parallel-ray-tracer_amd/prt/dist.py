@@ -44,8 +44,10 @@ def image_rows(H, rank, world, block=1):
 class FrameGather:
     """Gather per-rank compact row blocks [padded_rows, W, C] into the full frame on rank 0.
 
-    frames > 1: a frame batch (rt_render_frames) — blocks [frames, padded_rows, W, C] -> frames
-    [frames, H, W, C], one collective for the whole batch. buffers > 1: ping-pong blocks, so that the
+    frames > 1: a frame batch (rt_render_frames) — every rank's frames are compact ([frames, n_rows, W, C]
+    with its OWN n_rows, as rt_render_frames writes them: frame f at f * n_rows * W), at the start of a
+    block of frames * padded_rows rows (equal on every rank, as the collective needs) -> frames
+    [frames, H, W, C], one collective for the whole batch. Render into target(i), not blocks[i]. buffers > 1: ping-pong blocks, so that the
     gather of batch k (start(k % buffers), asynchronous on the collective's stream) overlaps the render of
     batch k + 1 into the other block; finish(i) makes the current stream wait for it and un-interleaves.
     World 1: the block IS the frame (no collective, no copy). On a GPU, rank 0 un-interleaves on a side
@@ -74,6 +76,19 @@ class FrameGather:
         if many and self.bk > 1 and H % (world * self.bk) != 0:  # general block layout: index copies
             self._idx = [torch.tensor(image_rows(H, q, world, self.bk), dtype=torch.long, device=like.device)
                          for q in range(world)]
+
+    def target(self, i=0):
+        """blocks[i] as this rank's render output: [frames, n_rows, W, C] compact frames (or [n_rows, W, C])"""
+        n = rank_rows(self.H, self.rank, self.world, self.bk)[2]
+        b = self.blocks[i]
+        if self.frames == 1:
+            return b[:n]
+        return b.view(-1)[:self.frames * n * self.W * self.C].view(self.frames, n, self.W, self.C)
+
+    def _part(self, P, q):
+        """rank q's compact frames inside its gathered block P[q]: [frames, n_q, W, C]"""
+        n = rank_rows(self.H, q, self.world, self.bk)[2]
+        return P[q].reshape(-1)[:P.shape[1] * n * self.W * self.C].view(P.shape[1], n, self.W, self.C)
 
     def rows(self):
         """this rank's rt_frame rows: (offset, stride, n) for single rows, (offset, stride, n, block)"""
@@ -126,13 +141,12 @@ class FrameGather:
                     P.view(self.world, F, M, B, self.W, self.C).permute(1, 2, 0, 3, 4, 5))
             else:
                 for q in range(self.world):
-                    frame.index_copy_(1, self._idx[q], P[q, :, :len(self._idx[q])])
+                    frame.index_copy_(1, self._idx[q], self._part(P, q))
         elif self.H % self.world == 0:  # one copy: frame row k * world + q <- rank q's compact row k
             frame.view(F, n, self.world, self.W, self.C).copy_(P.permute(1, 2, 0, 3, 4))
         else:
             for q in range(self.world):
-                nq = cyclic_rows(self.H, q, self.world)[2]
-                frame[:, q::self.world] = P[q, :, :nq]
+                frame[:, q::self.world] = self._part(P, q)
 
     def gather(self, i=0):
         """collective: every rank calls it after rendering into blocks[i]; the returned frame is ready on

@@ -178,6 +178,17 @@ def bmp_encode(rgb):
     return buf.tobytes()
 
 
+def bmp_from_bgra(px):
+    """bmp_write_file's bytes from pixels the kernels already quantised (rt_outputs.bgra: [H, W] or
+    [H, W, 1] packed B|G<<8|R<<16|255<<24, top-down rows): the 54-byte header (bmp_writer.c:97-120,
+    rth_bmp_header) + the rows bottom-up (bmp_writer.c:131-143). The root rank's BMP of a gathered frame."""
+    px = np.ascontiguousarray(px)
+    H, W = px.shape[:2]
+    hdr = np.zeros(54, np.uint8)
+    _check(_lib.host().rth_bmp_header(W, H, hdr.ctypes.data), "bmp_header")
+    return hdr.tobytes() + px.reshape(H, W).view(np.uint32)[::-1].astype("<u4").tobytes()
+
+
 def bmp_write_file(rgb, path):
     """bmp_write_file(pixels, width, height, filename), cpu/src/bmp_writer.c:177-211"""
     rgb = np.ascontiguousarray(rgb, dtype=np.float32)

@@ -14,12 +14,22 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def oracle_frame(W, H):
+    from tests.oracle_bind import OracleScene
+    from tests.scenes import scene_paths
+    o = OracleScene.load(*scene_paths("dragon"))
+    o.build_bvh(3)
+    return o.render(W, H, threads=16)
+
+
 @pytest.mark.parametrize("output", ["bgra8", "rgb"])
-def test_bench_prints_the_contract_line(output):
+def test_bench_prints_the_contract_line(output, tmp_path):
     W, H = 320, 180
+    bmp = tmp_path / "frame.bmp"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "6", "--warmup", "2",
                         "--frames", "4", "--width", str(W), "--height", str(H), "--no-cpu-baseline",
-                        "--output", output], capture_output=True, text=True, timeout=240, cwd=ROOT)
+                        "--output", output, "--bmp", str(bmp)], capture_output=True, text=True, timeout=240,
+                       cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]
@@ -38,18 +48,18 @@ def test_bench_prints_the_contract_line(output):
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
     assert rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"], rel=1e-9) and rf["achieved"] > 0
     assert rf["frames_per_launch"] == 4
-    from tests.oracle_bind import OracleScene
-    from tests.scenes import scene_paths
-    o = OracleScene.load(*scene_paths("dragon"))
-    o.build_bvh(3)
-    c = o.render(W, H, threads=16)["counters"]
+    ref = oracle_frame(W, H)
+    c = ref["counters"]
     assert rays == c["primary"] + c["reflection"] + c["shadow"]
+    from prt import host
+    assert bmp.read_bytes() == host.bmp_encode(ref["rgb"])  # the last timed frame, as bmp_write_file writes it
 
 
-def test_bench_two_ranks_on_one_gpu_count_the_whole_frame():
+def test_bench_two_ranks_on_one_gpu_count_the_whole_frame(tmp_path):
     """the N > 1 flow (8-row blocks per rank, two streams, ping-pong gathers) rehearsed with 2 gloo ranks
     on the one GPU of the test box (PRT_DIST_ONE_GPU; RCCL refuses two ranks on one device): the ranks'
-    rays add up to the whole frame's, and rank 0 prints the only line"""
+    rays add up to the whole frame's, rank 0 prints the only line and writes the gathered frame's BMP
+    (= the reference writer's bytes of the oracle's frame)"""
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -59,7 +69,7 @@ def test_bench_two_ranks_on_one_gpu_count_the_whole_frame():
     args = ["--steps", "4", "--warmup", "2", "--frames", "2", "--width", "320", "--height", "180"]
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-                        "--gpus", "2"] + args, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+                        "--gpus", "2", "--bmp", str(tmp_path / "g.bmp")] + args, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]
@@ -70,3 +80,5 @@ def test_bench_two_ranks_on_one_gpu_count_the_whole_frame():
     assert one.returncode == 0, one.stderr[-3000:]
     d1 = json.loads([l for l in one.stdout.splitlines() if l.startswith("{")][0])
     assert d["config"]["rays_per_frame"] == d1["config"]["rays_per_frame"]
+    from prt import host
+    assert (tmp_path / "g.bmp").read_bytes() == host.bmp_encode(oracle_frame(320, 180)["rgb"])
