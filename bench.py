@@ -118,6 +118,9 @@ def main():
     ap.add_argument("--output", choices=("bgra8", "rgb"), default="bgra8",
                     help="what each frame's kernel writes and the gather moves: bgra8 = the BMP writer's quantised "
                          "pixel (rt_outputs.bgra, 4 B), rgb = the f32 vec_t pixel (12 B)")
+    ap.add_argument("--no-rotate", action="store_true",
+                    help="N > 1: keep each rank on its own block residue in every frame (default: frame f of rank "
+                         "q renders residue (q + f) %% N, so every rank's batch costs the same)")
     ap.add_argument("--scene", default="dragon")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -185,7 +188,7 @@ def main():
     bgra = args.output == "bgra8"
     fg = FrameGather(H, W, 1 if bgra else 3, rank, world, dist,
                      like=torch.empty(0, dtype=torch.int32 if bgra else torch.float32, device="cuda"),
-                     frames=F, buffers=2, block=B)
+                     frames=F, buffers=2, block=B, rotate=not args.no_rotate)
 
     def out(blk):  # the kernel's output argument for a gather block
         return {"bgra": blk} if bgra else {"rgb": blk}
@@ -247,8 +250,9 @@ def main():
     last = rends[timed[-1][0]]
     st = last.stats()
     # whole-job ray count per frame (identical every frame: the render is deterministic), from the last
-    # launch's counters (a batch: the sum over its frames)
-    rays_local = st["rays"] // plan[-1]
+    # launch's counters (a batch: the sum over its frames), summed over the ranks before dividing by the
+    # frames (rotated rows: a rank's share differs frame by frame, the frame's total does not)
+    rays_local = st["rays"]
     if args.bmp and rank == 0:  # the BMP written from the root rank (untimed)
         frames = fg.frame if world > 1 else fg.target(latest[0])
         px = (frames if frames.dim() == 3 else frames[latest[1] - 1]).cpu().numpy()
@@ -261,7 +265,7 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(rays_t, op=dist.ReduceOp.SUM)
     elapsed = el.item()
-    rays_frame = int(rays_t.item())
+    rays_frame = int(rays_t.item()) // plan[-1]
 
     # algorithmic bytes of this rank's full-batch launch: one extra untimed launch with traversal counters
     rc = device.Renderer(local, counters=True, stream=stream)

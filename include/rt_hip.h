@@ -81,6 +81,10 @@ typedef struct rt_frame {
     int spp;     /* 1 = the reference's pixel-corner ray; s*s = s x s stratified grid, mean of clamped samples */
     int kernel;  /* RT_KERNEL_* */
     int row_block; /* 0 or 1: single rows; B > 1: rows in blocks of B (row_stride >= B) */
+    int frame_shift; /* 0: every frame of a batch renders the rows above. S > 0 (RT_KERNEL_FAST only): frame f
+                      * of rt_render_frames starts at (row_offset + f * S) % row_stride, so that ranks dealt
+                      * block-cyclic rows rotate through every block residue over a batch and their costs
+                      * even out; compact rows whose image row falls at or past height are skipped. */
 } rt_frame;
 
 /* Device output pointers (all nullable). rgb: [n_rows][width][3] f32 in [0,1] = vec_t pixels

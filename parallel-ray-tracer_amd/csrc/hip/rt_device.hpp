@@ -94,7 +94,7 @@ struct KArgs {
     // depth), the binary walks' stacks in global memory (gstack: [block][STACK][256] ints)
     int* gstack;
     int wcap;
-    int dyn_pad;
+    int frame_shift;  // rt_frame.frame_shift: frame f's rows start at (row_offset + f * frame_shift) % row_stride
     // XCD-aware dealing (nullable): tile_order holds 8 spatial regions' tiles, region r at
     // [region_off[r], region_off[r + 1]); workgroup b (on XCD b % 8) drains region b % 8 first
     const int* region_off;

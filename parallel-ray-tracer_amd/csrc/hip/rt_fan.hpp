@@ -125,11 +125,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         const Cam C = cam_of<BATCH>(A, frame);
         const int tx = (int)(tile % (unsigned)A.tiles_x), ty = (int)(tile / (unsigned)A.tiles_x);
         const int x = tx * TW + pi % TW, k = ty * TH + pi / TW;
-        const bool valid = x < A.W && k < A.n_rows;  // uniform in the group
+        const int y = image_row(A, k, frame);
+        const bool valid = x < A.W && k < A.n_rows && y < A.H;  // uniform in the group
         unsigned long long tr0 = 0;
         const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
         if (TRACE) tr0 = __builtin_amdgcn_s_memrealtime();
-        const int y = image_row(A, k);
         const size_t po = (size_t)frame * A.frame_px + (size_t)k * A.W + x;
         if (valid && role == 0 && A.bounce_hit)
             for (int i = 0; i < A.bounces; i++) A.bounce_hit[po * (size_t)A.bounces + i] = -2;

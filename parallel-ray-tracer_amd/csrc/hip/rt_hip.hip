@@ -71,6 +71,7 @@ struct rt_ctx {
     int* last_hit = nullptr;
     size_t last_pixels = 0;
     int last_W = 0, last_H = 0, last_off = 0, last_stride = 1, last_rows = 0, last_block = 1;  // the last frame's rows
+    int last_shift = 0;
     int last_frames = 1;     // frames of the last render (rt_render_frames)
     bool batch_sum = false;  // set while rt_render_frames launches frames one by one (counters add up)
     // frame batches: the cameras on the device (d_cams) and the host copy they were uploaded from
@@ -687,10 +688,16 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     if (n_frames < 1 || n_frames > 4096) return arg_err(ctx, "rt_render_frames: n_frames must be 1..4096");
     const rt_camera* cam = cams;
     const int rb = f->row_block > 1 ? f->row_block : 1;
+    const int fs = f->frame_shift;
     if (f->width <= 0 || f->height <= 0 || f->row_stride <= 0 || f->n_rows <= 0 || f->row_offset < 0 ||
-        f->row_block < 0 || (f->n_rows > rb && f->row_stride < rb) ||
-        (long long)f->row_offset + (long long)((f->n_rows - 1) / rb) * f->row_stride + (f->n_rows - 1) % rb >= f->height)
+        f->row_block < 0 || fs < 0 || (f->n_rows > rb && f->row_stride < rb) ||
+        (fs == 0 && (long long)f->row_offset + (long long)((f->n_rows - 1) / rb) * f->row_stride +
+                            (f->n_rows - 1) % rb >= f->height) ||
+        (fs > 0 && (f->row_offset >= f->row_stride || f->row_offset >= f->height ||
+                    (long long)f->n_rows > (long long)f->row_stride * f->height)))
         return arg_err(ctx, "rt_render: rows outside the frame");
+    if (fs > 0 && f->kernel != RT_KERNEL_FAST && f->kernel != RT_KERNEL_AUTO)
+        return arg_err(ctx, "rt_render: frame_shift needs RT_KERNEL_FAST");
     if (f->bounces < 1 || f->bounces > 8) return arg_err(ctx, "rt_render: bounces must be 1..8");
     int g = 1;
     while (g * g < f->spp) g++;
@@ -736,6 +743,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     A.row_offset = f->row_offset;
     A.row_stride = f->row_stride;
     A.row_block = rb;
+    A.frame_shift = fs;
     A.n_rows = f->n_rows;
     A.bounces = f->bounces;
     A.spp = f->spp;
@@ -1110,6 +1118,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     ctx->last_stride = f->row_stride;
     ctx->last_rows = f->n_rows;
     ctx->last_block = rb;
+    ctx->last_shift = fs;
     ctx->rendered = true;
     return RT_OK;
 }
@@ -1227,6 +1236,7 @@ extern "C" int rt_gather(rt_ctx* const* ctxs, int n, int root) {
         if (c->last_W != W || c->last_H != H) return arg_err(ctx, "rt_gather: frame sizes differ");
         if (c->last_frames != 1) return arg_err(ctx, "rt_gather: the last render was a frame batch");
         if (!c->last_rgb) return arg_err(ctx, "rt_gather: the last render had a bgra output only");
+        if (c->last_shift) return arg_err(ctx, "rt_gather: the last render rotated its rows (frame_shift)");
         for (int k = 0; k < c->last_rows; k++) {
             const long long y = c->last_off + (long long)(k / c->last_block) * c->last_stride + k % c->last_block;
             if (y < 0 || y >= H || cover[y]) return arg_err(ctx, "rt_gather: row sets do not partition the frame");

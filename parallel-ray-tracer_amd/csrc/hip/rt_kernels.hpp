@@ -783,8 +783,10 @@ __device__ __forceinline__ v3 clamp01(v3 c) {  // vec_constrain(col, 0, 1), vec.
 }
 
 // image row of compact output row k (rt_frame: rows in blocks of row_block, blocks row_stride apart)
-__device__ __forceinline__ int image_row(const KArgs& A, int k) {
-    return A.row_offset + (k / A.row_block) * A.row_stride + k % A.row_block;
+// (frame f of a batch with frame_shift: rows start at (row_offset + f * frame_shift) % row_stride)
+__device__ __forceinline__ int image_row(const KArgs& A, int k, int frame = 0) {
+    const int off = A.frame_shift ? (A.row_offset + frame * A.frame_shift) % A.row_stride : A.row_offset;
+    return off + (k / A.row_block) * A.row_stride + k % A.row_block;
 }
 
 // one frame's camera constants (main.c:243-250)
@@ -823,7 +825,8 @@ template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB 
 __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int frame, int x, int k,
                                              int* __restrict__ stk, Ctr& c, unsigned q = 0,
                                              int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
-    const int y = image_row(A, k);
+    const int y = image_row(A, k, frame);
+    if (y >= A.H) return;  // frame_shift: a rotated rank's compact rows past the image
     const size_t o = (size_t)frame * A.frame_px + (size_t)k * A.W + x;
     int hit0 = -1;
     float t0 = FMAX;

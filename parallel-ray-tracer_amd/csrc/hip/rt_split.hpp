@@ -47,7 +47,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         unsigned masks[MAXB];
 #pragma unroll
         for (int q = 0; q < MAXB; q++) masks[q] = 0;
-        if (x < A.W && k < A.n_rows) {
+        if (x < A.W && k < A.n_rows && image_row(A, k) < A.H) {
             c.pix++;
             const size_t px = (size_t)k * A.W + x;
             v3 o = mk(A.pos[0], A.pos[1], A.pos[2]);

@@ -57,7 +57,8 @@ class SceneDesc(ctypes.Structure):
 class Frame(ctypes.Structure):
     _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("row_offset", ctypes.c_int),
                 ("row_stride", ctypes.c_int), ("n_rows", ctypes.c_int), ("bounces", ctypes.c_int),
-                ("spp", ctypes.c_int), ("kernel", ctypes.c_int), ("row_block", ctypes.c_int)]
+                ("spp", ctypes.c_int), ("kernel", ctypes.c_int), ("row_block", ctypes.c_int),
+                ("frame_shift", ctypes.c_int)]
 
 
 STAT_FIELDS = ["primary", "reflection", "shadow", "shadow_skipped", "hits", "ch_inner", "ch_leaf",

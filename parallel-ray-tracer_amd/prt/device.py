@@ -58,10 +58,11 @@ def _ptr(x):
 
 
 def _rows(rows, height):
-    """rows tuple (offset, stride, n) or (offset, stride, n, block) -> rt_frame fields; None = full frame"""
+    """rows tuple (offset, stride, n[, block[, frame_shift]]) -> rt_frame fields; None = full frame"""
     if rows is None:
-        return 0, 1, height, 1
-    return (tuple(rows) + (1,))[:4]
+        return 0, 1, height, 1, 0
+    r = tuple(rows)
+    return r + (1, 0)[len(r) - 3:] if len(r) < 5 else r[:5]
 
 
 class Renderer:
@@ -104,8 +105,8 @@ class Renderer:
         the full frame.
         rgb / hit / t / bounce_hit ([n, W, bounces] int32) / bgra ([n, W] int32: the BMP-quantised pixel in
         top-down rows, rt_outputs.bgra): optional device tensors (torch) or raw pointers."""
-        ro, rs, nr, rb = _rows(rows, height)
-        f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel), rb)
+        ro, rs, nr, rb, sh = _rows(rows, height)
+        f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel), rb, sh)
         out = Outputs(_ptr(rgb), _ptr(hit), _ptr(t), _ptr(bounce_hit), _ptr(bgra))
         self._chk(_L.rt_render(self._ctx, ctypes.byref(cam), ctypes.byref(f), ctypes.byref(out)), "rt_render")
         self._last = (width, nr)
@@ -116,8 +117,8 @@ class Renderer:
                       t=None, bounce_hit=None, bgra=None):
         """rt_render_frames(): a batch of len(cams) frames of one shape (one persistent launch on the fast
         kernel); outputs [n_frames, n_rows, W, ...]. Asynchronous."""
-        ro, rs, nr, rb = _rows(rows, height)
-        f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel), rb)
+        ro, rs, nr, rb, sh = _rows(rows, height)
+        f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel), rb, sh)
         out = Outputs(_ptr(rgb), _ptr(hit), _ptr(t), _ptr(bounce_hit), _ptr(bgra))
         arr = (Camera * len(cams))(*cams)
         self._chk(_L.rt_render_frames(self._ctx, arr, len(cams), ctypes.byref(f), ctypes.byref(out)),

@@ -47,18 +47,24 @@ class FrameGather:
     frames > 1: a frame batch (rt_render_frames) — every rank's frames are compact ([frames, n_rows, W, C]
     with its OWN n_rows, as rt_render_frames writes them: frame f at f * n_rows * W), at the start of a
     block of frames * padded_rows rows (equal on every rank, as the collective needs) -> frames
-    [frames, H, W, C], one collective for the whole batch. Render into target(i), not blocks[i]. buffers > 1: ping-pong blocks, so that the
+    [frames, H, W, C], one collective for the whole batch. Render into target(i), not blocks[i].
+    rotate (frame batches of row blocks): frame f of rank q renders the block residue (q + f) % world
+    (rt_frame.frame_shift = block), so over a batch every rank renders every residue and the ranks' costs
+    even out whatever the image's cost per residue; every rank then renders padded_rows compact rows per
+    frame (rows past the image are skipped by the kernel) and rank 0 unpacks with one index copy. buffers > 1: ping-pong blocks, so that the
     gather of batch k (start(k % buffers), asynchronous on the collective's stream) overlaps the render of
     batch k + 1 into the other block; finish(i) makes the current stream wait for it and un-interleaves.
     World 1: the block IS the frame (no collective, no copy). On a GPU, rank 0 un-interleaves on a side
     stream, so the copy (F frames of H x W x C) does not delay rank 0's next render — which every rank's
     next gather would wait for."""
 
-    def __init__(self, H, W, C, rank, world, dist, like, frames=1, buffers=1, block=1):
+    def __init__(self, H, W, C, rank, world, dist, like, frames=1, buffers=1, block=1, rotate=False):
         import torch
         self.H, self.W, self.C, self.rank, self.world, self.dist = H, W, C, rank, world, dist
         self.frames = frames
         self.bk = max(1, block)
+        self.rotate = bool(rotate) and frames > 1 and self.bk > 1 and world > 1
+        self._flat = None  # rotate: (source rows, frame rows) of the one index copy
         self.n_max = padded_rows(H, world, self.bk)
         shape = (self.n_max, W, C) if frames == 1 else (frames, self.n_max, W, C)
         self.blocks = [torch.zeros(shape, dtype=like.dtype, device=like.device) for _ in range(buffers)]
@@ -79,7 +85,7 @@ class FrameGather:
 
     def target(self, i=0):
         """blocks[i] as this rank's render output: [frames, n_rows, W, C] compact frames (or [n_rows, W, C])"""
-        n = rank_rows(self.H, self.rank, self.world, self.bk)[2]
+        n = self.n_max if self.rotate else rank_rows(self.H, self.rank, self.world, self.bk)[2]
         b = self.blocks[i]
         if self.frames == 1:
             return b[:n]
@@ -93,6 +99,8 @@ class FrameGather:
     def rows(self):
         """this rank's rt_frame rows: (offset, stride, n) for single rows, (offset, stride, n, block)"""
         r = rank_rows(self.H, self.rank, self.world, self.bk)
+        if self.rotate:  # (offset, stride, padded rows, block, frame_shift = block)
+            return r[0], r[1], self.n_max, self.bk, self.bk
         return r if self.bk > 1 else r[:3]
 
     def start(self, i=0):
@@ -129,6 +137,9 @@ class FrameGather:
         return self.frame
 
     def _uninterleave(self, i):
+        if self.rotate:
+            self._unrotate(i)
+            return
         P = self.parts[i]
         frame = self.frame
         if self.frames == 1:
@@ -147,6 +158,26 @@ class FrameGather:
         else:
             for q in range(self.world):
                 frame[:, q::self.world] = self._part(P, q)
+
+    def _unrotate(self, i):
+        import torch
+        if self._flat is None:
+            N, B, F, n = self.world, self.bk, self.frames, self.n_max
+            src, dst = [], []
+            for q in range(N):
+                for f in range(F):
+                    res = (q + f) % N  # rt_frame: (row_offset + f * frame_shift) % row_stride, in blocks
+                    for k in range(n):
+                        y = res * B + (k // B) * N * B + k % B
+                        if y < self.H:
+                            src.append((q * F + f) * n + k)
+                            dst.append(f * self.H + y)
+            dev = self.frame.device
+            self._flat = (torch.tensor(src, dtype=torch.long, device=dev),
+                          torch.tensor(dst, dtype=torch.long, device=dev))
+        src, dst = self._flat
+        rows = self.parts[i].view(-1, self.W, self.C).index_select(0, src)
+        self.frame.view(-1, self.W, self.C).index_copy_(0, dst, rows)
 
     def gather(self, i=0):
         """collective: every rank calls it after rendering into blocks[i]; the returned frame is ready on

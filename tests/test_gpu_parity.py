@@ -554,3 +554,55 @@ def test_path_buffer_placements_render_the_same_frames(dev, name, monkeypatch):
         assert same_bits(a0["rgb"], a1["rgb"]) and same_bits(b0["rgb"], b1["rgb"]) and same_bits(f0, f1), v
         np.testing.assert_array_equal(a0["hit"], a1["hit"])
         assert a0["stats"]["rays"] == a1["stats"]["rays"], v
+
+
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan"])
+def test_rotated_row_blocks_cover_every_frame(dev, kernel):
+    """rt_frame.frame_shift: frame f of rank q renders block residue (q + f) % N (prt.dist rotate), rows
+    past the image skipped — over the N ranks every frame of the batch is rendered exactly once, bit for
+    bit the single full-frame renders, with the full frames' ray counts"""
+    import torch
+    from prt.dist import padded_rows
+    s = host.Scene.named("dragon").build_bvh(3)
+    W, H, N, B = 96, 54, 3, 8
+    cams = [host.camera(W, H), moved_camera(W, H, 0.25, 0.0), moved_camera(W, H, -0.4, 0.3), host.camera(W, H)]
+    full, rays = [], 0
+    for c in cams:
+        r = dev.Renderer(0, counters=True)
+        r.upload(s)
+        rgb = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        r.render(c, W, H, kernel=select(kernel), rgb=rgb)
+        r.sync()
+        full.append(rgb.cpu().numpy())
+        rays += r.stats()["rays"]
+        r.close()
+    n = padded_rows(H, N, B)
+    got = np.full((len(cams), H, W, 3), -1.0, np.float32)
+    seen = np.zeros((len(cams), H), np.int32)
+    total = 0
+    for q in range(N):
+        r = dev.Renderer(0, counters=True)
+        r.upload(s)
+        rgb = torch.full((len(cams), n, W, 3), -2.0, dtype=torch.float32, device="cuda")
+        r.render_frames(cams, W, H, rows=(q * B, N * B, n, B, B), kernel=select(kernel), rgb=rgb)
+        r.sync()
+        total += r.stats()["rays"]
+        r.close()
+        out = rgb.cpu().numpy()
+        for f in range(len(cams)):
+            off = (q * B + f * B) % (N * B)
+            for k in range(n):
+                y = off + (k // B) * N * B + k % B
+                if y < H:
+                    got[f, y] = out[f, k]
+                    seen[f, y] += 1
+    unforce()
+    assert (seen == 1).all()
+    for f in range(len(cams)):
+        assert same_bits(got[f], full[f]), (kernel, f)
+    assert total == rays
+    r = dev.Renderer(0)
+    r.upload(s)
+    with pytest.raises(dev.RtError):  # rotation is a fast-kernel feature
+        r.render_frames(cams, W, H, rows=(0, N * B, n, B, B), kernel="strict")
+    r.close()

@@ -54,7 +54,7 @@ def _bgra(rgb):
     return (q[..., 2] | (q[..., 1] << 8) | (q[..., 0] << 16) | np.uint32(255 << 24)).view(np.int32)[..., None]
 
 
-def _batch_worker(rank, world, port, W, H, out_path, block, fmt="rgb"):
+def _batch_worker(rank, world, port, W, H, out_path, block, fmt="rgb", rotate=False):
     """two ping-pong batches of 2 frames (the bench's pattern): start(0), render batch 1 while batch 0's
     gather runs, finish(0), start(1), finish(1); the frames of both batches must be the single frame"""
     import sys
@@ -73,16 +73,25 @@ def _batch_worker(rank, world, port, W, H, out_path, block, fmt="rgb"):
     o.build_bvh(3)
     bgra = fmt == "bgra8"  # the bench's default: 4-byte quantised pixels, C = 1
     g = FrameGather(H, W, 1 if bgra else 3, rank, world, dist, torch.zeros(1, dtype=torch.int32 if bgra else
-                    torch.float32), frames=2, buffers=2, block=block)
-    from prt.dist import image_rows
-    rows = image_rows(H, rank, world, block)
-    nr = len(rows)
-    px = o.render(W, H, threads=2)["rgb"][rows]
-    mine = torch.from_numpy(_bgra(px) if bgra else px)
+                    torch.float32), frames=2, buffers=2, block=block, rotate=rotate)
+    full = o.render(W, H, threads=2)["rgb"]
+    if bgra:
+        full = _bgra(full)
+    r = g.rows()
+    off, stride, n = r[:3]
+    B = r[3] if len(r) > 3 else 1
+    sh = r[4] if len(r) > 4 else 0
     out = []
     for b in range(2):
-        for f in range(2):
-            g.target(b)[f] = mine  # compact frames, as rt_render_frames writes them
+        for f in range(2):  # compact frames as rt_render_frames writes them (rotated: rt_frame.frame_shift)
+            o_f = (off + f * sh) % stride if sh else off
+            t = g.target(b)[f]
+            for k in range(n):
+                y = o_f + (k // B) * stride + k % B
+                if y < H:
+                    t[k] = torch.from_numpy(full[y])
+                else:
+                    t[k] = -1  # rows past the image (rotation): never unpacked
         g.start(b)
         if b == 1:
             out.append(g.finish(0).clone() if rank == 0 else None)
@@ -93,9 +102,11 @@ def _batch_worker(rank, world, port, W, H, out_path, block, fmt="rgb"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,H,block,fmt", [(2, 36, 1, "rgb"), (3, 37, 1, "rgb"), (2, 32, 8, "rgb"), (3, 37, 4, "rgb"),
-                                              (2, 32, 8, "bgra8"), (3, 37, 4, "bgra8")])
-def test_batched_pingpong_gather_equals_single_frame(tmp_path, world, H, block, fmt):
+@pytest.mark.parametrize("world,H,block,fmt,rotate", [(2, 36, 1, "rgb", False), (3, 37, 1, "rgb", False),
+                                                     (2, 32, 8, "rgb", False), (3, 37, 4, "rgb", False),
+                                                     (2, 32, 8, "bgra8", False), (3, 37, 4, "bgra8", False),
+                                                     (2, 36, 8, "bgra8", True), (3, 37, 4, "rgb", True)])
+def test_batched_pingpong_gather_equals_single_frame(tmp_path, world, H, block, fmt, rotate):
     import torch.multiprocessing as mp
 
     from tests.oracle_bind import OracleScene
@@ -103,7 +114,8 @@ def test_batched_pingpong_gather_equals_single_frame(tmp_path, world, H, block, 
 
     W = 64  # H % world == 0: one permuted copy; else per-rank strided copies
     out = str(tmp_path / "frames.npy")
-    mp.start_processes(_batch_worker, args=(world, _free_port(), W, H, out, block, fmt), nprocs=world, join=True,
+    mp.start_processes(_batch_worker, args=(world, _free_port(), W, H, out, block, fmt, rotate), nprocs=world,
+                       join=True,
                        start_method="spawn")
     got = np.load(out)
     o = OracleScene.load(*scene_paths("car_only"))

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--kernel", default="fast")
     ap.add_argument("--frames", default="1", help="frames per launch (rt_render_frames), comma list")
     ap.add_argument("--block", type=int, default=1, help="rows dealt in blocks of this many (prt.dist.rank_rows)")
+    ap.add_argument("--rotate", action="store_true", help="frame f of rank q renders residue (q + f) %% N "
+                    "(rt_frame.frame_shift = block; prt.dist.FrameGather rotate)")
     ap.add_argument("--streams", type=int, default=1, help="contexts on separate streams, launches alternate "
                     "(consecutive launches overlap); the time is then wall clock per frame")
     a = ap.parse_args()
@@ -40,6 +42,8 @@ def main():
             per_rank = []
             for q in range(n):
                 rows = rank_rows(a.H, q, n, a.block)
+                if a.rotate and n > 1 and a.block > 1:
+                    rows = (rows[0], rows[1], padded_rows(a.H, n, a.block), a.block, a.block)
                 nr = rows[2]
                 if a.streams == 1:
                     r = device.Renderer(0)
