@@ -118,6 +118,11 @@ def main():
     ap.add_argument("--output", choices=("bgra8", "rgb"), default="bgra8",
                     help="what each frame's kernel writes and the gather moves: bgra8 = the BMP writer's quantised "
                          "pixel (rt_outputs.bgra, 4 B), rgb = the f32 vec_t pixel (12 B)")
+    ap.add_argument("--tune", action="store_true",
+                    help="let rt_render autotune the batches' launch configuration per context (default: the "
+                         "untuned batch configuration, the 4-wave persistent kernel, which the tuner picks on every "
+                         "BASELINE configuration at N = 1 but not reliably per rank at N = 8, where its trials "
+                         "mislead it)")
     ap.add_argument("--no-rotate", action="store_true",
                     help="N > 1: keep each rank on its own block residue in every frame (default: frame f of rank "
                          "q renders residue (q + f) %% N, so every rank's batch costs the same)")
@@ -215,9 +220,13 @@ def main():
                 if fg.pending(b):
                     fg.finish(b)
 
-    # setup, like the upload: the first launch of a scene and batch shape is rt_render's launch-autotuning
-    # launch (every candidate configuration timed, rt_hip.hip); the next launch of that shape reads the
-    # timings. Each batch size of the plan is tuned here, then `warmup` frames run untimed.
+    tune_env = os.environ.get("PRT_TUNE")
+    if not args.tune:
+        os.environ["PRT_TUNE"] = "0"  # read by rt_render per call: batches run the 4-wave persistent kernel
+    # setup, like the upload: with --tune the first launch of a scene and batch shape is rt_render's
+    # launch-autotuning launch (every candidate configuration timed, rt_hip.hip) and the next launch of
+    # that shape reads the timings; each batch size of the plan goes through that here (without --tune
+    # these are plain warm-up launches), then `warmup` frames run untimed.
     for nf in sorted(set(plan)):
         for _ in range(2 * n_streams):  # per context: the tuning launch, then the launch reading its timings
             launch(nf)
@@ -276,6 +285,10 @@ def main():
     rc.close()
     bytes_launch = alg_bytes(stc, F * W * n_r, len(scene.lights), 4 if bgra else 12)
     k_avg_ms = sum(kfull) / len(kfull)
+    if tune_env is None:  # single frames: the autotuned configuration
+        os.environ.pop("PRT_TUNE", None)
+    else:
+        os.environ["PRT_TUNE"] = tune_env
     # single-frame latency of this rank's rows (one launch, one frame; its own tuning launch first)
     rl = device.Renderer(local, stream=stream)
     rl.upload(scene, accel=args.accel)
