@@ -50,11 +50,45 @@ def alg_bytes(st, pixels, n_lights, px_bytes=12):
     return nodes + 48 * tri + (84 + 32 * n_lights) * st["hits"] + px_bytes * pixels
 
 
-def cpu_baseline(scene_files, W, H, gpu_rays_for_rows, args):
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def usable_cpus():
+    """CPUs this process can actually use: its affinity set, capped by the cgroup v2 CPU quota (the GPU box
+    shares a 256-CPU host: 16 CPUs of quota per GPU)"""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def survey_bytes(st, pixels, n_lights, px_bytes):
+    """SURVEY §8d's byte model on the same counters: B_ray = 32 (1 + 2 I) + 40 T with the reference's record
+    sizes (32-B bvh_t box per tested box, 36 B of vertices + 4 B tri_idx per triangle test), plus per hit 12 B
+    normal + 36 B material + 24 B per light and the pixel. The wide walk tests the 8 child boxes of every
+    visited node (8 x 32 B per visit); strict fallbacks' binary visits are in the same counters (2 boxes
+    would be the exact figure: the difference is < 0.1 %)."""
+    rays = st["primary"] + st["reflection"] + st["shadow"]
+    boxes = 8 * (st["ch_inner"] + st["sh_inner"])
+    return 32 * (rays + boxes) + 40 * (st["ch_tri"] + st["sh_tri"]) + (48 + 24 * n_lights) * st["hits"] + \
+        px_bytes * pixels
+
+
+def cpu_baseline(scene_files, W, H, gpu_rays_for_rows, args, threads):
     """The reference itself (oracle/_ref/rt_ref_fast: cpu/src/*.c built with the makefile's flags) timed
     on this host, pthreads with the reference's atomic row scheduler; falls back to the C restatement
     built the same way (kind "port") when the prebuilt reference binary is absent."""
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
     stride = args.cpu_row_stride
     ref = os.path.join(ROOT, "oracle", "_ref", "rt_ref_fast")
     obj, mtl, lts = scene_files
@@ -93,7 +127,11 @@ def cpu_baseline(scene_files, W, H, gpu_rays_for_rows, args):
     out = {"value": rays / (res["median_ms"] / 1e3) / 1e6, "unit": "Mrays/s", "cores": threads, "kind": kind,
            "sample": f"rows y = k*{stride} of the same {W}x{H} frame ({res['rows']} rows, {rays} rays), "
                      f"median of {reps} frames, {threads} pthreads, reference atomic row scheduler, "
-                     f"heuristic-3 BVH (build untimed)"}
+                     f"heuristic-3 BVH (build untimed)",
+           "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+           "build": "cpu/src/*.c with the reference makefile's -O3 -ffast-math -flto, but -march=x86-64-v3 instead "
+                    "of -march=native: the binary is built in the build container and must run on any box "
+                    "(oracle/Makefile); AVX2 + FMA, the same vector ISA the reference's hot loop uses"}
     # the same at 1 thread, on a ~5 s sample (every stride1-th row, one frame)
     if threads > 1 and not args.no_single_thread:
         frame_1t = res["median_ms"] / 1e3 * stride * threads
@@ -119,10 +157,11 @@ def main():
                     help="what each frame's kernel writes and the gather moves: bgra8 = the BMP writer's quantised "
                          "pixel (rt_outputs.bgra, 4 B), rgb = the f32 vec_t pixel (12 B)")
     ap.add_argument("--tune", action="store_true",
-                    help="let rt_render autotune the batches' launch configuration per context (default: the "
-                         "untuned batch configuration, the 4-wave persistent kernel, which the tuner picks on every "
-                         "BASELINE configuration at N = 1 but not reliably per rank at N = 8, where its trials "
-                         "mislead it)")
+                    help="rt_frame.tune = 1 for the batches: each context times the candidate launch configurations "
+                         "(default: the library's rule for batches, the 4-wave persistent kernel, which the tuner "
+                         "picks on every BASELINE configuration at N = 1 but not reliably per rank at N = 8, where "
+                         "its trials mislead it)")
+    ap.add_argument("--variant", default="default", help="rt_frame.variant of the batches (prt.device.VARIANTS)")
     ap.add_argument("--no-rotate", action="store_true",
                     help="N > 1: keep each rank on its own block residue in every frame (default: frame f of rank "
                          "q renders residue (q + f) %% N, so every rank's batch costs the same)")
@@ -136,7 +175,10 @@ def main():
     ap.add_argument("--no-single-thread", action="store_true", help="skip the 1-thread CPU baseline sample")
     ap.add_argument("--kernel", default="fast")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the CPU baseline (default 16, the GPU box's CPU share; also timed at every "
+                         "host CPU, the line's cpu_baseline.all_cpus)")
+    ap.add_argument("--no-all-cpus", action="store_true", help="skip the all-host-CPUs baseline sample")
     ap.add_argument("--cpu-row-stride", type=int, default=0)
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--bmp", default="", help="after timing, rank 0 writes the last frame (gathered) as a BMP "
@@ -148,6 +190,9 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.gpus != world:  # never a silent one-GPU run labelled N: N ranks come from the launcher
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N ranks with "
+                 f"`python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}`")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal of the multi-rank flow on a one-GPU box (never set by the driver): PRT_DIST_ONE_GPU=1 puts
     # every rank on device 0, PRT_DIST_BACKEND=gloo replaces RCCL (which refuses two ranks on one GPU)
@@ -211,7 +256,7 @@ def main():
             if fg.pending(b):
                 fg.finish(b)
             rends[c].render_frames([cam] * nf, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
-                                   kernel=args.kernel, **out(fg.target(b)))
+                                   kernel=args.kernel, variant=args.variant, tune=args.tune, **out(fg.target(b)))
             fg.start(b)
 
     def drain():
@@ -220,9 +265,6 @@ def main():
                 if fg.pending(b):
                     fg.finish(b)
 
-    tune_env = os.environ.get("PRT_TUNE")
-    if not args.tune:
-        os.environ["PRT_TUNE"] = "0"  # read by rt_render per call: batches run the 4-wave persistent kernel
     # setup, like the upload: with --tune the first launch of a scene and batch shape is rt_render's
     # launch-autotuning launch (every candidate configuration timed, rt_hip.hip) and the next launch of
     # that shape reads the timings; each batch size of the plan goes through that here (without --tune
@@ -280,20 +322,18 @@ def main():
     rc = device.Renderer(local, counters=True, stream=stream)
     rc.upload(scene, accel=args.accel)
     rc.render_frames([cam] * F, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
-                     kernel=args.kernel, **out(fg.target(0)))
+                     kernel=args.kernel, variant=args.variant, **out(fg.target(0)))
     stc = rc.stats()
     rc.close()
     bytes_launch = alg_bytes(stc, F * W * n_r, len(scene.lights), 4 if bgra else 12)
+    survey_launch = survey_bytes(stc, F * W * n_r, len(scene.lights), 4 if bgra else 12)
+    simd_eff = (stc["ch_inner"] + stc["sh_inner"]) / max(1, 64 * stc["wave_steps"])
     k_avg_ms = sum(kfull) / len(kfull)
-    if tune_env is None:  # single frames: the autotuned configuration
-        os.environ.pop("PRT_TUNE", None)
-    else:
-        os.environ["PRT_TUNE"] = tune_env
-    # single-frame latency of this rank's rows (one launch, one frame; its own tuning launch first)
+    # single-frame latency of this rank's rows (one launch, one frame; autotuned: its trial launch first)
     rl = device.Renderer(local, stream=stream)
     rl.upload(scene, accel=args.accel)
     for _ in range(3):
-        rl.render(cam, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp, kernel=args.kernel,
+        rl.render(cam, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp, kernel=args.kernel, tune=True,
                   **out(fg.target(0)[0] if F > 1 else fg.target(0)))
     lat_ms = sorted(rl.kernel_times(2))[0]
     rl.close()
@@ -302,13 +342,14 @@ def main():
         dist.all_reduce(lat, op=dist.ReduceOp.MAX)
 
     if rank == 0:
-        traffic = None
+        traffic, pmc = None, {}
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
                 key = f"{args.scene}_{W}x{H}_{args.kernel}_{args.bvh}" + ("_bgra8" if bgra else "")
                 if key in tj:
                     traffic = tj[key]["hbm_bytes_per_launch"]
+                    pmc = tj[key]
             except Exception:
                 traffic = None
         achieved = bytes_launch / (k_avg_ms / 1e3) / 1e9
@@ -339,12 +380,25 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": k_avg_ms, "alg_bytes_per_launch": bytes_launch, "frames_per_launch": F,
                          "achieved_steady": bytes_launch / F * K / elapsed / 1e9, "streams": n_streams,
-                         "note": "algorithmic bytes (node/triangle/shading records the kernel reads) of one launch / "
-                                 "its HIP-event duration (two launches overlap on two streams, so this is "
-                                 "conservative; achieved_steady = the same bytes per frame x frames / wall time); "
-                                 "the ~6 MB scene stays L2/MALL-resident, so HBM traffic is far lower"},
+                         # the same launch priced with SURVEY §8d's formula (reference record sizes): comparable
+                         # with BASELINE.md's 3.45 / 6.3 Grays/s roofline-equivalent rates
+                         "survey_bytes_per_launch": survey_launch,
+                         "survey_achieved": survey_launch / (k_avg_ms / 1e3) / 1e9,
+                         "survey_frac": survey_launch / (k_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                         "simd_efficiency": simd_eff,
+                         # measured by rocprofv3 PMC passes of this command (profiles/pmc_traffic.json)
+                         "hbm_frac_measured": (traffic / (k_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                         "valu_issue_frac": pmc.get("valu_issue_frac"),
+                         "l2_read_bytes_per_launch": pmc.get("l2_read_bytes_per_launch"),
+                         "limiter": ("dependent-load latency and VALU issue (HBM traffic is ~1 % of the algorithmic "
+                                     "bytes: the scene is L2/MALL-resident)") if traffic and traffic < 0.05 * bytes_launch
+                                    else "see DESIGN.md §5",
+                         "note": "achieved / frac: algorithmic bytes (the node / triangle / shading records the kernel "
+                                 "reads, DESIGN.md §5) of one launch / its HIP-event duration. These are cache bytes, "
+                                 "not HBM bytes: hbm_frac_measured is the HBM share (FETCH_SIZE x 2 + WRITE_SIZE)"},
         }
         if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, usable_cpus())
             def gpu_rays_for_rows(stride):
                 nr = (H + stride - 1) // stride
                 rr = device.Renderer(local, stream=stream)
@@ -355,7 +409,15 @@ def main():
                 rr.close()
                 return n
             try:
-                result["cpu_baseline"] = cpu_baseline(files, W, H, gpu_rays_for_rows, args)
+                result["cpu_baseline"] = cpu_baseline(files, W, H, gpu_rays_for_rows, args, threads)
+                allc = min(256, usable_cpus())  # nproc: the CPUs this process may use (affinity, cgroup quota)
+                result["cpu_baseline"]["nproc"] = allc
+                if allc != threads and not args.no_all_cpus:  # also at nproc threads
+                    a1 = argparse.Namespace(**vars(args))
+                    a1.no_single_thread = True
+                    a1.cpu_row_stride = 0
+                    r = cpu_baseline(files, W, H, gpu_rays_for_rows, a1, allc)
+                    result["cpu_baseline"]["all_cpus"] = {k: r[k] for k in ("value", "unit", "cores", "sample")}
             except Exception as e:  # reported, never silently replaced
                 result["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(result), flush=True)

@@ -13,7 +13,9 @@
  *
  * The per-pixel hot path (ray generation, BVH traversal, ray-triangle intersection, Lambert/Blinn
  * shading with shadow rays, the BOUNCES reflection loop, clamp) runs in ONE HIP kernel per frame
- * (RT_KERNEL_WAVEFRONT, an A/B alternative, splits it into ~6 launches per bounce).
+ * (or per batch of frames, rt_render_frames). Every launch configuration is chosen through the
+ * arguments below (rt_frame.variant / tune / waves_cap / dealing / regroup); the library reads no
+ * environment variable on the render path except two diagnostics (PRT_TILE_TRACE, PRT_TUNE_LOG).
  */
 #ifndef RT_HIP_H
 #define RT_HIP_H
@@ -64,9 +66,34 @@ enum {
 enum {
     RT_KERNEL_AUTO = 0,   /* RT_KERNEL_FAST */
     RT_KERNEL_STRICT = 1, /* reference-order traversal, exact slab divisions: bit-exact by construction */
-    RT_KERNEL_FAST = 2,   /* persistent waves, one 8x8 tile per wave, one lane per pixel path (k_persist) */
-    RT_KERNEL_WAVEFRONT = 3, /* wavefront pipeline: traversal kernels over HBM ray queues (rt_wf.hpp); A/B only */
-    RT_KERNEL_WAVE = 4    /* persistent per-lane ray state machine in one kernel (k_wave); A/B only */
+    RT_KERNEL_FAST = 2    /* the fast walk (8-wide quantised BVH) in the launch configuration rt_frame.variant
+                             names; every variant renders the same bits as RT_KERNEL_STRICT */
+};
+
+/* rt_frame.variant: launch configuration of RT_KERNEL_FAST */
+enum {
+    RT_VARIANT_DEFAULT = 0,  /* the library's rule: RT_VARIANT_PERSIST4 for frame batches, RT_VARIANT_PERSIST for single
+                                frames, RT_VARIANT_SPLIT for single 1-spp frames of scenes with >= 3 lights; with
+                                rt_frame.tune = 1 the measured fastest candidate instead */
+    RT_VARIANT_PERSIST = 1,  /* k_persist: one lane per pixel path, walks in lockstep, 3 waves per SIMD */
+    RT_VARIANT_PERSIST4 = 2, /* k_persist at 4 waves per SIMD (path levels in LDS) */
+    RT_VARIANT_SPLIT = 3,    /* closest chains / shadow batches / resolve: three launches (1 spp; one frame per launch) */
+    RT_VARIANT_COOP2 = 4,    /* k_coop: 2 lanes per ray (shorter chains for small row sets) */
+    RT_VARIANT_COOP4 = 5,    /* k_coop: 4 lanes per ray */
+    RT_VARIANT_COOP8 = 6,    /* k_coop: 8 lanes per ray */
+    RT_VARIANT_FAN = 7,      /* k_fan: 1 + lights lanes per pixel (shadow fan-out; 1..7 lights) */
+    RT_VARIANT_CHAIN = 8,    /* k_chain: one lane per pixel path, each lane's walks back to back, 3 waves per SIMD */
+    RT_VARIANT_CHAIN4 = 9    /* k_chain at 4 waves per SIMD */
+};
+
+/* rt_frame.dealing: order in which persistent waves take 8x8 tiles (k_persist, k_chain) */
+enum {
+    RT_DEAL_DEFAULT = 0,  /* XCD-aware: 4 x 2 regions for batches of full frames, 8 row bands otherwise */
+    RT_DEAL_GLOBAL = 1,   /* one counter over the centre-out order */
+    RT_DEAL_ROWS = 2,     /* 8 bands of tile rows, band r drained first by the workgroups of XCD r */
+    RT_DEAL_COLUMNS = 3,  /* 8 bands of tile columns */
+    RT_DEAL_BLOCKS = 4,   /* 4 x 2 blocks */
+    RT_DEAL_ROW_MAJOR = 5 /* one counter, row-major tile order */
 };
 
 /* Rows rendered: y = row_offset + (k / B) * row_stride + k % B for k in [0, n_rows), B = max(1, row_block)
@@ -85,6 +112,15 @@ typedef struct rt_frame {
                       * of rt_render_frames starts at (row_offset + f * S) % row_stride, so that ranks dealt
                       * block-cyclic rows rotate through every block residue over a batch and their costs
                       * even out; compact rows whose image row falls at or past height are skipped. */
+    /* launch configuration (RT_KERNEL_FAST; all zero = the library's defaults) */
+    int variant;   /* RT_VARIANT_* */
+    int tune;      /* 1 (with RT_VARIANT_DEFAULT): the first frame of each (scene upload, frame shape) runs every
+                      candidate variant three times into the same outputs, the next frame of that shape reads their
+                      HIP-event times and the fastest renders from then on; 0: the default rule, no trial launches */
+    int waves_cap; /* persistent grids: at most this many workgroups (4 waves each) per CU; 0 = occupancy limit */
+    int dealing;   /* RT_DEAL_* */
+    int regroup;   /* k_chain: lanes whose walk ended wait until this many wait (or no lane walks), then advance
+                      together; 0 = the default (16) */
 } rt_frame;
 
 /* Device output pointers (all nullable). rgb: [n_rows][width][3] f32 in [0,1] = vec_t pixels

@@ -2,7 +2,10 @@
 //
 //   raytracer [threads] [ntris] [--scene NAME] [--assets DIR] [--width W] [--height H]
 //             [--bounces B] [--iterations K] [--warmup W] [--bvh-heuristic H] [--seed S]
-//             [--gpus N] [--spp S] [--kernel fast|strict|wavefront|wave] [--out FILE.bmp] [--cache DIR]
+//             [--gpus N] [--spp S] [--kernel fast|strict|VARIANT] [--tune] [--out FILE.bmp] [--cache DIR]
+//   VARIANT: persist, persist4, split, coop2, coop4, coop8, fan, chain, chain4 (rt_frame.variant; the fast
+//   kernel's launch configurations, all rendering the same bits); --tune: measure the candidates on the
+//   first frame and keep the fastest (rt_frame.tune)
 //
 // Positional arguments and defaults are the reference's (options.h: 1920x1080, car_boxed, BOUNCES 4,
 // ITERATIONS 1, BVH_HEURISTIC 3, SEED 1; main.c:97-131: `threads` in 1..63, `ntris` = random mode).
@@ -31,7 +34,7 @@ struct Args {
     int threads = 1;
     long ntris = -1;
     std::string scene = "car_boxed", assets = "../assets", out, kernel = "fast", cache;
-    int W = 1920, H = 1080, bounces = 4, iterations = 1, warmup = 0, heuristic = 3, gpus = 1, spp = 1;
+    int W = 1920, H = 1080, bounces = 4, iterations = 1, warmup = 0, heuristic = 3, gpus = 1, spp = 1, tune = 0;
     unsigned seed = 1;
 };
 
@@ -61,6 +64,7 @@ Args parse(int argc, char** argv) {
         else if (s == "--gpus") a.gpus = std::atoi(val().c_str());
         else if (s == "--spp") a.spp = std::atoi(val().c_str());
         else if (s == "--kernel") a.kernel = val();
+        else if (s == "--tune") a.tune = 1;
         else if (s == "--out") a.out = val();
         else if (s == "--cache") a.cache = val();
         else if (s.rfind("--", 0) == 0) usage(("unknown option " + s).c_str());
@@ -151,10 +155,14 @@ int main(int argc, char** argv) {
             return EXIT_FAILURE;
         }
     }
-    int kern = a.kernel == "strict" ? RT_KERNEL_STRICT
-               : a.kernel == "wavefront" ? RT_KERNEL_WAVEFRONT
-               : a.kernel == "wave" ? RT_KERNEL_WAVE
-               : a.kernel == "fast" ? RT_KERNEL_FAST : -1;
+    static const char* variants[] = {"fast", "persist", "persist4", "split", "coop2",
+                                     "coop4", "coop8", "fan", "chain", "chain4"};
+    int kern = a.kernel == "strict" ? RT_KERNEL_STRICT : -1, variant = RT_VARIANT_DEFAULT;
+    for (int v = 0; v < 10 && kern < 0; v++)
+        if (a.kernel == variants[v]) {
+            kern = RT_KERNEL_FAST;
+            variant = v;
+        }
     if (kern < 0) {
         std::fprintf(stderr, "unknown --kernel %s\n", a.kernel.c_str());
         return EXIT_FAILURE;
@@ -172,6 +180,8 @@ int main(int argc, char** argv) {
                 int nr = 0;
                 for (int j = g; j < nb; j += G) nr += std::min(B, a.H - j * B);
                 rt_frame f{a.W, a.H, g * B, G * B, nr, a.bounces, a.spp, kern, B};
+                f.variant = variant;
+                f.tune = a.tune;
                 int s = rt_render(ctx[g], &cam, &f, nullptr);
                 if (s == RT_OK) s = rt_sync(ctx[g], nullptr);
                 status[g] = s;

@@ -72,7 +72,7 @@ struct KArgs {
     unsigned long long* counters;  // RT_NCOUNT slots (rt_stats order)
     unsigned int* work;            // persistent-kernel tile / pixel counter
     int n_tiles, tiles_x;
-    int refill_below;              // k_wave: leave the traversal loop when fewer lanes than this still trace
+    int regroup;                   // k_chain: lanes whose walk ended advance together once this many wait
     unsigned long long* tile_trace;  // diagnostics (PRT_TILE_TRACE): per-tile timeline (rt_kernels.hpp)
     const int* tile_order;           // nullable: k-th dealt tile = tile_order[k] (default: row-major)
     // split pipeline (rt_split.hpp): per (level, tile slot) records, path info, visibility bytes, batches

@@ -20,8 +20,7 @@
 #include "rt_fan.hpp"
 #include "rt_output.hpp"
 #include "rt_split.hpp"
-#include "rt_wave.hpp"
-#include "rt_wf.hpp"
+#include "rt_chain.hpp"
 
 #include <cstdlib>
 
@@ -95,36 +94,30 @@ struct rt_ctx {
     unsigned* d_sbatch = nullptr;
     size_t srec_cap = 0, spinfo_cap = 0, svis_cap = 0, sbatch_cap = 0;
     unsigned long long* d_counters = nullptr;  // rtd::NCOUNT
-    std::unordered_map<long long, int*> orders;  // tile dealing orders (PRT_TILE_ORDER), per tx x ty tile grid
+    std::unordered_map<long long, int*> orders;  // tile dealing orders (rt_frame.dealing), per tx x ty tile grid
     unsigned int* d_work = nullptr;
-    // wavefront pipeline buffers (rt_wf.hpp), sized for wf_pix pixels x wf_lights lights
-    void* wf_mem = nullptr;
-    size_t wf_pix = 0;
-    int wf_lights = 0;
-    float4 *wf_cq[2] = {nullptr, nullptr}, *wf_sq = nullptr, *wf_hrec = nullptr, *wf_lev = nullptr;
-    unsigned char* wf_vis = nullptr;
-    int *wf_fq = nullptr, *wf_plen = nullptr;
-    unsigned* wf_q = nullptr;
     static constexpr int NEV = 64;  // ring of per-launch event pairs (rt_kernel_times)
     hipEvent_t ev0s[NEV] = {}, ev1s[NEV] = {};
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // the last launch's pair
+    hipEvent_t gather_ev = nullptr;           // completion of the last rt_gather into this (root) context
     long long launches = 0;
     bool rendered = false;
     // launch autotuning of RT_KERNEL_FAST (rt_render): the candidate configurations are timed on the
     // first frame of a (scene upload, frame shape) and the fastest one renders the frames after it
-    static constexpr int TUNE_MAX = 8, TUNE_REPS = 3;
+    static constexpr int TUNE_MAX = 10, TUNE_REPS = 3;
     struct Tune {
         long long scene = -1;
         int W = 0, rows = 0, bounces = 0, spp = 0, frames = 0;
+        int off = 0, stride = 0, block = 0, shift = 0, dealing = 0, cap_req = 0;  // the rest of the frame shape
         int n = 0, choice = -1;  // candidates; the chosen one (-1: not decided yet)
         bool pending = false;    // trial launches enqueued, timings not read yet
-        int mode[TUNE_MAX] = {};  // M_PERSIST, M_SPLIT, or the group size G of k_coop (2, 4, 8)
+        int mode[TUNE_MAX] = {};  // RT_VARIANT_*
         int cap[TUNE_MAX] = {};
         float ms[TUNE_MAX] = {};
         hipEvent_t e0[TUNE_MAX * TUNE_REPS] = {}, e1[TUNE_MAX * TUNE_REPS] = {};
     };
-    // one tuning state per (scene upload, width, rows, bounces, spp, frames): a context that alternates
-    // frame shapes (e.g. batches of two sizes) keeps every decision
+    // one tuning state per (scene upload, frame shape: width, rows, their offset / stride / block / shift,
+    // bounces, spp, frames, dealing, waves cap): a context that alternates frame shapes keeps every decision
     std::vector<Tune> tunes;
     long long scene_gen = 0;  // bumped by every upload
 };
@@ -418,6 +411,7 @@ namespace {
 // resident workgroups per CU of a persistent kernel (occupancy API, capped at 8)
 template <class K>
 int resident(K kernel, int device, int cap = 8, size_t dyn_lds = 0) {
+    if (cap <= 0) cap = 8;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, rtd::BLOCK, dyn_lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
@@ -426,209 +420,67 @@ int resident(K kernel, int device, int cap = 8, size_t dyn_lds = 0) {
     return std::max(1, std::min(per_cu, cap)) * cus;
 }
 
-// per-CU block cap from the environment (A/B knobs), else `def`
-int env_cap(const char* name, int def) {
-    const char* e = std::getenv(name);
-    return e && std::atoi(e) > 0 ? std::atoi(e) : def;
-}
-
+// k_persist / k_chain (the persistent one-lane-per-path kernels) in configuration `variant`:
+//   RT_VARIANT_PERSIST   k_persist, <= 168 VGPRs (3 waves per SIMD), path levels in registers;
+//   RT_VARIANT_PERSIST4  k_persist, <= 128 VGPRs (4 waves per SIMD), path levels in a path buffer: in LDS after
+//                        the wide stack sized to the scene's wide depth when 4 workgroups of that fit a CU (LDS
+//                        measured 1.2 % faster than the global slab on dragon, 2.3 % on car_boxed), else global;
+//   RT_VARIANT_CHAIN(4)  k_chain (rt_chain.hpp), 3 (4) waves per SIMD, path levels in LDS.
+// `cap`: workgroups per CU at most (0: the occupancy limit); the grid never exceeds the tiles / 4.
 template <int MAXB>
-void launch(const rtd::KArgs& A, int kernel, bool count, dim3 grid_tiles, int device, hipStream_t s, int cap,
-            int occ = 3) {
-    if (kernel == RT_KERNEL_STRICT) {
-        if (count) rtd::k_tiles<MAXB, true, true><<<grid_tiles, rtd::BLOCK, 0, s>>>(A);
-        else rtd::k_tiles<MAXB, true, false><<<grid_tiles, rtd::BLOCK, 0, s>>>(A);
-    } else if (kernel == RT_KERNEL_FAST) {
-        // one wave per 8x8 tile, never more workgroups than tiles / 4
-        auto k = count ? rtd::k_persist<MAXB, false, true> : rtd::k_persist<MAXB, false, false>;
-        if (const char* e = std::getenv("PRT_PERSIST_REG"); e && std::atoi(e) == 0)  // A/B: stack-only walk
-            k = count ? rtd::k_persist<MAXB, false, true, false> : rtd::k_persist<MAXB, false, false, false>;
-        if (const char* e = std::getenv("PRT_PERSIST_OCC"); e && std::atoi(e) == 4) occ = 4;  // A/B knob
-        // occ 4: <= 128 VGPRs, 4 waves per SIMD, each path level's colour + material in a path buffer. The
-        // buffer lives in LDS (after the wide stack sized to the scene's wide depth; DYN kernels) when 4
-        // workgroups of that still fit a CU, else in global memory (where its 2 MB per XCD competes with
-        // the scene for L2: LDS measured 1.2 % faster on dragon, 2.3 % on car_boxed; PRT_PB_LDS=0 = A/B)
-        size_t dyn = 0;
-        const size_t pbl_dyn = sizeof(int) * 2 * (size_t)A.wcap * rtd::BLOCK + sizeof(float4) * rtd::BLOCK * MAXB;
-        bool pbl = occ == 4 && A.gstack && A.wcap > 0;
-        if (const char* e = std::getenv("PRT_PB_LDS"); e && std::atoi(e) == 0) pbl = false;
+void launch_paths(const rtd::KArgs& A, int variant, bool count, int device, hipStream_t s, int cap) {
+    const bool batch = A.n_frames > 1;
+    const bool chain = (variant == RT_VARIANT_CHAIN || variant == RT_VARIANT_CHAIN4) && A.s.wide.nodes && A.gstack &&
+                       A.wcap > 0;
+    const size_t lds_wide = sizeof(int) * 2 * (size_t)A.wcap * rtd::BLOCK;
+    const size_t lds_pb = sizeof(float4) * rtd::BLOCK * MAXB;
+    const int cu_cap = cap > 0 ? cap : 8;
+    if (chain) {
+        auto k = count ? rtd::k_chain<MAXB, true, 3, false> : rtd::k_chain<MAXB, false, 3, false>;
+        if (variant == RT_VARIANT_CHAIN4) k = count ? rtd::k_chain<MAXB, true, 4, false> : rtd::k_chain<MAXB, false, 4, false>;
+        if (batch) {
+            k = count ? rtd::k_chain<MAXB, true, 3, true> : rtd::k_chain<MAXB, false, 3, true>;
+            if (variant == RT_VARIANT_CHAIN4) k = count ? rtd::k_chain<MAXB, true, 4, true> : rtd::k_chain<MAXB, false, 4, true>;
+        }
+        const size_t dyn = lds_wide + lds_pb;
+        const int blocks = std::max(1, std::min(resident(k, device, cu_cap, dyn), (A.n_tiles * A.n_frames + 3) / 4));
+        k<<<blocks, rtd::BLOCK, dyn, s>>>(A);
+        return;
+    }
+    if (A.tile_trace) {  // diagnostics (PRT_TILE_TRACE): the 3-wave kernel with per-tile timestamps
+        auto k = count ? rtd::k_persist<MAXB, false, true, true, 3, true> : rtd::k_persist<MAXB, false, false, true, 3, true>;
+        k<<<std::max(1, std::min(resident(k, device, cu_cap), (A.n_tiles + 3) / 4)), rtd::BLOCK, 0, s>>>(A);
+        return;
+    }
+    auto k = count ? rtd::k_persist<MAXB, false, true> : rtd::k_persist<MAXB, false, false>;
+    if (batch) k = count ? rtd::k_persist<MAXB, false, true, true, 3, false, true> : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
+    size_t dyn = 0;
+    if (variant == RT_VARIANT_PERSIST4) {
+        bool pbl = A.gstack && A.wcap > 0;
         if (pbl) {
             int per_cu = 0;
             auto kp = rtd::k_persist<MAXB, false, false, true, 4, false, true, 2, true>;
-            pbl = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, rtd::BLOCK, pbl_dyn) == hipSuccess &&
+            pbl = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, rtd::BLOCK, lds_wide + lds_pb) == hipSuccess &&
                   per_cu >= 4;
         }
-        if (occ == 4) {
+        if (pbl) {
+            dyn = lds_wide + lds_pb;
+            k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, false, 2, true>
+                      : rtd::k_persist<MAXB, false, false, true, 4, false, false, 2, true>;
+            if (batch) k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, 2, true>
+                                 : rtd::k_persist<MAXB, false, false, true, 4, false, true, 2, true>;
+        } else {
             k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, false, true>
                       : rtd::k_persist<MAXB, false, false, true, 4, false, false, true>;
-            if (pbl)
-                k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, false, 2, true>
-                          : rtd::k_persist<MAXB, false, false, true, 4, false, false, 2, true>;
+            if (batch) k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, true>
+                                 : rtd::k_persist<MAXB, false, false, true, 4, false, true, true>;
         }
-        if (A.n_frames > 1) {  // frame batch: cameras from A.cams
-            k = count ? rtd::k_persist<MAXB, false, true, true, 3, false, true>
-                      : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
-            if (occ == 4) {
-                k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, true>
-                          : rtd::k_persist<MAXB, false, false, true, 4, false, true, true>;
-                if (pbl)
-                    k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, 2, true>
-                              : rtd::k_persist<MAXB, false, false, true, 4, false, true, 2, true>;
-            }
-            if (const char* e = std::getenv("PRT_PERSIST_OCC"); e && A.gstack && A.wcap > 0) {  // DYN A/B knob
-                const int o = std::atoi(e);
-                if (o == 5) k = count ? rtd::k_persist<MAXB, false, true, true, 5, false, true, true, true>
-                                      : rtd::k_persist<MAXB, false, false, true, 5, false, true, true, true>;
-                if (o == 6) k = count ? rtd::k_persist<MAXB, false, true, true, 6, false, true, true, true>
-                                      : rtd::k_persist<MAXB, false, false, true, 6, false, true, true, true>;
-                if (o == 8) k = count ? rtd::k_persist<MAXB, false, true, true, 8, false, true, true, true>
-                                      : rtd::k_persist<MAXB, false, false, true, 8, false, true, true, true>;
-                if (o == 5 || o == 6 || o == 8) {
-                    dyn = sizeof(int) * 2 * (size_t)A.wcap * rtd::BLOCK;
-                    pbl = false;
-                }
-            }
-        }
-        if (pbl) dyn = pbl_dyn;
-        if (A.tile_trace) {  // diagnostics (PRT_TILE_TRACE)
-            k = count ? rtd::k_persist<MAXB, false, true, true, 3, true> : rtd::k_persist<MAXB, false, false, true, 3, true>;
-            dyn = 0;
-        }
-        if (const char* e = std::getenv("PRT_REGEN"); e && std::atoi(e) == 1 && A.spp <= 1) {  // A/B: path regeneration
-            auto kr = count ? rtd::k_regen<MAXB, true> : rtd::k_regen<MAXB, false>;
-            int blocks = std::max(1, std::min(resident(kr, device), (A.n_tiles + 3) / 4));
-            kr<<<blocks, rtd::BLOCK, 0, s>>>(A);
-            return;
-        }
-        int blocks = std::max(1, std::min(resident(k, device, cap, dyn), (A.n_tiles + 3) / 4));
-        k<<<blocks, rtd::BLOCK, dyn, s>>>(A);
-    } else {
-        const char* ev = std::getenv("PRT_WAVE_VARIANT");  // "4": the 128-VGPR build (A/B knob)
-        const int variant = ev ? std::atoi(ev) : 0;
-        auto k = count ? rtd::k_wave<MAXB, true> : rtd::k_wave<MAXB, false>;
-        if (variant == 4) k = count ? rtd::k_wave4<MAXB, true> : rtd::k_wave4<MAXB, false>;
-        int blocks = std::max(1, std::min(resident(k, device), (A.n_tiles + 3) / 4));
-        k<<<blocks, rtd::BLOCK, 0, s>>>(A);
     }
+    const int blocks = std::max(1, std::min(resident(k, device, cu_cap, dyn), (A.n_tiles + 3) / 4));
+    k<<<blocks, rtd::BLOCK, dyn, s>>>(A);
 }
 
 rtd::DBvh dview(const DevView& v) { return rtd::DBvh{v.nodes, v.leaves, v.tris, v.orig, v.root}; }
-
-// one allocation for every wavefront buffer, carved at 256-B boundaries
-int wf_reserve(rt_ctx* ctx, size_t npix, int lights) {
-    const int L = std::max(lights, 1);
-    if (ctx->wf_mem && ctx->wf_pix >= npix && ctx->wf_lights >= L) return RT_OK;
-    if (ctx->wf_mem) HIPC(hipFree(ctx->wf_mem));
-    ctx->wf_mem = nullptr;
-    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t sz[] = {al(npix * 32), al(npix * 32), al(npix * L * 32), al(npix * 16), al(npix * rtd::WF_MAXB * 16),
-                         al(npix * L), al(npix * L * 4), al(npix * 4), al(rtd::Q_N * 4)};
-    size_t total = 0;
-    for (size_t b : sz) total += b;
-    HIPC(hipMalloc(&ctx->wf_mem, total));
-    char* p = (char*)ctx->wf_mem;
-    ctx->wf_cq[0] = (float4*)p;
-    p += sz[0];
-    ctx->wf_cq[1] = (float4*)p;
-    p += sz[1];
-    ctx->wf_sq = (float4*)p;
-    p += sz[2];
-    ctx->wf_hrec = (float4*)p;
-    p += sz[3];
-    ctx->wf_lev = (float4*)p;
-    p += sz[4];
-    ctx->wf_vis = (unsigned char*)p;
-    p += sz[5];
-    ctx->wf_fq = (int*)p;
-    p += sz[6];
-    ctx->wf_plen = (int*)p;
-    p += sz[7];
-    ctx->wf_q = (unsigned*)p;
-    ctx->wf_pix = npix;
-    ctx->wf_lights = L;
-    return RT_OK;
-}
-
-template <class K>
-int blocks_resident(K kernel, int device, int cap) {
-    return std::max(1, std::min(resident(kernel, device), cap));
-}
-
-// the wavefront pipeline: ~6 launches per bounce level on the context stream, counts stay on the device
-int launch_wf(rt_ctx* ctx, const rtd::KArgs& K, bool count) {
-    const size_t npix = (size_t)K.W * K.n_rows;
-    // queue entries are 8x8-tile-padded pixel ids (k_wf_primary writes n_tiles * 64 entries)
-    const size_t nent = (size_t)K.n_tiles * 64;
-    if (nent < npix || K.tiles_x * 8 < K.W || (size_t)K.n_tiles * 8 < (size_t)K.n_rows * K.tiles_x)
-        return arg_err(ctx, "launch_wf: tile grid does not cover the frame");
-    int rc = wf_reserve(ctx, nent, K.s.n_lights);
-    if (rc) return rc;
-    rtd::WfArgs A;
-    std::memset(&A, 0, sizeof A);
-    A.s = K.s;
-    for (int i = 0; i < 3; i++) {
-        A.pos[i] = K.pos[i];
-        A.ul[i] = K.ul[i];
-        A.ix[i] = K.ix[i];
-        A.iy[i] = K.iy[i];
-    }
-    A.W = K.W;
-    A.n_rows = K.n_rows;
-    A.row_offset = K.row_offset;
-    A.row_stride = K.row_stride;
-    A.tiles_x = K.tiles_x;
-    A.n_tiles = K.n_tiles;
-    A.bounces = K.bounces;
-    A.cq[0] = ctx->wf_cq[0];
-    A.cq[1] = ctx->wf_cq[1];
-    A.sq = ctx->wf_sq;
-    A.hrec = ctx->wf_hrec;
-    A.vis = ctx->wf_vis;
-    A.fq = ctx->wf_fq;
-    A.lev = ctx->wf_lev;
-    A.plen = ctx->wf_plen;
-    A.rgb = K.rgb;
-    A.hit = K.hit;
-    A.t = K.t;
-    A.q = ctx->wf_q;
-    A.counters = K.counters;
-    A.refill_below = K.refill_below;
-    auto knob = [](const char* name, int dflt) {  // A/B tuning knobs (tools/ab.py)
-        const char* e = std::getenv(name);
-        return e ? std::atoi(e) : dflt;
-    };
-    A.chunk_min = std::max(1, knob("PRT_WF_CHUNK_MIN", 64));
-    A.chunk_max = std::max(A.chunk_min, knob("PRT_WF_CHUNK_MAX", 2048));
-    const int bpc = knob("PRT_WF_BPC", 0);  // workgroups per CU for the trace kernels (0 = occupancy API)
-    hipStream_t s = ctx->stream;
-    const int dev = ctx->device;
-    const int B = rtd::WF_BLOCK;
-    const int grid_px = (int)std::max<size_t>(1, std::min<size_t>((npix + B - 1) / B, 2048));
-    const int grid_id = (int)std::max<size_t>(1, std::min<size_t>(((size_t)K.n_tiles * 64 + B - 1) / B, 2048));
-    auto tc = count ? rtd::k_wf_trace<false, true> : rtd::k_wf_trace<false, false>;
-    auto ts = count ? rtd::k_wf_trace<true, true> : rtd::k_wf_trace<true, false>;
-    int gtc = blocks_resident(tc, dev, (int)((nent + 255) / 256));
-    int gts = blocks_resident(ts, dev, (int)((nent * std::max(1, K.s.n_lights) + 255) / 256));
-    if (bpc > 0) {
-        int cus = 256;
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        gtc = gts = bpc * cus;
-    }
-    HIPC(hipMemsetAsync(ctx->wf_q, 0, rtd::Q_N * sizeof(unsigned), s));
-    rtd::k_wf_primary<<<grid_id, B, 0, s>>>(A);
-    for (int lv = 0; lv < K.bounces; lv++) {
-        A.level = lv;
-        A.cur = lv & 1;
-        tc<<<gtc, B, 0, s>>>(A);
-        rtd::k_wf_fallback<false><<<64, B, 0, s>>>(A);
-        rtd::k_wf_shade<<<grid_px, B, 0, s>>>(A);
-        ts<<<gts, B, 0, s>>>(A);
-        rtd::k_wf_fallback<true><<<64, B, 0, s>>>(A);
-        rtd::k_wf_accum<<<grid_px, B, 0, s>>>(A);
-    }
-    rtd::k_wf_fold<<<grid_px, B, 0, s>>>(A);
-    return RT_OK;
-}
 
 }  // namespace
 
@@ -702,7 +554,11 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     int g = 1;
     while (g * g < f->spp) g++;
     if (f->spp < 1 || g * g != f->spp || g > 16) return arg_err(ctx, "rt_render: spp must be a square 1..256");
-    if (f->kernel < RT_KERNEL_AUTO || f->kernel > RT_KERNEL_WAVE) return arg_err(ctx, "rt_render: bad kernel");
+    if (f->kernel < RT_KERNEL_AUTO || f->kernel > RT_KERNEL_FAST) return arg_err(ctx, "rt_render: bad kernel");
+    if (f->variant < RT_VARIANT_DEFAULT || f->variant > RT_VARIANT_CHAIN4 || f->tune < 0 || f->tune > 1 ||
+        f->waves_cap < 0 || f->waves_cap > 8 || f->dealing < RT_DEAL_DEFAULT || f->dealing > RT_DEAL_ROW_MAJOR ||
+        f->regroup < 0 || f->regroup > 64)
+        return arg_err(ctx, "rt_render: bad launch configuration (variant / tune / waves_cap / dealing / regroup)");
     HIPC(hipSetDevice(ctx->device));
     const size_t pixels = (size_t)f->width * f->n_rows;  // per frame
     const size_t all_px = pixels * (size_t)n_frames;
@@ -723,7 +579,6 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     A.s.ref = dview(ctx->ref);
     A.s.acc = ctx->acc.nodes ? dview(ctx->acc) : A.s.ref;
     A.s.wide = rtd::DWide{ctx->wide_nodes, ctx->wide_tris, ctx->wide_orig};
-    if (const char* e = std::getenv("PRT_WIDE"); e && std::atoi(e) == 0) A.s.wide.nodes = nullptr;  // A/B knob
     A.s.shade = ctx->d_shade;
     A.s.mats = ctx->d_mats;
     A.s.lights = ctx->d_lights;
@@ -757,13 +612,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     A.work = ctx->d_work;
     A.tiles_x = (f->width + 7) / 8;
     A.n_tiles = A.tiles_x * ((f->n_rows + 7) / 8);
-    int kernel = f->kernel == RT_KERNEL_AUTO ? RT_KERNEL_FAST : f->kernel;
-    // the wavefront pipeline and k_wave render 1 spp; spp > 1 goes to the per-pixel path kernel
-    if ((kernel == RT_KERNEL_WAVEFRONT || kernel == RT_KERNEL_WAVE) && (f->spp > 1 || (out && out->bounce_hit)))
-        kernel = RT_KERNEL_FAST;  // spp > 1 and per-level hit dumps: the fused path kernels
-    if ((f->bounces > rtd::WF_MAXB || ctx->n_lights > 32 || rb > 1 || bgra) && kernel == RT_KERNEL_WAVEFRONT)
-        kernel = RT_KERNEL_FAST;  // (the wavefront pipeline's primary-ray stage takes single rows only and
-                                  // its fold stage writes f32 pixels only)
+    const int kernel = f->kernel == RT_KERNEL_AUTO ? RT_KERNEL_FAST : f->kernel;
     if (n_frames > 1 && kernel != RT_KERNEL_FAST) {  // one launch per frame, outputs at frame offsets
         for (int i = 0; i < n_frames; i++) {
             rt_outputs o{rgb ? rgb + 3 * pixels * i : nullptr, A.hit ? A.hit + pixels * i : nullptr,
@@ -816,8 +665,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         }
         A.cams = ctx->d_cams;
     }
-    A.refill_below = kernel == RT_KERNEL_WAVEFRONT ? 48 : 32;  // tuning knob, PRT_REFILL_BELOW overrides (0..64)
-    if (const char* e = std::getenv("PRT_REFILL_BELOW")) A.refill_below = std::max(0, std::min(64, std::atoi(e)));
+    A.regroup = f->regroup > 0 ? f->regroup : 16;
     const bool count = (ctx->flags & RT_FLAG_COUNTERS) != 0;
     dim3 grid((f->width + 15) / 16, (f->n_rows + 15) / 16);
     const int slot = (int)(ctx->launches % rt_ctx::NEV);
@@ -839,9 +687,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     // Tile dealing order of the persistent kernels: centre-out (default). The frame ends when the slowest
     // tile does (PRT_TILE_TRACE: 8x8 tiles range from 2 us to ~1.9 ms; expensive ones are deep reflection
     // chains, usually on the object in view); dealing from the centre starts them first (bench frame
-    // -7 %). PRT_TILE_ORDER=rows: row-major (A/B knob). One cached permutation per tile grid.
-    const char* order_env = std::getenv("PRT_TILE_ORDER");
-    const bool centre_out = kernel == RT_KERNEL_FAST && !(order_env && std::strcmp(order_env, "rows") == 0);
+    // -7 %). RT_DEAL_ROW_MAJOR: row-major. One cached permutation per tile grid.
+    const bool centre_out = kernel == RT_KERNEL_FAST && f->dealing != RT_DEAL_ROW_MAJOR;
     auto order_for = [&](int tx, int ty, const int*& out_ord) -> int {
         out_ord = nullptr;
         if (!centre_out) return RT_OK;
@@ -868,53 +715,42 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         return RT_OK;
     };
     if (int rc = order_for(A.tiles_x, A.n_tiles / A.tiles_x, A.tile_order)) return rc;
-    // XCD-aware dealing of k_persist: the centre-out order split into 8 spatial regions, region r drained
-    // first by the workgroups on XCD r (rtd::next_item), so each XCD's L2 holds the part of the scene its
-    // region's rays touch. PRT_XCD: 3 = 4 x 2 blocks of tiles, 1 = 8 bands of tile rows, 2 = 8 bands of
-    // tile columns, 0 = one global counter. Same-box, ms per frame: 16-frame batches of the full frame,
-    // dragon 1.060 / 0.938 (blocks) / 0.980 (rows) / 0.942 (columns), sportscar 0.599 / 0.504, car_boxed
-    // 1.067 / 1.041; a single frame 1.862 / 1.871 (blocks) / 1.732 (rows); an 8-GPU rank's rows, batched,
-    // 0.220 / 0.208 (blocks) / 0.202 (rows). Default: blocks for batches of the full frame, row bands
-    // otherwise. Device layout: 9 region offsets, then the concatenated regions' tiles.
-    const char* xcd_env = std::getenv("PRT_XCD");
+    // XCD-aware dealing of k_persist / k_chain: the centre-out order split into 8 spatial regions, region r
+    // drained first by the workgroups on XCD r (rtd::next_item), so each XCD's L2 holds the part of the scene
+    // its region's rays touch. rt_frame.dealing: BLOCKS = 4 x 2 blocks of tiles, ROWS = 8 bands of tile
+    // rows, COLUMNS = 8 bands of tile columns, GLOBAL = one counter. Same-box, ms per frame: 16-frame
+    // batches of the full frame, dragon 1.060 (global) / 0.938 (blocks) / 0.980 (rows) / 0.942 (columns),
+    // sportscar 0.599 / 0.504, car_boxed 1.067 / 1.041; a single frame 1.862 / 1.871 (blocks) / 1.732
+    // (rows); an 8-GPU rank's rows, batched, 0.220 / 0.208 (blocks) / 0.202 (rows). Default: blocks for
+    // batches of the full frame, row bands otherwise. Device layout: 9 region offsets, then the
+    // concatenated regions' tiles.
     const int* region_off = nullptr;
     const int* region_order = nullptr;
     const bool full_frame = f->row_offset == 0 && f->n_rows == f->height;
-    const int xcd_mode = xcd_env ? std::atoi(xcd_env) : (n_frames > 1 && full_frame ? 3 : 1);
+    const int xcd_mode = f->dealing == RT_DEAL_DEFAULT ? (n_frames > 1 && full_frame ? 3 : 1)
+                         : f->dealing == RT_DEAL_ROWS    ? 1
+                         : f->dealing == RT_DEAL_COLUMNS ? 2
+                         : f->dealing == RT_DEAL_BLOCKS  ? 3
+                                                         : 0;
     if (centre_out && xcd_mode >= 1 && xcd_mode <= 3) {
         const int tx = A.tiles_x, ty = A.n_tiles / A.tiles_x;
-        // order inside a region: centre-out (default) or Z-order (PRT_XCD_ORDER=z: consecutive tiles are
-        // neighbours; A/B: batches dragon -2 %, sportscar +2 %, car_boxed +1 %, a single frame +5 %)
-        const char* zo = std::getenv("PRT_XCD_ORDER");
-        const bool zorder = zo && zo[0] == 'z';
-        const long long key = ((long long)(xcd_mode + (zorder ? 4 : 0)) << 58) | ((long long)tx << 32) | (unsigned)ty;
+        const long long key = ((long long)xcd_mode << 58) | ((long long)tx << 32) | (unsigned)ty;
         auto it = ctx->orders.find(key);
         if (it == ctx->orders.end()) {
             const int n = tx * ty;
             std::vector<int> ord(n);
             for (int i = 0; i < n; i++) ord[i] = i;
             const float cx = 0.5f * tx, cy = 0.5f * ty;
-            auto morton = [](unsigned x, unsigned y) {
-                unsigned long long m = 0;
-                for (int i = 0; i < 16; i++)
-                    m |= (unsigned long long)((x >> i) & 1u) << (2 * i) | (unsigned long long)((y >> i) & 1u) << (2 * i + 1);
-                return m;
-            };
-            if (zorder)
-                std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
-                    return morton(a % tx, a / tx) < morton(b % tx, b / tx);
-                });
-            else
-                std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
-                    const float ax = a % tx + 0.5f - cx, ay = a / tx + 0.5f - cy;
-                    const float bx = b % tx + 0.5f - cx, by = b / tx + 0.5f - cy;
-                    return ax * ax + ay * ay < bx * bx + by * by;
-                });
+            std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+                const float ax = a % tx + 0.5f - cx, ay = a / tx + 0.5f - cy;
+                const float bx = b % tx + 0.5f - cx, by = b / tx + 0.5f - cy;
+                return ax * ax + ay * ay < bx * bx + by * by;
+            });
             std::vector<int> dev(9 + n);
             int at = 9;
             for (int r = 0; r < 8; r++) {
                 dev[r] = at;
-                for (int t : ord) {  // 1: 8 bands of tile rows, 2: 8 bands of tile columns, 3: 4 x 2 blocks
+                for (int t : ord) {
                     const int reg = xcd_mode == 1 ? (t / tx) * 8 / ty
                                     : xcd_mode == 2 ? (t % tx) * 8 / tx
                                                     : (t % tx) * 4 / tx + 4 * ((t / tx) * 2 / ty);
@@ -931,43 +767,43 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         region_off = it->second;
         region_order = it->second + 9;
     }
-    // RT_KERNEL_FAST has several launch configurations (`mode`, `cap` waves per SIMD of a persistent grid):
-    //   M_PERSIST  k_persist, one lane per pixel path, 8x8 tiles;
-    //   M_SPLIT    (1 spp) the split pipeline (rt_split.hpp): closest chains, shadow batches, resolve;
-    //   G = 2/4/8  k_coop (rt_coop.hpp): G lanes per ray, 64/G-pixel tiles — shorter chains per tile,
-    //              which is what a frame split over many GPUs (few tiles per wave) is bound by.
-    // Which is fastest depends on the scene and on the frame shape (same-box A/B): dragon
-    // wants k_persist at its full 3 waves/SIMD, car_boxed k_persist at 2 (-15 %: fewer incoherent
-    // reflection chains in flight thrash the caches less), sportscar (4 lights) the split pipeline at 2.
-    // Every configuration renders the same bits, so the context measures: the first frame of a
-    // (scene, frame shape) runs each candidate TUNE_REPS times (all into the same outputs), the next
-    // frame reads the timings and keeps the fastest. PRT_TUNE=0 (or forcing a configuration through
-    // PRT_SPLIT / PRT_PERSIST_CAP / PRT_SPLIT_OCC_A / PRT_COOP) disables it; PRT_TUNE_LOG=1 prints the timings.
-    enum { M_PERSIST = 0, M_SPLIT = 1, M_FAN = 3, M_PERSIST4 = 6 };  // 2, 4, 8: k_coop with G = mode
-    const char* split_env = std::getenv("PRT_SPLIT");
-    const char* cap_env = std::getenv("PRT_PERSIST_CAP");
-    const char* occa_env = std::getenv("PRT_SPLIT_OCC_A");
-    const char* coop_env = std::getenv("PRT_COOP");
-    const char* tune_env = std::getenv("PRT_TUNE");
+    // RT_KERNEL_FAST launch configurations (rt_frame.variant; every one renders the same bits):
+    //   PERSIST / PERSIST4  k_persist, one lane per pixel path, walks in lockstep, 8x8 tiles;
+    //   CHAIN / CHAIN4      k_chain (rt_chain.hpp), one lane per pixel path, each lane's walks back to back;
+    //   SPLIT               (1 spp, single frames) closest chains, shadow batches, resolve (rt_split.hpp);
+    //   COOP2/4/8           k_coop (rt_coop.hpp): G lanes per ray, 64/G-pixel tiles — shorter chains per tile,
+    //                       which is what a frame split over many GPUs (few tiles per wave) is bound by;
+    //   FAN                 k_fan (rt_fan.hpp): 1 + lights lanes per pixel.
+    // Default rule (measured): PERSIST4 for frame batches, PERSIST for single frames, SPLIT for
+    // single 1-spp frames of scenes with >= 3 lights. rt_frame.tune = 1 measures instead: the first frame of a (scene upload, frame shape) runs each
+    // candidate TUNE_REPS times (all into the same outputs), the next frame of that shape reads the timings
+    // and keeps the fastest; PRT_TUNE_LOG=1 prints them.
     const bool split_ok =
-        kernel == RT_KERNEL_FAST && f->spp == 1 && ctx->n_lights <= 32 && !A.tile_trace && n_frames == 1;
-    const bool coop_ok = kernel == RT_KERNEL_FAST && ctx->wide_n > 0;
-    const bool fan_ok = coop_ok && ctx->n_lights >= 1 && ctx->n_lights <= 7;
+        kernel == RT_KERNEL_FAST && f->spp == 1 && ctx->n_lights >= 1 && ctx->n_lights <= 32 && !A.tile_trace && n_frames == 1;
+    const bool wide_ok = kernel == RT_KERNEL_FAST && ctx->wide_n > 0;
+    const bool fan_ok = wide_ok && ctx->n_lights >= 1 && ctx->n_lights <= 7;
     const int fan_r = ctx->n_lights <= 1 ? 2 : ctx->n_lights <= 3 ? 4 : 8;  // lanes per pixel: 1 + lights
-    const char* fan_env = std::getenv("PRT_FAN");
-    int mode = split_ok && (split_env ? std::atoi(split_env) == 1 : ctx->n_lights >= 3) ? M_SPLIT : M_PERSIST;
-    if (mode == M_PERSIST && n_frames > 1) mode = M_PERSIST4;  // untuned batches: 4 waves/SIMD (-8 %)
-    if (coop_ok && coop_env && (std::atoi(coop_env) == 2 || std::atoi(coop_env) == 4 || std::atoi(coop_env) == 8))
-        mode = std::atoi(coop_env);
-    if (fan_ok && fan_env && std::atoi(fan_env) == 1) mode = M_FAN;
-    int cap = mode == M_SPLIT ? env_cap("PRT_SPLIT_OCC_A", 2) : env_cap("PRT_PERSIST_CAP", 8);
-    const bool tunable = kernel == RT_KERNEL_FAST && !A.tile_trace && !split_env && !cap_env && !occa_env &&
-                         !coop_env && !fan_env && !(tune_env && std::atoi(tune_env) == 0);
+    auto usable = [&](int v) {
+        if (v == RT_VARIANT_SPLIT) return split_ok;
+        if (v == RT_VARIANT_FAN) return fan_ok;
+        if (v >= RT_VARIANT_COOP2 && v <= RT_VARIANT_COOP8) return wide_ok;
+        if (v == RT_VARIANT_CHAIN || v == RT_VARIANT_CHAIN4) return wide_ok && !A.tile_trace;
+        return true;
+    };
+    int mode = f->variant;
+    if (mode == RT_VARIANT_DEFAULT)
+        mode = split_ok && ctx->n_lights >= 3 ? RT_VARIANT_SPLIT : n_frames > 1 ? RT_VARIANT_PERSIST4 : RT_VARIANT_PERSIST;
+    if (!usable(mode)) mode = RT_VARIANT_PERSIST;  // (no wide view, or a diagnostics trace)
+    int cap = f->waves_cap > 0 ? f->waves_cap : (mode == RT_VARIANT_SPLIT ? 2 : 0);
+    const bool tunable = kernel == RT_KERNEL_FAST && f->tune == 1 && f->variant == RT_VARIANT_DEFAULT && !A.tile_trace;
     rt_ctx::Tune* Tp = nullptr;
+    auto same_shape = [&](const rt_ctx::Tune& t) {
+        return t.scene == ctx->scene_gen && t.W == f->width && t.rows == f->n_rows && t.bounces == f->bounces &&
+               t.spp == f->spp && t.frames == n_frames && t.off == f->row_offset && t.stride == f->row_stride &&
+               t.block == rb && t.shift == fs && t.dealing == f->dealing && t.cap_req == f->waves_cap;
+    };
     for (auto& t : ctx->tunes)
-        if (t.scene == ctx->scene_gen && t.W == f->width && t.rows == f->n_rows && t.bounces == f->bounces &&
-            t.spp == f->spp && t.frames == n_frames)
-            Tp = &t;
+        if (same_shape(t)) Tp = &t;
     if (!Tp && tunable) {
         if (ctx->tunes.size() >= 16) {  // bounded: drop the oldest decision (its events with it)
             for (int i = 0; i < rt_ctx::TUNE_MAX * rt_ctx::TUNE_REPS; i++) {
@@ -978,33 +814,33 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         }
         ctx->tunes.emplace_back();
         Tp = &ctx->tunes.back();
+        rt_ctx::Tune& T = *Tp;
+        T.scene = ctx->scene_gen;
+        T.W = f->width;
+        T.rows = f->n_rows;
+        T.bounces = f->bounces;
+        T.spp = f->spp;
+        T.frames = n_frames;
+        T.off = f->row_offset;
+        T.stride = f->row_stride;
+        T.block = rb;
+        T.shift = fs;
+        T.dealing = f->dealing;
+        T.cap_req = f->waves_cap;
+        // candidates (COOP8 is 3x slower than COOP4 everywhere measured: a variant, not a candidate)
+        const int md[9] = {RT_VARIANT_CHAIN4, RT_VARIANT_CHAIN, RT_VARIANT_PERSIST, RT_VARIANT_PERSIST4,
+                           RT_VARIANT_PERSIST, RT_VARIANT_SPLIT, RT_VARIANT_COOP4, RT_VARIANT_COOP2, RT_VARIANT_FAN};
+        const int cp[9] = {0, 0, 0, 0, 2, 2, 0, 0, 0};
+        for (int i = 0; i < 9 && T.n < rt_ctx::TUNE_MAX; i++)
+            if (usable(md[i])) {
+                T.mode[T.n] = md[i];
+                T.cap[T.n] = f->waves_cap > 0 ? f->waves_cap : cp[i];
+                T.n++;
+            }
     }
-    rt_ctx::Tune dummy;
-    rt_ctx::Tune& T = Tp ? *Tp : dummy;
     bool trial = false;
     if (tunable) {
-        if (T.scene != ctx->scene_gen || T.W != f->width || T.rows != f->n_rows || T.bounces != f->bounces ||
-            T.spp != f->spp || T.frames != n_frames) {
-            T.frames = n_frames;
-            T.scene = ctx->scene_gen;
-            T.W = f->width;
-            T.rows = f->n_rows;
-            T.bounces = f->bounces;
-            T.spp = f->spp;
-            T.n = 0;
-            T.choice = -1;
-            T.pending = false;
-            // (coop8 is 3x slower than coop4 everywhere measured: a knob, PRT_COOP=8, not a candidate)
-            const int md[7] = {M_PERSIST, M_PERSIST4, M_PERSIST, M_SPLIT, 4, 2, M_FAN};
-            const int cp[7] = {8, 8, 2, 2, 8, 8, 8};
-            for (int i = 0; i < 7 && T.n < rt_ctx::TUNE_MAX; i++)
-                if ((md[i] != M_SPLIT || (split_ok && ctx->n_lights >= 1)) && (md[i] != M_FAN || fan_ok) &&
-                    (md[i] < 2 || md[i] == M_FAN || coop_ok)) {
-                    T.mode[T.n] = md[i];
-                    T.cap[T.n] = cp[i];
-                    T.n++;
-                }
-        }
+        rt_ctx::Tune& T = *Tp;
         if (T.pending) {
             HIPC(hipEventSynchronize(T.e1[T.n * rt_ctx::TUNE_REPS - 1]));
             int best = 0;
@@ -1021,16 +857,10 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             T.choice = best;
             T.pending = false;
             if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1) {
+                static const char* names[] = {"default", "persist", "persist4", "split", "coop2",
+                                              "coop4",   "coop8",   "fan",      "chain", "chain4"};
                 std::fprintf(stderr, "[prt tune] %dx%d b%d spp%d f%d:", T.W, T.rows, T.bounces, T.spp, T.frames);
-                for (int c = 0; c < T.n; c++) {
-                    const int m = T.mode[c];
-                    std::fprintf(stderr, " %s%s/%d %.3f ms",
-                                 m == M_PERSIST ? "persist" : m == M_PERSIST4 ? "persist-occ4" : m == M_SPLIT ? "split"
-                                 : m == M_FAN ? "fan" : "coop",
-                                 m == M_FAN ? std::to_string(fan_r).c_str()
-                                 : (m >= 2 && m != M_PERSIST4) ? std::to_string(m).c_str() : "",
-                                 T.cap[c], T.ms[c]);
-                }
+                for (int c = 0; c < T.n; c++) std::fprintf(stderr, " %s/%d %.3f ms", names[T.mode[c]], T.cap[c], T.ms[c]);
                 std::fprintf(stderr, " -> %d\n", best);
             }
         } else if (T.choice < 0) {
@@ -1041,40 +871,45 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             cap = T.cap[T.choice];
         }
     }
-    // one frame of configuration (mode, cap); d_work holds the persistent grids' work counters, and the
+    // one frame of configuration (variant, cap); d_work holds the persistent grids' work counters, and the
     // ray counters restart with every launch (rt_get_stats reports the frame, not the trial launches)
     auto dispatch = [&](int md, int cp) -> int {
         if (!ctx->batch_sum)  // a per-frame loop of a batch keeps adding to the batch's counters
             HIPC(hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT, ctx->stream));
         HIPC(hipMemsetAsync(ctx->d_work, 0, 1024, ctx->stream));
-        if (md == M_SPLIT) return f->bounces <= 4 ? launch_split<4>(ctx, A, count, cp) : launch_split<8>(ctx, A, count, cp);
-        if (md >= 2 && md != M_PERSIST4) {
+        if (kernel == RT_KERNEL_STRICT) {
+            auto k = count ? rtd::k_tiles<4, true, true> : rtd::k_tiles<4, true, false>;
+            if (f->bounces > 4) k = count ? rtd::k_tiles<8, true, true> : rtd::k_tiles<8, true, false>;
+            k<<<grid, rtd::BLOCK, 0, ctx->stream>>>(A);
+            return RT_OK;
+        }
+        if (md == RT_VARIANT_SPLIT) return f->bounces <= 4 ? launch_split<4>(ctx, A, count, cp) : launch_split<8>(ctx, A, count, cp);
+        if (md == RT_VARIANT_FAN || (md >= RT_VARIANT_COOP2 && md <= RT_VARIANT_COOP8)) {
             rtd::KArgs B = A;
-            const int gr = md == M_FAN ? fan_r : md;  // lanes per pixel
+            const int gr = md == RT_VARIANT_FAN ? fan_r : md == RT_VARIANT_COOP2 ? 2 : md == RT_VARIANT_COOP4 ? 4 : 8;
             const int tw = gr == 2 ? 8 : 4, th = gr == 8 ? 2 : 4;  // rtd::GTile<gr>
             B.tiles_x = (f->width + tw - 1) / tw;
             const int ty = (f->n_rows + th - 1) / th;
             B.n_tiles = B.tiles_x * ty;
             if (int rc = order_for(B.tiles_x, ty, B.tile_order)) return rc;
             trace_n = (size_t)B.n_tiles;
-            if (md == M_FAN)
+            if (md == RT_VARIANT_FAN)
                 return f->bounces <= 4 ? launch_fan<4>(B, gr, count, ctx->device, ctx->stream, cp)
                                        : launch_fan<8>(B, gr, count, ctx->device, ctx->stream, cp);
-            return f->bounces <= 4 ? launch_coop<4>(B, md, count, ctx->device, ctx->stream, cp)
-                                   : launch_coop<8>(B, md, count, ctx->device, ctx->stream, cp);
+            return f->bounces <= 4 ? launch_coop<4>(B, gr, count, ctx->device, ctx->stream, cp)
+                                   : launch_coop<8>(B, gr, count, ctx->device, ctx->stream, cp);
         }
-        if (kernel == RT_KERNEL_WAVEFRONT) return launch_wf(ctx, A, count);
-        const int occ = md == M_PERSIST4 ? 4 : 3;
         rtd::KArgs P = A;
-        if (region_off && kernel == RT_KERNEL_FAST) {
+        if (region_off) {
             P.region_off = region_off;
             P.tile_order = region_order;
         }
-        if (f->bounces <= 4) launch<4>(P, kernel, count, grid, ctx->device, ctx->stream, cp, occ);
-        else launch<8>(P, kernel, count, grid, ctx->device, ctx->stream, cp, occ);
+        if (f->bounces <= 4) launch_paths<4>(P, md, count, ctx->device, ctx->stream, cp);
+        else launch_paths<8>(P, md, count, ctx->device, ctx->stream, cp);
         return RT_OK;
     };
     if (trial) {
+        rt_ctx::Tune& T = *Tp;
         const int nt = T.n * rt_ctx::TUNE_REPS;
         for (int i = 0; i < nt; i++) {
             if (!T.e0[i]) HIPC(hipEventCreate(&T.e0[i]));
@@ -1215,7 +1050,7 @@ int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count, int cap_a) {
     auto kb = count ? rtd::k_split_shadow<true> : rtd::k_split_shadow<false>;
     // persistent grids; a block is one wave per SIMD, so the cap is waves per SIMD
     const int ga = std::max(1, std::min(resident(ka, ctx->device, cap_a), (A.n_tiles + 3) / 4));
-    const int gb = std::max(1, resident(kb, ctx->device, env_cap("PRT_SPLIT_OCC_B", 8)));
+    const int gb = std::max(1, resident(kb, ctx->device, 8));
     ka<<<ga, rtd::BLOCK, 0, s>>>(A);
     kb<<<gb, rtd::BLOCK, 0, s>>>(A);
     rtd::k_split_resolve<MAXB><<<(int)((A.nslots + 255) / 256), 256, 0, s>>>(A);
@@ -1287,7 +1122,9 @@ extern "C" int rt_gather(rt_ctx* const* ctxs, int n, int root) {
                                                          c->last_stride, c->last_rows, c->last_block);
         HIPC(hipGetLastError());
     }
-    HIPC(hipEventRecord(ctx->ev1, ctx->stream));
+    // the gather's completion has its own event: ev0s / ev1s stay the render launches' (rt_kernel_times)
+    if (!ctx->gather_ev) HIPC(hipEventCreateWithFlags(&ctx->gather_ev, hipEventDisableTiming));
+    HIPC(hipEventRecord(ctx->gather_ev, ctx->stream));
     ctx->last_rgb = ctx->d_full;
     ctx->last_hit = all_hit ? ctx->d_full_hit : nullptr;
     ctx->last_pixels = px;
@@ -1362,7 +1199,7 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     free_scene(ctx);
-    if (ctx->wf_mem) (void)hipFree(ctx->wf_mem);
+    if (ctx->gather_ev) (void)hipEventDestroy(ctx->gather_ev);
     if (ctx->d_rgb_own) (void)hipFree(ctx->d_rgb_own);
     if (ctx->d_cams) (void)hipFree(ctx->d_cams);
     if (ctx->d_pathbuf) (void)hipFree(ctx->d_pathbuf);

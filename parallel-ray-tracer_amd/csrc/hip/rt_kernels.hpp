@@ -966,85 +966,3 @@ void k_persist(KArgs A) {
 }
 
 }  // namespace rtd
-
-namespace rtd {
-
-// Path regeneration: persistent waves, one lane = one pixel path as in k_persist, but a lane whose path
-// ends takes the next pixel at once, from a wave-local pool filled one 8x8 tile at a time (one atomic
-// per tile), instead of idling until the whole tile's deepest path is done. Primary and reflection rays
-// run the same closest-hit code, so lanes at different bounce levels still traverse in lockstep.
-// Per-pixel arithmetic is path_step/fold_path's: results are k_persist's bit for bit. spp == 1 only.
-template <int MAXB, bool COUNT>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(3))) void k_regen(KArgs A) {
-    __shared__ int lds[STACK * BLOCK];
-    int* stk = lds + threadIdx.x;
-    const unsigned lane = threadIdx.x & 63u;
-    Ctr c = {};
-    int px = -1, pk = 0, it = 0, L = 0, hit0 = -1;
-    bool tail = false;
-    float t0 = FMAX;
-    v3 o = mk(0.0f, 0.0f, 0.0f), d = o;
-    v3 cols[MAXB];
-    int mats[MAXB];
-#pragma unroll
-    for (int q = 0; q < MAXB; q++) {
-        cols[q] = o;
-        mats[q] = 0;
-    }
-    unsigned tile = 0, nxt = 64;  // wave-uniform pixel pool: the 64 slots of `tile`, next unassigned slot
-    bool drained = false;
-    for (;;) {
-        // ---- give every idle lane the next pixel of the pool
-        for (;;) {
-            const unsigned long long need = __ballot(px < 0);
-            if (!need || drained) break;
-            if (nxt >= 64u) {
-                unsigned t = 0;
-                if (lane == 0) t = atomicAdd(A.work, 1u);
-                t = __shfl(t, 0, 64);
-                if (t >= (unsigned)A.n_tiles) {
-                    drained = true;
-                    break;
-                }
-                tile = t;
-                nxt = 0;
-            }
-            const unsigned take = min((unsigned)__popcll(need), 64u - nxt);
-            const unsigned rank = (unsigned)__popcll(need & ((1ull << lane) - 1ull));
-            if (px < 0 && rank < take) {
-                const unsigned q = nxt + rank;
-                const int x = (int)(tile % (unsigned)A.tiles_x) * 8 + (int)(q & 7u);
-                const int k = (int)(tile / (unsigned)A.tiles_x) * 8 + (int)(q >> 3);
-                if (x < A.W && k < A.n_rows) {  // slots outside the frame stay idle and refill again
-                    px = x;
-                    pk = k;
-                    it = 0;
-                    if (A.bounce_hit)
-                        for (int i = 0; i < A.bounces; i++) A.bounce_hit[((size_t)k * A.W + x) * A.bounces + i] = -2;
-                    o = mk(A.pos[0], A.pos[1], A.pos[2]);
-                    d = primary_dir(A, (float)x, (float)image_row(A, k));
-                }
-            }
-            nxt += take;
-        }
-        if (!__ballot(px >= 0)) break;
-        // ---- one bounce level of every busy lane's path
-        if (px >= 0) {
-            if (path_step<MAXB, false, COUNT, true>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0, A.bounce_hit,
-                                                    pk * A.W + px, stk, c)) {
-                const v3 col = clamp01(fold_path<MAXB>(A.s, cols, mats, L, tail));
-                const size_t w = (size_t)pk * A.W + px;
-                c.pix++;
-                store_px(A.rgb, A.bgra, w, col);
-                if (A.hit) A.hit[w] = hit0;
-                if (A.t) A.t[w] = t0;
-                px = -1;
-            } else {
-                ++it;
-            }
-        }
-    }
-    flush<COUNT>(c, A.counters);
-}
-
-}  // namespace rtd

@@ -262,13 +262,10 @@ extern "C" int rth_wbvh_build(const rt_bvh_node* bvh, int n_nodes, const int* tr
     bool bad = false;
     const int root = w.make(bvh, n_nodes, 0, 0, bad);
     if (bad || root < 0) return RT_E_ARG;
-    // collapse policy: SAH-optimal (default) or greedy largest-area (PRT_WIDE_COLLAPSE=greedy, A/B);
-    // PRT_WIDE_CNODE: cost of a wide-node visit in triangle tests (default 2: the best of 2/3/4 in the
-    // measured sweep — dragon -3.5 % vs 4, car_boxed even)
-    const char* ce = std::getenv("PRT_WIDE_COLLAPSE");
-    const bool sah = !(ce && std::strcmp(ce, "greedy") == 0);
-    const char* cn = std::getenv("PRT_WIDE_CNODE");
-    if (sah) w.sah_costs(cn ? (float)std::atof(cn) : 2.0f);
+    // collapse policy: SAH-optimal, a wide-node visit priced at 2 triangle tests (the best of 2 / 3 / 4 in the
+    // measured sweep — dragon -3.5 % vs 4, car_boxed even; the greedy largest-area collapse: +1.6 % / +3 %;
+    // DESIGN.md §3)
+    w.sah_costs(2.0f);
 
     // breadth-first: interior children of a wide node get consecutive indices
     struct Item {
@@ -285,10 +282,10 @@ extern "C" int rth_wbvh_build(const rt_bvh_node* bvh, int n_nodes, const int* tr
         const BNode& B = w.bn[it.b];
         std::vector<int> kids;
         std::vector<char> kid_leaf;
-        if (B.l < 0 || (sah && w.as_leaf[it.b])) {
+        if (B.l < 0 || w.as_leaf[it.b]) {
             kids.push_back(it.b);  // a leaf root
             kid_leaf.push_back(1);
-        } else if (sah) {  // the cost-optimal distribution of this node's 8 slots
+        } else {  // the cost-optimal distribution of this node's 8 slots
             std::vector<std::pair<int, bool>> c2;
             w.collect(B.l, w.split[it.b][WIDTH], c2);
             w.collect(B.r, WIDTH - w.split[it.b][WIDTH], c2);
@@ -296,22 +293,6 @@ extern "C" int rth_wbvh_build(const rt_bvh_node* bvh, int n_nodes, const int* tr
                 kids.push_back(pr.first);
                 kid_leaf.push_back(pr.second ? 1 : 0);
             }
-        } else {  // greedy: open the largest-area interior child until WIDTH
-            kids = {B.l, B.r};
-            while ((int)kids.size() < WIDTH) {
-                int best = -1;
-                float ba = -1.0f;
-                for (int c = 0; c < (int)kids.size(); c++)
-                    if (w.bn[kids[c]].l >= 0 && area(w.bn[kids[c]].b) > ba) {
-                        ba = area(w.bn[kids[c]].b);
-                        best = c;
-                    }
-                if (best < 0) break;
-                const int o = kids[best];
-                kids[best] = w.bn[o].l;
-                kids.push_back(w.bn[o].r);
-            }
-            for (int c : kids) kid_leaf.push_back(w.bn[c].l < 0 ? 1 : 0);
         }
         const int k = (int)kids.size();
         max_kids = std::max(max_kids, k);

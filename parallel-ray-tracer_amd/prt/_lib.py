@@ -58,7 +58,8 @@ class Frame(ctypes.Structure):
     _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("row_offset", ctypes.c_int),
                 ("row_stride", ctypes.c_int), ("n_rows", ctypes.c_int), ("bounces", ctypes.c_int),
                 ("spp", ctypes.c_int), ("kernel", ctypes.c_int), ("row_block", ctypes.c_int),
-                ("frame_shift", ctypes.c_int)]
+                ("frame_shift", ctypes.c_int), ("variant", ctypes.c_int), ("tune", ctypes.c_int),
+                ("waves_cap", ctypes.c_int), ("dealing", ctypes.c_int), ("regroup", ctypes.c_int)]
 
 
 STAT_FIELDS = ["primary", "reflection", "shadow", "shadow_skipped", "hits", "ch_inner", "ch_leaf",
@@ -97,15 +98,13 @@ def host():
         L.rth_triangles_random.argtypes = [ctypes.c_size_t, P(Rng), P(P(Triangle))]
         L.rth_bvh_build.argtypes = [P(Triangle), ctypes.c_size_t, ctypes.c_int, P(Rng), P(P(BvhNode)),
                                     P(ctypes.c_int), P(P(ctypes.c_int)), P(BvhStats)]
-        if hasattr(L, "rth_wbvh_build"):  # absent from older builds (A/B via PRT_LIB_DIR)
-            L.rth_wbvh_build.argtypes = [P(BvhNode), ctypes.c_int, P(ctypes.c_int), P(Triangle), ctypes.c_int,
-                                         ctypes.c_float, P(P(ctypes.c_uint32)), P(P(ctypes.c_int)), P(WbvhInfo)]
-        if hasattr(L, "rth_triangles_load_cached"):
-            L.rth_triangles_load_cached.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
-                                                    P(P(Triangle)), P(ctypes.c_size_t), P(ctypes.c_int)]
-            L.rth_bvh_build_cached.argtypes = [P(Triangle), ctypes.c_size_t, ctypes.c_int, P(Rng), ctypes.c_char_p,
-                                               P(P(BvhNode)), P(ctypes.c_int), P(P(ctypes.c_int)), P(BvhStats),
-                                               P(ctypes.c_int)]
+        L.rth_wbvh_build.argtypes = [P(BvhNode), ctypes.c_int, P(ctypes.c_int), P(Triangle), ctypes.c_int,
+                                     ctypes.c_float, P(P(ctypes.c_uint32)), P(P(ctypes.c_int)), P(WbvhInfo)]
+        L.rth_triangles_load_cached.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                                P(P(Triangle)), P(ctypes.c_size_t), P(ctypes.c_int)]
+        L.rth_bvh_build_cached.argtypes = [P(Triangle), ctypes.c_size_t, ctypes.c_int, P(Rng), ctypes.c_char_p,
+                                           P(P(BvhNode)), P(ctypes.c_int), P(P(ctypes.c_int)), P(BvhStats),
+                                           P(ctypes.c_int)]
         L.rth_camera.argtypes = [ctypes.c_int, ctypes.c_int, P(Camera)]
         L.rth_bmp_write.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
         L.rth_bmp_encode.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]

@@ -12,7 +12,12 @@ from ._lib import BvhNode, Camera, Frame, Light, Opts, SceneDesc, Stats, Triangl
 
 P = ctypes.POINTER
 
-KERNELS = {"auto": 0, "strict": 1, "fast": 2, "wavefront": 3, "wave": 4}
+KERNELS = {"auto": 0, "strict": 1, "fast": 2}
+# rt_frame.variant (launch configurations of the fast kernel, include/rt_hip.h); a variant name is also
+# accepted as `kernel` (kernel="coop4" == kernel="fast", variant="coop4")
+VARIANTS = {"default": 0, "persist": 1, "persist4": 2, "split": 3, "coop2": 4, "coop4": 5, "coop8": 6, "fan": 7,
+            "chain": 8, "chain4": 9}
+DEALING = {"default": 0, "global": 1, "rows": 2, "columns": 3, "blocks": 4, "row_major": 5}
 ACCEL = {"auto": 0, "reference": 1}
 FLAG_COUNTERS = 1
 
@@ -48,12 +53,25 @@ def gather(renderers, root=0):
     r._last = (W, H)
 
 
-def _ptr(x):
-    """device pointer of a torch tensor / int / None"""
+def _ptr(x, what="", n=0, dtypes=(), device=None):
+    """device pointer of a torch tensor / raw int pointer / None. A tensor must be contiguous, of one of
+    `dtypes`, on `device` and hold at least n elements (the kernel writes n of them); raw pointers are the
+    caller's responsibility."""
     if x is None:
         return None
     if isinstance(x, int):
         return x
+    import torch
+    if not isinstance(x, torch.Tensor):
+        raise RtError(f"{what}: expected a torch tensor, an int pointer or None, got {type(x).__name__}")
+    if not x.is_contiguous():
+        raise RtError(f"{what}: tensor is not contiguous")
+    if dtypes and x.dtype not in dtypes:
+        raise RtError(f"{what}: dtype {x.dtype}, expected {' or '.join(str(d) for d in dtypes)}")
+    if x.numel() < n:
+        raise RtError(f"{what}: {x.numel()} elements, the frame needs {n}")
+    if x.device.type != "cuda" or (device is not None and x.device.index != device):
+        raise RtError(f"{what}: tensor on {x.device}, expected cuda:{device}")
     return x.data_ptr()
 
 
@@ -99,27 +117,45 @@ class Renderer:
         self.scene = scene
         return self
 
-    def render(self, cam, width, height, rows=None, bounces=4, spp=1, kernel="auto", rgb=None, hit=None, t=None,
-               bounce_hit=None, bgra=None):
-        """render_frame(): asynchronous. rows = (offset, stride, n[, block]) (rt_frame; prt.dist) or None for
-        the full frame.
-        rgb / hit / t / bounce_hit ([n, W, bounces] int32) / bgra ([n, W] int32: the BMP-quantised pixel in
-        top-down rows, rt_outputs.bgra): optional device tensors (torch) or raw pointers."""
+    def _frame(self, width, height, rows, bounces, spp, kernel, variant, tune, waves_cap, dealing, regroup):
         ro, rs, nr, rb, sh = _rows(rows, height)
-        f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel), rb, sh)
-        out = Outputs(_ptr(rgb), _ptr(hit), _ptr(t), _ptr(bounce_hit), _ptr(bgra))
+        if isinstance(kernel, str) and kernel in VARIANTS:
+            kernel, variant = "fast", kernel
+        v = VARIANTS.get(variant, variant) if variant is not None else 0
+        return Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel), rb, sh, v,
+                     1 if tune else 0, waves_cap, DEALING.get(dealing, dealing), regroup), nr
+
+    def _outputs(self, nf, nr, width, bounces, rgb, hit, t, bounce_hit, bgra):
+        import torch
+        n = nf * nr * width
+        i32 = (torch.int32,)
+        return Outputs(_ptr(rgb, "rgb", 3 * n, (torch.float32,), self.device),
+                       _ptr(hit, "hit", n, i32, self.device), _ptr(t, "t", n, (torch.float32,), self.device),
+                       _ptr(bounce_hit, "bounce_hit", n * bounces, i32, self.device),
+                       _ptr(bgra, "bgra", n, (torch.int32, getattr(torch, "uint32", torch.int32)), self.device))
+
+    def render(self, cam, width, height, rows=None, bounces=4, spp=1, kernel="auto", rgb=None, hit=None, t=None,
+               bounce_hit=None, bgra=None, variant=None, tune=False, waves_cap=0, dealing="default", regroup=0):
+        """render_frame(): asynchronous. rows = (offset, stride, n[, block[, frame_shift]]) (rt_frame; prt.dist)
+        or None for the full frame.
+        rgb / hit / t / bounce_hit ([n, W, bounces] int32) / bgra ([n, W] int32: the BMP-quantised pixel in
+        top-down rows, rt_outputs.bgra): optional device tensors (torch: checked for size, dtype, device and
+        contiguity) or raw pointers. variant / tune / waves_cap / dealing / regroup: the fast kernel's launch
+        configuration (rt_frame; VARIANTS, DEALING)."""
+        f, nr = self._frame(width, height, rows, bounces, spp, kernel, variant, tune, waves_cap, dealing, regroup)
+        out = self._outputs(1, nr, width, bounces, rgb, hit, t, bounce_hit, bgra)
         self._chk(_L.rt_render(self._ctx, ctypes.byref(cam), ctypes.byref(f), ctypes.byref(out)), "rt_render")
         self._last = (width, nr)
         self._size = (width, height)
         self._frames = 1
 
     def render_frames(self, cams, width, height, rows=None, bounces=4, spp=1, kernel="auto", rgb=None, hit=None,
-                      t=None, bounce_hit=None, bgra=None):
+                      t=None, bounce_hit=None, bgra=None, variant=None, tune=False, waves_cap=0, dealing="default",
+                      regroup=0):
         """rt_render_frames(): a batch of len(cams) frames of one shape (one persistent launch on the fast
         kernel); outputs [n_frames, n_rows, W, ...]. Asynchronous."""
-        ro, rs, nr, rb, sh = _rows(rows, height)
-        f = Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel), rb, sh)
-        out = Outputs(_ptr(rgb), _ptr(hit), _ptr(t), _ptr(bounce_hit), _ptr(bgra))
+        f, nr = self._frame(width, height, rows, bounces, spp, kernel, variant, tune, waves_cap, dealing, regroup)
+        out = self._outputs(len(cams), nr, width, bounces, rgb, hit, t, bounce_hit, bgra)
         arr = (Camera * len(cams))(*cams)
         self._chk(_L.rt_render_frames(self._ctx, arr, len(cams), ctypes.byref(f), ctypes.byref(out)),
                   "rt_render_frames")

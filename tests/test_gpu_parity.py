@@ -16,25 +16,18 @@ from prt import host
 
 pytestmark = pytest.mark.gpu
 RGB_TOL = 1e-5
-# every kernel the C-ABI exposes: STRICT, FAST (production), and the A/B variants WAVEFRONT and WAVE;
-# "coopG" = FAST forced to its group-cooperative configuration (k_coop, G lanes per ray, PRT_COOP=G);
-# "fan" = FAST forced to the shadow fan-out (k_fan, 1 + lights lanes per pixel, PRT_FAN=1)
-KERNELS = ["strict", "fast", "wavefront", "wave", "coop2", "coop4", "coop8", "fan"]
-FORCE = {"coop2": ("PRT_COOP", "2"), "coop4": ("PRT_COOP", "4"), "coop8": ("PRT_COOP", "8"), "fan": ("PRT_FAN", "1")}
+# every kernel and launch configuration the C-ABI exposes (rt_frame.kernel / rt_frame.variant): STRICT, FAST
+# with its default rule ("fast"), and each variant forced: k_persist at 4 waves/SIMD ("persist4"), k_chain
+# ("chain", "chain4": each lane's walks back to back), k_coop ("coopG": G lanes per ray), k_fan ("fan":
+# 1 + lights lanes per pixel). The split pipeline has its own tests.
+KERNELS = ["strict", "fast", "persist4", "chain", "chain4", "coop2", "coop4", "coop8", "fan"]
 
 
 def select(kernel):
-    """kernel name -> rt_kernel name, with PRT_COOP / PRT_FAN set (or cleared) for the library"""
-    unforce()
-    if kernel in FORCE:
-        os.environ[FORCE[kernel][0]] = FORCE[kernel][1]
-        return "fast"
+    """test kernel name -> the `kernel` argument of prt.device (a variant name selects RT_KERNEL_FAST + it)"""
     return kernel
 
 
-def unforce():
-    for k in ("PRT_COOP", "PRT_FAN"):
-        os.environ.pop(k, None)
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 G = json.load(open(os.path.join(GOLD, "golden.json")))
 
@@ -66,7 +59,6 @@ def render(dev, scene, W, H, kernel, rows=None, spp=1, bounces=4, counters=False
     r.render(host.camera(W, H), W, H, rows=rows, bounces=bounces, spp=spp, kernel=select(kernel), rgb=rgb, hit=hit,
              t=t)
     r.sync()
-    unforce()
     st = r.stats()
     out = {"rgb": rgb.cpu().numpy(), "hit": hit.cpu().numpy(), "t": t.cpu().numpy(), "stats": st}
     r.close()
@@ -184,7 +176,7 @@ def test_strict_traversal_counters_match_reference_order(dev, scenes):
         assert st[k] == c[k], k
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan"])
+@pytest.mark.parametrize("kernel", ["fast", "chain4", "coop4", "fan"])
 @pytest.mark.parametrize("spp", [4, 16])
 def test_spp_matches_oracle(dev, scenes, spp, kernel):
     from tests.oracle_bind import OracleScene
@@ -195,6 +187,47 @@ def test_spp_matches_oracle(dev, scenes, spp, kernel):
     out = render(dev, scenes["car_only"], 64, 36, kernel, spp=spp, counters=True)
     assert same_bits(out["rgb"], ref)
     assert out["stats"]["primary"] == 64 * 36 * spp
+
+
+_SPP64 = {}
+
+
+@pytest.mark.parametrize("kernel", ["fast", "persist4", "chain4", "coop4", "fan"])
+def test_car_boxed_64spp_matches_oracle(dev, scenes, kernel):
+    """BASELINE config 5 (car_boxed 3840x2160, 64 spp, multi-bounce): the reference has one corner ray per
+    pixel (cpu/src/main.c:228-239); SURVEY §8d defines spp = s x s stratified sub-pixel samples, mean of the
+    clamped samples (orc_render_spp restates it). Bit-exact against the oracle on the full 160x90 frame and
+    on every 97th row of the 4K frame, with primary rays = 64 x pixels and the same reflection / shadow
+    counts; spp = 1 of the same renderer is the reference's own fixture."""
+    import torch
+    from tests.oracle_bind import OracleScene
+    from tests.scenes import scene_paths
+    if "oracle" not in _SPP64:
+        o = OracleScene.load(*scene_paths("car_boxed"))
+        o.build_bvh(3)
+        _SPP64["oracle"] = o
+        _SPP64["small"] = o.render_spp(160, 90, 64)
+        n4k = (2160 + 96) // 97
+        _SPP64["4k"] = o.render_spp(3840, 2160, 64, rows=(0, 97, n4k))
+    small, c_small = _SPP64["small"]
+    out = render(dev, scenes["car_boxed"], 160, 90, kernel, spp=64, counters=True)
+    assert same_bits(out["rgb"], small), np.abs(out["rgb"] - small).max()
+    st = out["stats"]
+    assert st["primary"] == 64 * 160 * 90 == c_small["primary"]
+    for k in ("reflection", "shadow", "shadow_skipped"):
+        assert st[k] == c_small[k], k
+    big, c_big = _SPP64["4k"]
+    n4k = (2160 + 96) // 97
+    out = render(dev, scenes["car_boxed"], 3840, 2160, kernel, rows=(0, 97, n4k), spp=64, counters=True)
+    assert same_bits(out["rgb"], big[0:2160:97]), np.abs(out["rgb"] - big[0:2160:97]).max()
+    st = out["stats"]
+    assert st["primary"] == 64 * 3840 * n4k == c_big["primary"]
+    for k in ("reflection", "shadow", "shadow_skipped"):
+        assert st[k] == c_big[k], k
+    one = render(dev, scenes["car_boxed"], 160, 90, kernel, spp=1)
+    ref = np.load(os.path.join(GOLD, "car_boxed_160x90_strict.npz"))
+    assert same_bits(one["rgb"], ref["rgb"])
+    np.testing.assert_array_equal(one["hit"], ref["hit"])
 
 
 @pytest.mark.parametrize("name", ["dragon", "sportscar", "two_cars"])
@@ -269,7 +302,6 @@ def test_bounce_hits_match_oracle(dev, scenes, kernel):
     rgb = torch.empty((72, 128, 3), dtype=torch.float32, device="cuda")
     r.render(host.camera(128, 72), 128, 72, kernel=select(kernel), rgb=rgb, bounce_hit=bh)
     r.sync()
-    unforce()
     np.testing.assert_array_equal(bh.cpu().numpy(), ref["bounce_hit"])
     assert same_bits(rgb.cpu().numpy(), ref["rgb"])
     r.close()
@@ -346,16 +378,14 @@ def test_cli_drop_in_writes_the_reference_bmp(tmp_path):
 
 
 @pytest.mark.parametrize("name", ["car_boxed", "sportscar", "dragon"])
-def test_split_pipeline_equals_persistent_kernel(dev, name, monkeypatch):
-    """RT_KERNEL_FAST has two implementations (k_persist; closest/shadow/resolve split, chosen for >= 3
-    lights): both forced, on 1-, 4- and 2-light scenes, bit-exact to each other and to the fixtures,
-    with identical ray counts"""
+def test_split_pipeline_equals_persistent_kernel(dev, name):
+    """RT_VARIANT_SPLIT (closest/shadow/resolve, the default for >= 3 lights) against RT_VARIANT_PERSIST, on
+    1-, 4- and 2-light scenes: bit-exact to each other and to the fixtures, with identical ray counts"""
     s = host.Scene.named(name).build_bvh(3)
     outs = {}
-    for v in ("0", "1"):
-        monkeypatch.setenv("PRT_SPLIT", v)
-        outs[v] = render(dev, s, 96, 54, "fast", counters=True)
-    a, b = outs["0"], outs["1"]
+    for v in ("persist", "split"):
+        outs[v] = render(dev, s, 96, 54, v, counters=True)
+    a, b = outs["persist"], outs["split"]
     np.testing.assert_array_equal(a["hit"], b["hit"])
     assert same_bits(a["t"], b["t"]) and same_bits(a["rgb"], b["rgb"])
     for k in ("primary", "reflection", "shadow", "shadow_skipped", "hits", "pixels"):
@@ -366,17 +396,15 @@ def test_split_pipeline_equals_persistent_kernel(dev, name, monkeypatch):
         assert same_bits(b["rgb"], ref["rgb"])
 
 
-@pytest.mark.parametrize("name,n_cand", [("sportscar", 7), ("car_boxed", 7), ("dragon", 7)])
+@pytest.mark.parametrize("name,n_cand", [("sportscar", 9), ("car_boxed", 9), ("dragon", 9)])
 def test_autotuned_frames_equal_forced_configuration(dev, name, n_cand, monkeypatch, capfd):
-    """rt_render's launch autotuner (rt_hip.hip, RT_KERNEL_FAST): the trial frame (every candidate, each
+    """rt_render's launch autotuner (rt_frame.tune = 1, rt_hip.hip): the trial frame (every candidate, each
     TUNE_REPS times, into the same outputs) and the frames after the decision are bit-exact to a forced
     k_persist frame; the decision is logged once, over all candidates"""
     import torch
     s = host.Scene.named(name).build_bvh(3)
     W, H = 96, 54
-    monkeypatch.setenv("PRT_SPLIT", "0")
-    ref = render(dev, s, W, H, "fast")
-    monkeypatch.delenv("PRT_SPLIT")
+    ref = render(dev, s, W, H, "persist")
     monkeypatch.setenv("PRT_TUNE_LOG", "1")
     r = dev.Renderer(0)
     r.upload(s)
@@ -384,7 +412,7 @@ def test_autotuned_frames_equal_forced_configuration(dev, name, n_cand, monkeypa
         hit = torch.full((H, W), -7, dtype=torch.int32, device="cuda")
         t = torch.zeros((H, W), dtype=torch.float32, device="cuda")
         rgb = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
-        r.render(host.camera(W, H), W, H, kernel="fast", rgb=rgb, hit=hit, t=t)
+        r.render(host.camera(W, H), W, H, kernel="fast", rgb=rgb, hit=hit, t=t, tune=True)
         r.sync()
         np.testing.assert_array_equal(hit.cpu().numpy(), ref["hit"])
         assert same_bits(t.cpu().numpy(), ref["t"]) and same_bits(rgb.cpu().numpy(), ref["rgb"]), frame
@@ -405,7 +433,7 @@ def moved_camera(W, H, dx, dz):
     return c
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "strict"])
+@pytest.mark.parametrize("kernel", ["fast", "chain4", "coop4", "fan", "strict"])
 @pytest.mark.parametrize("name", ["car_boxed", "dragon"])
 def test_frame_batch_equals_single_frames(dev, name, kernel):
     """rt_render_frames: a batch of frames (different cameras, one persistent launch on the fast paths)
@@ -434,7 +462,6 @@ def test_frame_batch_equals_single_frames(dev, name, kernel):
         r.render_frames(cams, W, H, rows=rows, kernel=select(kernel), rgb=rgb, hit=hit)
         r.sync()
         st = r.stats()
-        unforce()
         r.close()
         for i, (srgb, shit, _) in enumerate(singles):
             assert same_bits(rgb[i].cpu().numpy(), srgb), (kernel, rows, i)
@@ -447,33 +474,46 @@ def test_frame_batch_equals_single_frames(dev, name, kernel):
             assert same_bits(rgb[0].cpu().numpy(), ref["rgb"])
 
 
-@pytest.mark.parametrize("xcd", ["0", "1", "2"])
-def test_xcd_aware_dealing_renders_the_same_frames(dev, xcd, monkeypatch):
-    """k_persist's tile dealing (rt_hip.hip, rtd::next_item): one global counter (PRT_XCD=0), 8 row
-    bands, 8 column bands, and the default 4 x 2 blocks drained first by their own XCD — the same bits
+@pytest.mark.parametrize("kernel", ["fast", "chain4"])
+@pytest.mark.parametrize("dealing", ["global", "rows", "columns", "row_major"])
+def test_xcd_aware_dealing_renders_the_same_frames(dev, dealing, kernel):
+    """the persistent kernels' tile dealing (rt_frame.dealing, rtd::next_item): one global counter, 8 row
+    bands, 8 column bands, row-major, against 4 x 2 blocks drained first by their own XCD — the same bits
     for a frame, a row subset and a frame batch, and the same ray counts"""
     import torch
     s = host.Scene.named("dragon").build_bvh(3)
     W, H = 200, 120
     outs = {}
-    for v in ("3", xcd):
-        monkeypatch.setenv("PRT_XCD", v)
-        monkeypatch.setenv("PRT_TUNE", "0")
-        a = render(dev, s, W, H, "fast", counters=True)
-        b = render(dev, s, W, H, "fast", rows=(8, 24, 40, 8))
+    for v in ("blocks", dealing):
+        a = render_dealt(dev, s, W, H, kernel, v, counters=True)
+        b = render_dealt(dev, s, W, H, kernel, v, rows=(8, 24, 40, 8))
         r = dev.Renderer(0)
         r.upload(s)
         rgb = torch.empty((3, H, W, 3), dtype=torch.float32, device="cuda")
-        r.render_frames([host.camera(W, H)] * 3, W, H, kernel="fast", rgb=rgb)
+        r.render_frames([host.camera(W, H)] * 3, W, H, kernel=kernel, rgb=rgb, dealing=v)
         r.sync()
         outs[v] = (a, b, rgb.cpu().numpy())
         r.close()
-    (a0, b0, f0), (a1, b1, f1) = outs["3"], outs[xcd]
+    (a0, b0, f0), (a1, b1, f1) = outs["blocks"], outs[dealing]
     assert same_bits(a0["rgb"], a1["rgb"]) and same_bits(b0["rgb"], b1["rgb"]) and same_bits(f0, f1)
     np.testing.assert_array_equal(a0["hit"], a1["hit"])
     assert a0["stats"]["rays"] == a1["stats"]["rays"]
     for i in range(3):
         assert same_bits(f1[i], a0["rgb"])
+
+
+def render_dealt(dev, scene, W, H, kernel, dealing, rows=None, counters=False):
+    import torch
+    r = dev.Renderer(0, counters=counters)
+    r.upload(scene)
+    nr = rows[2] if rows else H
+    rgb = torch.empty((nr, W, 3), dtype=torch.float32, device="cuda")
+    hit = torch.empty((nr, W), dtype=torch.int32, device="cuda")
+    r.render(host.camera(W, H), W, H, rows=rows, kernel=kernel, rgb=rgb, hit=hit, dealing=dealing)
+    r.sync()
+    out = {"rgb": rgb.cpu().numpy(), "hit": hit.cpu().numpy(), "stats": r.stats()}
+    r.close()
+    return out
 
 
 def quantise(rgb):
@@ -483,14 +523,11 @@ def quantise(rgb):
 
 
 @pytest.mark.parametrize("kernel", KERNELS + ["split"])
-def test_bgra_output_is_the_bmp_writers_quantisation(dev, scenes, kernel, monkeypatch):
+def test_bgra_output_is_the_bmp_writers_quantisation(dev, scenes, kernel):
     """rt_outputs.bgra (the kernels quantise as they store): equal to vec_to_bgra of the same
     frame's f32 pixels, with or without an rgb output, for a frame, a row-block subset and a frame batch;
     the full frame's rows bottom-up are bmp_write_file's pixel bytes of the reference fixture"""
     import torch
-    if kernel == "split":  # the fast kernel's closest/shadow/resolve pipeline
-        monkeypatch.setenv("PRT_SPLIT", "1")
-        kernel = "fast"
     W, H = 160, 90
     s = scenes["car_boxed"]
     ref = np.load(os.path.join(GOLD, "car_boxed_160x90_strict.npz"))
@@ -516,47 +553,40 @@ def test_bgra_output_is_the_bmp_writers_quantisation(dev, scenes, kernel, monkey
         r.render_frames([host.camera(W, H), moved_camera(W, H, 0.25, 0.0)], W, H, rows=rows,
                         kernel=select(kernel), bgra=batch)
         r.sync()
-        unforce()
         np.testing.assert_array_equal(batch[0].cpu().numpy().view(np.uint32), q)
         assert not np.array_equal(batch[1].cpu().numpy(), batch[0].cpu().numpy())
         r.close()
 
 
 @pytest.mark.parametrize("name", ["dragon", "car_boxed"])
-def test_path_buffer_placements_render_the_same_frames(dev, name, monkeypatch):
-    """k_persist at 4 waves per SIMD keeps each path level in a path buffer: in LDS after the wide stack
-    (default when 4 workgroups fit) or in global memory (PRT_PB_LDS=0); both equal the 3-wave register
-    kernel bit for bit — a frame, a frame batch, 4 spp — with the same ray counts"""
+def test_path_level_placements_render_the_same_frames(dev, name):
+    """path levels in registers (k_persist, 3 waves/SIMD), in the LDS path buffer (k_persist at 4 waves/SIMD,
+    k_chain): the same bits for a frame, a frame batch with a moved camera and 4 spp, with the same ray counts"""
     import torch
     s = host.Scene.named(name).build_bvh(3)
     W, H = 200, 120
     outs = {}
-    monkeypatch.setenv("PRT_TUNE", "0")
-    for v in ("occ3", "lds", "global"):
-        monkeypatch.delenv("PRT_PERSIST_OCC", raising=False)
-        if v != "occ3":
-            monkeypatch.setenv("PRT_PERSIST_OCC", "4")
-            monkeypatch.setenv("PRT_PB_LDS", "1" if v == "lds" else "0")
-        a = render(dev, s, W, H, "fast", counters=True)
-        b = render(dev, s, W, H, "fast", spp=4)
+    for v in ("persist", "persist4", "chain", "chain4"):
+        a = render(dev, s, W, H, v, counters=True)
+        b = render(dev, s, W, H, v, spp=4)
         r = dev.Renderer(0)
         r.upload(s)
         rgb = torch.empty((3, H, W, 3), dtype=torch.float32, device="cuda")
         r.render_frames([host.camera(W, H), moved_camera(W, H, 0.25, 0.0), host.camera(W, H)], W, H,
-                        kernel="fast", rgb=rgb)
+                        kernel=v, rgb=rgb)
         r.sync()
         outs[v] = (a, b, rgb.cpu().numpy())
         r.close()
-    a0, b0, f0 = outs["occ3"]
+    a0, b0, f0 = outs["persist"]
     assert same_bits(f0[0], a0["rgb"]) and same_bits(f0[2], a0["rgb"])
-    for v in ("lds", "global"):
+    for v in ("persist4", "chain", "chain4"):
         a1, b1, f1 = outs[v]
         assert same_bits(a0["rgb"], a1["rgb"]) and same_bits(b0["rgb"], b1["rgb"]) and same_bits(f0, f1), v
         np.testing.assert_array_equal(a0["hit"], a1["hit"])
         assert a0["stats"]["rays"] == a1["stats"]["rays"], v
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan"])
+@pytest.mark.parametrize("kernel", ["fast", "chain4", "coop4", "fan"])
 def test_rotated_row_blocks_cover_every_frame(dev, kernel):
     """rt_frame.frame_shift: frame f of rank q renders block residue (q + f) % N (prt.dist rotate), rows
     past the image skipped — over the N ranks every frame of the batch is rendered exactly once, bit for
@@ -596,7 +626,6 @@ def test_rotated_row_blocks_cover_every_frame(dev, kernel):
                 if y < H:
                     got[f, y] = out[f, k]
                     seen[f, y] += 1
-    unforce()
     assert (seen == 1).all()
     for f in range(len(cams)):
         assert same_bits(got[f], full[f]), (kernel, f)

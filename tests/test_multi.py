@@ -86,10 +86,11 @@ def _batch_worker(rank, world, port, W, H, out_path, block, fmt="rgb", rotate=Fa
         for f in range(2):  # compact frames as rt_render_frames writes them (rotated: rt_frame.frame_shift)
             o_f = (off + f * sh) % stride if sh else off
             t = g.target(b)[f]
+            fr = _tagged(full, b, f)  # every frame distinct: a frame unpacked into the wrong slot fails
             for k in range(n):
                 y = o_f + (k // B) * stride + k % B
                 if y < H:
-                    t[k] = torch.from_numpy(full[y])
+                    t[k] = torch.from_numpy(fr[y])
                 else:
                     t[k] = -1  # rows past the image (rotation): never unpacked
         g.start(b)
@@ -100,6 +101,13 @@ def _batch_worker(rank, world, port, W, H, out_path, block, fmt="rgb", rotate=Fa
         np.save(out_path, torch.stack(out).numpy())
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _tagged(frame, b, f):
+    """frame f of ping-pong block b with a per-frame tag XOR-ed into every word's low bits (block 1's frame 1
+    untagged: its BMP is checked against the reference writer)"""
+    tag = [[1, 2], [3, 0]][b][f]
+    return (np.ascontiguousarray(frame).view(np.int32) ^ np.int32(tag)).view(frame.dtype)
 
 
 @pytest.mark.parametrize("world,H,block,fmt,rotate", [(2, 36, 1, "rgb", False), (3, 37, 1, "rgb", False),
@@ -129,7 +137,7 @@ def test_batched_pingpong_gather_equals_single_frame(tmp_path, world, H, block, 
     assert got.shape == (2, 2, H, W, 1 if fmt == "bgra8" else 3)
     for b in range(2):
         for f in range(2):
-            assert np.array_equal(got[b, f].view(np.int32), ref.view(np.int32)), (b, f)
+            assert np.array_equal(got[b, f].view(np.int32), _tagged(ref, b, f).view(np.int32)), (b, f)
 
 
 @pytest.mark.parametrize("world", [2, 3])

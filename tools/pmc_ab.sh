@@ -1,6 +1,6 @@
 #!/bin/bash
-# PMC passes (separate runs, no trace domains) over tools/ab.py variants on one frame shape, for the
-# per-kernel medians of tools/pmc_summary.py. usage: tools/pmc_ab.sh <tag> <ab.py args...>
+# PMC passes (separate runs, no trace domains) over tools/ab_variants.py variants on one frame shape, for
+# the per-kernel medians of tools/pmc_summary.py. usage: tools/pmc_ab.sh <tag> <ab_variants.py args...>
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 tag=$1; shift
@@ -8,7 +8,7 @@ out=gpurun_out/pmc_$tag
 mkdir -p $out
 pass() {  # name counters...
     local name=$1; shift
-    timeout -s KILL 120 rocprofv3 --pmc "$@" -d $out/$name -o run --output-format csv -- python3 tools/ab.py --rounds 1 --frames 3 "${ARGS[@]}" > $out/$name.log 2>&1
+    timeout -s KILL 120 rocprofv3 --pmc "$@" -d $out/$name -o run --output-format csv -- python3 tools/ab_variants.py --rounds 1 --frames 3 "${ARGS[@]}" > $out/$name.log 2>&1
     local rc=$?
     echo "=== $name rc=$rc"
     [ $rc -eq 0 ] || { tail -5 $out/$name.log; exit $rc; }

@@ -53,7 +53,7 @@ def main():
     last = np.array([e[w == x].max() for x in waves])
     busy = np.array([dur[w == x].sum() for x in waves])
     # k_coop<4> and k_fan<4> (2-3 lights) deal 4x4 tiles
-    tw, tht = (4, 4) if os.environ.get("PRT_COOP") == "4" or os.environ.get("PRT_FAN") == "1" else (8, 8)
+    tw, tht = (8, 8)  # (PRT_TILE_TRACE records the 8x8 tiles of k_persist, the configuration it forces)
     tx = (a.W + tw - 1) // tw
     rows = dur.reshape(-1, tx).mean(1) if len(dur) % tx == 0 else None
     res = {
