@@ -60,6 +60,16 @@ def cpu_model():
     return "unknown"
 
 
+def avx512_host():
+    """the AVX-512 subsets -march=x86-64-v4 needs are on this host (and the v4 reference build exists)"""
+    try:
+        flags = next(l for l in open("/proc/cpuinfo") if l.startswith("flags")).split()
+    except (OSError, StopIteration):
+        return False
+    need = ("avx512f", "avx512bw", "avx512cd", "avx512dq", "avx512vl")
+    return all(f in flags for f in need) and os.access(os.path.join(ROOT, "oracle", "_ref", "rt_ref_v4"), os.X_OK)
+
+
 def usable_cpus():
     """CPUs this process can actually use: its affinity set, capped by the cgroup v2 CPU quota (the GPU box
     shares a 256-CPU host: 16 CPUs of quota per GPU)"""
@@ -90,7 +100,8 @@ def cpu_baseline(scene_files, W, H, gpu_rays_for_rows, args, threads):
     on this host, pthreads with the reference's atomic row scheduler; falls back to the C restatement
     built the same way (kind "port") when the prebuilt reference binary is absent."""
     stride = args.cpu_row_stride
-    ref = os.path.join(ROOT, "oracle", "_ref", "rt_ref_fast")
+    v4 = avx512_host()
+    ref = os.path.join(ROOT, "oracle", "_ref", "rt_ref_v4" if v4 else "rt_ref_fast")
     obj, mtl, lts = scene_files
     if os.path.exists(ref) and os.access(ref, os.X_OK):
         kind = "reference"
@@ -129,9 +140,11 @@ def cpu_baseline(scene_files, W, H, gpu_rays_for_rows, args, threads):
                      f"median of {reps} frames, {threads} pthreads, reference atomic row scheduler, "
                      f"heuristic-3 BVH (build untimed)",
            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
-           "build": "cpu/src/*.c with the reference makefile's -O3 -ffast-math -flto, but -march=x86-64-v3 instead "
-                    "of -march=native: the binary is built in the build container and must run on any box "
-                    "(oracle/Makefile); AVX2 + FMA, the same vector ISA the reference's hot loop uses"}
+           "build": ("cpu/src/*.c with the reference makefile's -O3 -ffast-math -flto; -march=native (cpu/makefile:14) "
+                     "is not available for a binary built in the build container (no reference sources on the GPU "
+                     "box), so " + ("-march=x86-64-v4 -mtune=znver3 (AVX-512, what this host supports; gcc 11 "
+                                    "knows no znver4/5)" if v4 else "-march=x86-64-v3 (AVX2 + FMA; no AVX-512 here)")
+                     + " (oracle/Makefile)") if kind == "reference" else "oracle/port/oracle.c, -O3 -ffast-math"}
     # the same at 1 thread, on a ~5 s sample (every stride1-th row, one frame)
     if threads > 1 and not args.no_single_thread:
         frame_1t = res["median_ms"] / 1e3 * stride * threads
@@ -228,8 +241,11 @@ def main():
         rr_.upload(scene, accel=args.accel)
     cam = host.camera(W, H)
     K = args.steps
-    F = max(1, min(args.frames, K))
-    plan = [F] * (K // F) + ([K % F] if K % F else [])  # launches covering exactly K frames
+    # launches covering exactly K frames, as few as --frames allows and of (nearly) equal size: K = 20 at 16
+    # frames per launch is 10 + 10, not 16 + 4 (a 4-frame launch is tail-bound: 1.3 vs 0.93 ms per frame)
+    n_launch = -(-K // max(1, min(args.frames, K)))
+    plan = [K // n_launch + (1 if i < K % n_launch else 0) for i in range(n_launch)]
+    F = plan[0]
     # rows: 8-row blocks dealt cyclically to the ranks (an 8x8 tile of a rank's rows is an 8x8 tile of the
     # image; costs average out over the blocks), gathered to rank 0 with one RCCL collective per batch
     # (prt/dist.py, tested with gloo in tests/test_multi.py); two ping-pong blocks so a batch's gather

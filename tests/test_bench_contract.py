@@ -1,6 +1,6 @@
 """bench.py's output contract on the GPU, on a small frame: one JSON line with every key the task's
 contract names, the metric string of BASELINE.json, value = rays per frame / ms per step, the
-roofline's frac = achieved / peak, a plan that covers --steps exactly (6 frames in batches of 4: 4 + 2),
+roofline's frac = achieved / peak, a plan that covers --steps exactly (6 frames in batches of at most 4: 3 + 3),
 and rays per frame equal to the oracle's count for the same frame (the reference's definition:
 primary + traced reflection + traced shadow rays)."""
 import json
@@ -47,7 +47,7 @@ def test_bench_prints_the_contract_line(output, tmp_path):
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
     assert rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"], rel=1e-9) and rf["achieved"] > 0
-    assert rf["frames_per_launch"] == 4
+    assert rf["frames_per_launch"] == 3
     ref = oracle_frame(W, H)
     c = ref["counters"]
     assert rays == c["primary"] + c["reflection"] + c["shadow"]
