@@ -50,6 +50,20 @@ def alg_bytes(st, pixels, n_lights, px_bytes=12):
     return nodes + 48 * tri + (84 + 32 * n_lights) * st["hits"] + px_bytes * pixels
 
 
+def data_note(name, n_tris, is_standin):
+    if name.startswith("random"):
+        return (f"synthetic: the reference's random-triangle mode (cpu/src/main.c:115-131, srand(1)), {n_tris} "
+                "triangles in [-5, 5]^3, no lights")
+    if name in ("dragon", "dragon871k") and is_standin(name):
+        return ("synthetic stand-in mesh: the reference snapshot has no assets/dragon/triangles.obj "
+                "(.MISSING_LARGE_BLOBS); prt/scenes.py generates a Cornell room + torus-knot tube "
+                f"({n_tris} triangles) with the real dragon .mtl and lights.obj")
+    if is_standin(name):
+        return (f"synthetic stand-in mesh ({n_tris} triangles, prt/scenes.py) with the real {name} .mtl and "
+                "lights.obj: the snapshot has no mesh for this scene (.MISSING_LARGE_BLOBS)")
+    return "reference asset"
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -58,6 +72,12 @@ def cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def parse_count(txt):
+    """'1m' -> 1000000, '200k' -> 200000, '5000' -> 5000"""
+    mul = {"k": 1000, "m": 1000000}.get(txt[-1:].lower(), 1)
+    return int(txt[:-1] if mul > 1 else txt) * mul
 
 
 def avx512_host():
@@ -227,8 +247,13 @@ def main():
     from prt.scenes import is_standin, scene_paths
 
     W, H = args.width, args.height
-    files = scene_paths(args.scene)
-    scene = host.Scene.load(*files).build_bvh(args.bvh)
+    if args.scene.startswith("random"):  # random-triangle mode (main.c:115-131): random<N>, e.g. random1m, random200k
+        n_rand = parse_count(args.scene[len("random"):] or "10k")
+        files = (f"random:{n_rand}", "-", "-")
+        scene = host.Scene.random(n_rand).build_bvh(args.bvh)
+    else:
+        files = scene_paths(args.scene)
+        scene = host.Scene.load(*files).build_bvh(args.bvh)
     stream = torch.cuda.current_stream().cuda_stream
     # N > 1: two contexts on two streams, launches alternating: a launch's tail (its longest reflection
     # chains) overlaps the next launch's work (tools/rank_rows.py --streams 2: 8-GPU rank rows 0.191 ->
@@ -381,9 +406,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": ("synthetic stand-in mesh: the reference snapshot has no assets/dragon/triangles.obj "
-                     "(.MISSING_LARGE_BLOBS); prt/scenes.py generates a Cornell room + 98,304-tri knot with the "
-                     "real dragon .mtl and lights.obj" if is_standin(args.scene) else "reference asset"),
+            "data": data_note(args.scene, scene.n_triangles, is_standin),
             "config": {"workload": f"{args.scene} {W}x{H}, {args.spp} spp, {args.bounces} bounces, one fused "
                                    f"traversal+intersect+shade persistent launch per batch of {F} frames, "
                                    f"output {args.output}",

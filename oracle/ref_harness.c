@@ -230,10 +230,11 @@ int main(int argc, char** argv) {
     }
     if (!strcmp(cmd, "time")) {
         if (argc != 11) {
-            fprintf(stderr, "time <obj> <mtl> <lights> <W> <H> <threads> <row_offset> <row_stride> <reps>\n");
+            fprintf(stderr, "time <obj|random:N> <mtl> <lights> <W> <H> <threads> <row_offset> <row_stride> <reps>\n");
             return 2;
         }
-        load_scene(argv[2], argv[3], argv[4]);
+        if (!strncmp(argv[2], "random:", 7)) random_scene(atoi(argv[2] + 7)); /* random mode, main.c:115-131 */
+        else load_scene(argv[2], argv[3], argv[4]);
         W = atoi(argv[5]); H = atoi(argv[6]);
         int threads = atoi(argv[7]);
         row_offset = atoi(argv[8]);

@@ -10,8 +10,14 @@ scenes in assets/*.tar.gz and stores:
   golden.json                      md5 of full-resolution frames and of the BVH dumps, plus the
                                    SURVEY §8c values they must equal
 
+  stress (round 2): the high-triangle-count workloads -- the sportscar stand-in (514k-triangle car, the
+  real sportscar .mtl), dragon871k (Stanford-dragon triangle count) and random mode at 1M triangles
+  (main.c:115-131) -- at 96x54 (full arrays), 320x180 (md5), and for the 1080p frames of dragon,
+  dragon871k and sportscar every 97th pixel, the full frame's md5 and the reference's ray counts.
+
 Frame binary layout (ref_harness.c): int32 hit[N] | f32 t[N] | f32 rgb[3N], row-major idx = y*W + x.
 Only needed in the build container (where /root/reference exists); the fixtures are committed.
+usage: make_golden.py [all | cars | standin | stress ...]  (sections update golden.json in place)
 """
 import hashlib
 import json
@@ -44,9 +50,79 @@ def frame(path, W, H):
     return raw, hit, t, rgb
 
 
-def main():
-    out = {"generator": "tests/golden/make_golden.py", "frames": {}, "bvh": {}}
+def counts(scene_files, W, H, tmp):
+    """the reference's own ray counts (rt_ref_count: linker-wrapped traversal calls)"""
+    p = os.path.join(tmp, "c.bin")
+    r = subprocess.run([os.path.join(REF, "rt_ref_count"), "render", *scene_files, str(W), str(H),
+                        str(os.cpu_count() or 8), p], check=True, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                       text=True)
+    line = [l for l in r.stderr.splitlines() if l.startswith("COUNTS")][-1]
+    kv = dict(x.split("=") for x in line.split()[1:])
+    closest = int(kv["trav"]) - W * H
+    return {"closest": closest, "shadow": int(kv["light"]), "total": closest + int(kv["light"])}
+
+
+def standin(out, tmp, names):
+    out.setdefault("standin", {})
+    for scene in names:
+        obj, mtl, lts = scene_paths(scene)
+        ent = {"obj_md5": hashlib.md5(open(obj, "rb").read()).hexdigest()}
+        for (W, H) in ((96, 54), (320, 180)):
+            p = os.path.join(tmp, f"{scene}_{W}x{H}.bin")
+            run("rt_ref_strict", "render", obj, mtl, lts, W, H, os.cpu_count() or 8, p)
+            raw, hit, t, rgb = frame(p, W, H)
+            ent[f"{W}x{H}_md5"] = hashlib.md5(raw).hexdigest()
+            if W == 96:
+                np.savez_compressed(os.path.join(HERE, f"{scene}_{W}x{H}_strict.npz"), hit=hit, t=t, rgb=rgb)
+        p = os.path.join(tmp, f"{scene}.bvh")
+        run("rt_ref_strict", "bvh", obj, mtl, p)
+        raw = open(p, "rb").read()
+        ent["bvh_h3_md5"] = hashlib.md5(raw).hexdigest()
+        ent["bvh_h3_nodes"] = int(np.frombuffer(raw[:4], np.int32)[0])
+        out["standin"][scene] = ent
+
+
+def stress(out, tmp):
+    standin(out, tmp, ("sportscar", "dragon871k"))
+    out.setdefault("rays", {})
+    for scene in ("dragon", "dragon871k", "sportscar"):
+        W, H = 1920, 1080
+        p = os.path.join(tmp, f"{scene}_1080p.bin")
+        run("rt_ref_strict", "render", *scene_paths(scene), W, H, os.cpu_count() or 8, p)
+        raw, hit, t, rgb = frame(p, W, H)
+        out["standin"][scene]["1920x1080_md5"] = hashlib.md5(raw).hexdigest()
+        idx = np.arange(0, W * H, 97)
+        np.savez_compressed(os.path.join(HERE, f"{scene}_1080p_strict_sample.npz"), idx=idx,
+                            hit=hit.reshape(-1)[idx], t=t.reshape(-1)[idx], rgb=rgb.reshape(-1, 3)[idx])
+        os.remove(p)
+        out["rays"][f"{scene}_{W}x{H}"] = counts(scene_paths(scene), W, H, tmp)
+    # random-triangle mode at 1M triangles (SURVEY §8d's BVH stress): primary rays only (kr = 0, no lights)
+    p = os.path.join(tmp, "random1m.bin")
+    run("rt_ref_strict", "random", 1000000, 96, 54, os.cpu_count() or 8, p)
+    raw, hit, t, rgb = frame(p, 96, 54)
+    np.savez_compressed(os.path.join(HERE, "random1m_96x54_strict.npz"), hit=hit, t=t, rgb=rgb)
+    out["frames"]["random1m_96x54_strict"] = {"md5": hashlib.md5(raw).hexdigest(), "W": 96, "H": 54}
+    p = os.path.join(tmp, "random1m.bvh")
+    run("rt_ref_strict", "bvhrand", 1000000, p)
+    raw = open(p, "rb").read()
+    out["bvh"]["random1m_h3"] = {"md5": hashlib.md5(raw).hexdigest(), "nodes": int(np.frombuffer(raw[:4], np.int32)[0])}
+
+
+def main(sections):
+    gpath = os.path.join(HERE, "golden.json")
+    out = json.load(open(gpath)) if os.path.exists(gpath) and "all" not in sections else {}
+    out.setdefault("generator", "tests/golden/make_golden.py")
+    out.setdefault("frames", {})
+    out.setdefault("bvh", {})
     tmp = tempfile.mkdtemp()
+    if "stress" in sections:
+        stress(out, tmp)
+    if "standin" in sections or "all" in sections:
+        standin(out, tmp, ("dragon", "sportscar", "two_cars"))
+    if "cars" not in sections and "all" not in sections:
+        with open(gpath, "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
+        return
     for scene in ("car_boxed", "car_only"):
         obj, mtl, lts = scene_paths(scene)
         for flav, binary in (("strict", "rt_ref_strict"), ("fast", "rt_ref_fast")):
@@ -81,36 +157,11 @@ def main():
     raw = open(p, "rb").read()
     out["bvh"]["random10k_h3"] = {"md5": hashlib.md5(raw).hexdigest(),
                                   "nodes": int(np.frombuffer(raw[:4], np.int32)[0])}
-    # stand-in scenes (meshes generated by prt/scenes.py; the reference renders them as-is)
-    out["standin"] = {}
-    for scene in ("dragon", "sportscar", "two_cars"):
-        obj, mtl, lts = scene_paths(scene)
-        ent = {"obj_md5": hashlib.md5(open(obj, "rb").read()).hexdigest()}
-        for (W, H) in ((96, 54), (320, 180)):
-            p = os.path.join(tmp, f"{scene}_{W}x{H}.bin")
-            run("rt_ref_strict", "render", obj, mtl, lts, W, H, os.cpu_count() or 8, p)
-            raw, hit, t, rgb = frame(p, W, H)
-            ent[f"{W}x{H}_md5"] = hashlib.md5(raw).hexdigest()
-            if W == 96:
-                np.savez_compressed(os.path.join(HERE, f"{scene}_{W}x{H}_strict.npz"), hit=hit, t=t, rgb=rgb)
-        p = os.path.join(tmp, f"{scene}.bvh")
-        run("rt_ref_strict", "bvh", obj, mtl, p)
-        raw = open(p, "rb").read()
-        ent["bvh_h3_md5"] = hashlib.md5(raw).hexdigest()
-        ent["bvh_h3_nodes"] = int(np.frombuffer(raw[:4], np.int32)[0])
-        out["standin"][scene] = ent
     # ray counts from the reference itself (rt_ref_count: linker-wrapped traversal calls)
-    out["rays"] = {}
+    out.setdefault("rays", {})
     for scene in ("car_boxed", "car_only"):
         for (W, H) in ((160, 90), (1920, 1080)):
-            p = os.path.join(tmp, "c.bin")
-            r = subprocess.run([os.path.join(REF, "rt_ref_count"), "render", *scene_paths(scene), str(W), str(H),
-                                "8", p], check=True, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
-            line = [l for l in r.stderr.splitlines() if l.startswith("COUNTS")][-1]
-            kv = dict(x.split("=") for x in line.split()[1:])
-            closest = int(kv["trav"]) - W * H
-            out["rays"][f"{scene}_{W}x{H}"] = {"closest": closest, "shadow": int(kv["light"]),
-                                                "total": closest + int(kv["light"])}
+            out["rays"][f"{scene}_{W}x{H}"] = counts(scene_paths(scene), W, H, tmp)
     # values SURVEY §8c / Appendix A recorded independently during the survey
     out["survey"] = {
         "car_boxed_1920x1080_strict": "6caa907524126a25bf7bdce0610a6586",
@@ -129,4 +180,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or ["all"])

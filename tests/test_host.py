@@ -80,7 +80,7 @@ def test_bvh_h6_matches_oracle():
     np.testing.assert_array_equal(s.tri_idx, idx)
 
 
-@pytest.mark.parametrize("scene", ["dragon", "two_cars"])
+@pytest.mark.parametrize("scene", ["dragon", "two_cars", "sportscar", "dragon871k"])
 def test_bvh_h3_standins_match_reference(scene):
     """multi-material scenes exercise the reference's axis-3 read (bvh.c:229-231) as laid out by O-strict"""
     s = host.Scene.named(scene).build_bvh(3)
@@ -94,6 +94,13 @@ def test_bvh_random_mode_matches_reference():
     assert hashlib.md5(raw).hexdigest() == G["bvh"]["random10k_h3"]["md5"]
     o = OracleScene.random(10000)
     assert s.triangles.tobytes() == o.triangles_bytes()
+
+
+def test_bvh_random_mode_one_million_matches_reference():
+    """random mode at 1M triangles (SURVEY §8d's BVH stress): the heuristic-3 tree is the reference's"""
+    s = host.Scene.random(1000000).build_bvh(3)
+    raw = np.int32(len(s.nodes)).tobytes() + s.nodes.tobytes() + s.tri_idx.astype(np.int32).tobytes()
+    assert hashlib.md5(raw).hexdigest() == G["bvh"]["random1m_h3"]["md5"]
 
 
 def _check_tree(nodes, idx, tris):
