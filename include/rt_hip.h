@@ -181,13 +181,41 @@ int rt_sync(rt_ctx* ctx, float* kernel_ms);
 /* per-launch kernel times (HIP events recorded on the context stream around each kernel) of the last
  * n launches (n <= 64), oldest first; synchronises; returns the number written or < 0 */
 int rt_kernel_times(rt_ctx* ctx, float* ms, int n);
-/* Multi-GPU in one process (the CLI's --gpus N): gathers the last frames of n contexts into ctxs[root]'s
- * device frame. Every context must have rendered the same width x height, and their row sets must
- * partition the frame (rank g of n: row_offset = g, row_stride = n, SURVEY §8e cyclic rows). Peer copies
- * over xGMI are ordered on the root's stream after each source's last render (events); the rows are
- * un-interleaved on the root. Afterwards the root's last frame is the full frame (rgb, and hit when every
- * context wrote one): rt_download / rt_download_bmp read it. Asynchronous like rt_render. */
+/* Multi-GPU in one process without RCCL (the fallback of the CLI's --gpus N; also several contexts on ONE
+ * device): gathers the last render of n contexts -- a frame or a frame batch, f32 rgb or BGRA8 (rt_outputs.bgra),
+ * the same kind on every context -- into ctxs[root]'s full frames [frames][height][width]. Every context must
+ * have rendered the same shape, and their row sets must partition each frame (rank g of n: cyclic rows
+ * {g, n}, block-cyclic rows {g*B, n*B, .., row_block = B}, rotated residues with frame_shift).
+ * Each source's xGMI peer copies are issued on ITS stream after its render (the sources' copy engines run at
+ * once), the root waits for them (events) and un-interleaves the rows. Afterwards the root's last render is
+ * the full frame(s) (rgb or bgra, and hit when every context wrote one): rt_download / rt_download_bmp read a
+ * single frame. Asynchronous like rt_render. */
 int rt_gather(rt_ctx* const* ctxs, int n, int root);
+/* rt_gather into a caller's device buffer d_dst on the root's device ([frames][height][width] x 3 floats or
+ * x 1 uint32, the last renders' kind), e.g. to keep a gathered frame batch; d_dst NULL = rt_gather */
+int rt_gather_to(rt_ctx* const* ctxs, int n, int root, void* d_dst);
+
+/* RCCL communicator over contexts (the framebuffer gather over xGMI). Two ways to build one:
+ *   rt_comm_init      -- one process driving n devices (the CLI's --gpus N): ncclCommInitAll over the contexts'
+ *                        devices, rank i = ctxs[i] (one context per device);
+ *   rt_comm_init_rank -- one rank per process (N processes, one GPU each): ncclCommInitRank with an id that
+ *                        rank 0 made with rt_comm_get_id and handed to every rank (any channel: MPI, a file,
+ *                        torch.distributed).
+ * rt_comm_gather(comm, root, d_dst): every rank's last render (a frame or frame batch, rgb or BGRA8; the row
+ * sets must partition each frame, as for rt_gather) is sent to `root` with ncclSend / ncclRecv in one group,
+ * on each context's stream (so after its render), and un-interleaved there into d_dst ([frames][height][width]
+ * x 3 floats or x 1 uint32; a device pointer on the root's device) or, with d_dst NULL, into the root
+ * context's own buffer, which then is its last render (rt_download / rt_download_bmp). Across processes the
+ * ranks first exchange their row-set descriptors (one 64-B ncclAllGather). Collective: every rank calls it.
+ * Asynchronous on the streams, except that exchange. Hit indices are not gathered (rt_gather does). */
+typedef struct rt_comm rt_comm;
+#define RT_COMM_ID_BYTES 128 /* sizeof(ncclUniqueId) */
+int rt_comm_get_id(unsigned char* id /* RT_COMM_ID_BYTES */);
+int rt_comm_init(rt_ctx* const* ctxs, int n, rt_comm** out);
+int rt_comm_init_rank(rt_ctx* ctx, int nranks, int rank, const unsigned char* id, rt_comm** out);
+int rt_comm_gather(rt_comm* comm, int root, void* d_dst);
+const char* rt_comm_last_error(rt_comm* comm);
+void rt_comm_destroy(rt_comm* comm);
 /* bmp_write_file's bytes of the last frame (cpu/src/bmp_writer.c:88-211): 54-B header + BGRA8 rows
  * bottom-up, (uint8_t)(c * 255.0f) per channel (vec_to_bgra), quantised on the device. Needs a full
  * frame (all rows; after rt_gather for multi-GPU). cap >= 54 + 4 * width * height; synchronous. */

@@ -2,7 +2,8 @@
 //
 //   raytracer [threads] [ntris] [--scene NAME] [--assets DIR] [--width W] [--height H]
 //             [--bounces B] [--iterations K] [--warmup W] [--bvh-heuristic H] [--seed S]
-//             [--gpus N] [--spp S] [--kernel fast|strict|VARIANT] [--tune] [--out FILE.bmp] [--cache DIR]
+//             [--gpus N] [--gather auto|rccl|peer] [--spp S] [--kernel fast|strict|VARIANT] [--tune]
+//             [--out FILE.bmp] [--cache DIR]
 //   VARIANT: persist, persist4, split, coop2, coop4, coop8, fan, chain, chain4 (rt_frame.variant; the fast
 //   kernel's launch configurations, all rendering the same bits); --tune: measure the candidates on the
 //   first frame and keep the fastest (rt_frame.tune)
@@ -11,8 +12,9 @@
 // ITERATIONS 1, BVH_HEURISTIC 3, SEED 1; main.c:97-131: `threads` in 1..63, `ntris` = random mode).
 // Scenes load from <assets>/<scene>/{triangles.obj,triangles.mtl,lights.obj}, default assets "../assets"
 // as in main.c:113-114. The frame renders on the GPU(s) through the rt_* C-ABI; with --gpus N the
-// rows are dealt cyclically over N devices (one rt_ctx each, one host thread each) and gathered on GPU 0
-// (rt_gather). Output: <scene>.bmp (main.c:191, quantised on the GPU) and the reference's stdout metric
+// rows are dealt over N devices in 8-row blocks (one rt_ctx each, one host thread each) and gathered on
+// GPU 0 with RCCL (rt_comm_gather; --gather peer: xGMI peer copies, rt_gather; --gather rccl at one GPU
+// runs the RCCL path over a one-rank communicator). Output: <scene>.bmp (main.c:191, quantised on the GPU) and the reference's stdout metric
 // lines, plus ray counts. --cache DIR keeps the parsed triangles and the BVH in binary cache files
 // (rth_*_cached: identical results, no re-parse / re-build of unchanged scenes).
 #include <algorithm>
@@ -33,7 +35,7 @@ namespace {
 struct Args {
     int threads = 1;
     long ntris = -1;
-    std::string scene = "car_boxed", assets = "../assets", out, kernel = "fast", cache;
+    std::string scene = "car_boxed", assets = "../assets", out, kernel = "fast", cache, gather = "auto";
     int W = 1920, H = 1080, bounces = 4, iterations = 1, warmup = 0, heuristic = 3, gpus = 1, spp = 1, tune = 0;
     unsigned seed = 1;
 };
@@ -66,6 +68,7 @@ Args parse(int argc, char** argv) {
         else if (s == "--kernel") a.kernel = val();
         else if (s == "--tune") a.tune = 1;
         else if (s == "--out") a.out = val();
+        else if (s == "--gather") a.gather = val();
         else if (s == "--cache") a.cache = val();
         else if (s.rfind("--", 0) == 0) usage(("unknown option " + s).c_str());
         else pos.push_back(s);
@@ -76,6 +79,7 @@ Args parse(int argc, char** argv) {
     }
     if (pos.size() == 2) a.ntris = std::atol(pos[1].c_str());  // main.c:112-131 (argc == 3)
     if (a.W <= 0 || a.H <= 0 || a.iterations <= 0 || a.gpus <= 0) usage("invalid frame settings");
+    if (a.gather != "auto" && a.gather != "rccl" && a.gather != "peer") usage("--gather: auto, rccl or peer");
     if (a.out.empty()) a.out = a.scene + ".bmp";
     return a;
 }
@@ -167,6 +171,15 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "unknown --kernel %s\n", a.kernel.c_str());
         return EXIT_FAILURE;
     }
+    // the frame gather: RCCL over the G devices (one communicator per device, one process) by default at G > 1
+    rt_comm* comm = nullptr;
+    if (a.gather == "rccl" || (a.gather == "auto" && G > 1)) {
+        if (rt_comm_init(ctx.data(), G, &comm) != RT_OK) {
+            std::fprintf(stderr, "RCCL communicator: %s; gathering with peer copies\n", rt_last_error(ctx[0]));
+            comm = nullptr;
+        }
+    }
+    std::printf("Frame gather: %s\n", comm ? "RCCL" : G > 1 ? "peer copies" : "none (one GPU)");
     std::vector<float> frame((size_t)a.W * a.H * 3);
     unsigned long long rays = 0;
     auto render_all = [&]() {
@@ -199,9 +212,13 @@ int main(int argc, char** argv) {
     for (int i = 0; i < a.iterations; i++) {  // main.c:171-185
         auto s = std::chrono::steady_clock::now();
         render_all();
-        // cyclic rows of every GPU -> GPU 0's frame (peer copies over xGMI, rt_gather), then to the host
-        if ((G > 1 && rt_gather(ctx.data(), G, 0) != RT_OK) || rt_download(ctx[0], frame.data(), nullptr) != RT_OK) {
-            std::fprintf(stderr, "gather: %s\n", rt_last_error(ctx[0]));
+        // every GPU's 8-row blocks -> GPU 0's frame: RCCL send / recv over xGMI (rt_comm_gather), or xGMI peer
+        // copies (rt_gather) when RCCL is not wanted or not available; then to the host
+        int gs = RT_OK;
+        if (comm) gs = rt_comm_gather(comm, 0, nullptr);
+        else if (G > 1) gs = rt_gather(ctx.data(), G, 0);
+        if (gs != RT_OK || rt_download(ctx[0], frame.data(), nullptr) != RT_OK) {
+            std::fprintf(stderr, "gather: %s\n", comm ? rt_comm_last_error(comm) : rt_last_error(ctx[0]));
             return EXIT_FAILURE;
         }
         double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - s).count();
@@ -243,6 +260,7 @@ int main(int argc, char** argv) {
     std::printf("Expected FPS: %.3f\n", 1000 / mean);
     std::printf("Rays per frame (primary+reflection+shadow): %llu\n", rays);
     std::printf("Throughput: %.1f Mrays/s\n", rays / (median(times) / 1e3) / 1e6);
+    rt_comm_destroy(comm);
     for (auto* c : ctx) rt_destroy(c);
     rth_free(tris);
     rth_free(lights);

@@ -4,6 +4,7 @@
 // and the CPU render_frame (cpu/src/main.c:214-264). All state is per context; every call returns a
 // status; HIP errors are captured into rt_last_error() instead of being printed and ignored.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -67,6 +68,7 @@ struct rt_ctx {
     float* d_rgb_own = nullptr;
     size_t rgb_cap = 0;
     float* last_rgb = nullptr;
+    unsigned* last_bgra = nullptr;  // the last render's BGRA8 output (rt_outputs.bgra), or a gathered full frame
     int* last_hit = nullptr;
     size_t last_pixels = 0;
     int last_W = 0, last_H = 0, last_off = 0, last_stride = 1, last_rows = 0, last_block = 1;  // the last frame's rows
@@ -87,6 +89,8 @@ struct rt_ctx {
     size_t stage_cap = 0;
     unsigned* d_bmp = nullptr;
     size_t bmp_cap = 0;
+    unsigned* d_full_bgra = nullptr;  // gathered BGRA8 frames (rt_gather / rt_comm_gather of bgra renders)
+    size_t full_bgra_cap = 0;
     // split pipeline buffers (rt_split.hpp)
     float4* d_srec = nullptr;
     unsigned* d_spinfo = nullptr;
@@ -100,6 +104,7 @@ struct rt_ctx {
     hipEvent_t ev0s[NEV] = {}, ev1s[NEV] = {};
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // the last launch's pair
     hipEvent_t gather_ev = nullptr;           // completion of the last rt_gather into this (root) context
+    hipEvent_t copy_ev = nullptr;             // rt_gather: this (source) context's peer copies issued
     long long launches = 0;
     bool rendered = false;
     // launch autotuning of RT_KERNEL_FAST (rt_render): the candidate configurations are timed on the
@@ -625,6 +630,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             if (rc) return rc;
         }
         ctx->last_rgb = rgb;
+        ctx->last_bgra = bgra;
         ctx->last_hit = A.hit;
         ctx->last_pixels = all_px;
         ctx->last_frames = n_frames;
@@ -944,6 +950,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     }
     ctx->launches++;
     ctx->last_rgb = rgb;
+    ctx->last_bgra = bgra;
     ctx->last_hit = A.hit;
     ctx->last_pixels = all_px;
     ctx->last_frames = n_frames;
@@ -1058,81 +1065,351 @@ int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count, int cap_a) {
 }
 }  // namespace
 
-extern "C" int rt_gather(rt_ctx* const* ctxs, int n, int root) {
-    if (!ctxs || n <= 0 || root < 0 || root >= n || !ctxs[root]) return RT_E_ARG;
-    rt_ctx* ctx = ctxs[root];
-    const int W = ctx->last_W, H = ctx->last_H;
-    std::vector<char> cover((size_t)std::max(H, 0), 0);
-    bool all_hit = true;
-    size_t stage = 0;
-    for (int i = 0; i < n; i++) {
-        rt_ctx* c = ctxs[i];
-        if (!c || !c->rendered) return arg_err(ctx, "rt_gather: a context has not rendered");
-        if (c->last_W != W || c->last_H != H) return arg_err(ctx, "rt_gather: frame sizes differ");
-        if (c->last_frames != 1) return arg_err(ctx, "rt_gather: the last render was a frame batch");
-        if (!c->last_rgb) return arg_err(ctx, "rt_gather: the last render had a bgra output only");
-        if (c->last_shift) return arg_err(ctx, "rt_gather: the last render rotated its rows (frame_shift)");
-        for (int k = 0; k < c->last_rows; k++) {
-            const long long y = c->last_off + (long long)(k / c->last_block) * c->last_stride + k % c->last_block;
-            if (y < 0 || y >= H || cover[y]) return arg_err(ctx, "rt_gather: row sets do not partition the frame");
-            cover[y] = 1;
-        }
-        all_hit = all_hit && c->last_hit;
-        if (c->device != ctx->device) stage += (size_t)W * c->last_rows * (3 * sizeof(float) + sizeof(int));
+namespace {
+// One rank's part of a gathered frame batch: its last render's compact rows (rt_frame) and payload. 16 ints:
+// the descriptor the RCCL ranks of different processes exchange (rt_comm_gather).
+struct Part {
+    int W, H, frames, rows, off, stride, block, shift;
+    int words;  // 32-bit words per pixel: 1 = BGRA8 (rt_outputs.bgra), 3 = f32 rgb
+    int hit;    // 1: the render wrote hit indices too
+    int pad[6];
+};
+static_assert(sizeof(Part) == 64, "descriptor size");
+
+Part part_of(const rt_ctx* c) {
+    Part p{};
+    p.W = c->last_W;
+    p.H = c->last_H;
+    p.frames = c->last_frames;
+    p.rows = c->last_rows;
+    p.off = c->last_off;
+    p.stride = c->last_stride;
+    p.block = c->last_block;
+    p.shift = c->last_shift;
+    p.words = c->last_bgra ? 1 : 3;
+    p.hit = c->last_hit ? 1 : 0;
+    return p;
+}
+const void* payload_of(const rt_ctx* c) { return c->last_bgra ? (const void*)c->last_bgra : (const void*)c->last_rgb; }
+size_t part_px(const Part& p) { return (size_t)p.frames * p.rows * p.W; }
+
+// "" when the parts' rows partition every frame of the batch (rows a rotated rank renders past the image are
+// skipped), else what is wrong
+std::string check_parts(const std::vector<Part>& ps) {
+    const Part& a = ps[0];
+    if (a.W <= 0 || a.H <= 0) return "a rank has not rendered";
+    std::vector<char> cover((size_t)a.H);
+    for (const Part& p : ps) {
+        if (p.W != a.W || p.H != a.H) return "frame sizes differ";
+        if (p.frames != a.frames) return "frame counts differ";
+        if (p.words != a.words) return "outputs differ (bgra vs rgb)";
+        if (p.rows < 0 || p.stride < 1 || p.block < 1) return "bad row set";
     }
-    for (char v : cover)
-        if (!v) return arg_err(ctx, "rt_gather: row sets do not cover the frame");
-    HIPC(hipSetDevice(ctx->device));
-    const size_t px = (size_t)W * H;
+    for (int f = 0; f < a.frames; f++) {
+        std::fill(cover.begin(), cover.end(), 0);
+        for (const Part& p : ps) {
+            const long long start = p.shift ? (p.off + (long long)f * p.shift) % p.stride : p.off;
+            for (int k = 0; k < p.rows; k++) {
+                const long long y = start + (long long)(k / p.block) * p.stride + k % p.block;
+                if (y >= a.H && p.shift) continue;
+                if (y < 0 || y >= a.H || cover[y]) return "row sets do not partition the frame";
+                cover[y] = 1;
+            }
+        }
+        for (char v : cover)
+            if (!v) return "row sets do not cover the frame";
+    }
+    return "";
+}
+
+// compact part -> full frames on stream s (root's device)
+int unshuffle(rt_ctx* ctx, const void* src, void* dst, const Part& p, int words, hipStream_t s) {
+    const size_t n = part_px(p);
+    if (!n) return RT_OK;
+    const int grid = (int)std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 4096));
+    rtd::k_unshuffle_frames<<<grid, 256, 0, s>>>((const unsigned*)src, (unsigned*)dst, p.W, p.H, p.frames, p.rows,
+                                                   p.off, p.stride, p.block, p.shift, words);
+    HIPC(hipGetLastError());
+    return RT_OK;
+}
+
+// the root's full frames (its own buffers unless the caller gave one); afterwards its last render IS them
+int full_target(rt_ctx* ctx, const Part& a, void* user, void** dst, int** dst_hit, bool want_hit) {
+    const size_t px = (size_t)a.frames * a.W * a.H;
     int rc;
-    if ((rc = grow(ctx, &ctx->d_full, ctx->full_cap, 3 * px))) return rc;
-    if (all_hit && (rc = grow(ctx, &ctx->d_full_hit, ctx->full_hit_cap, px))) return rc;
-    if (stage && (rc = grow(ctx, &ctx->d_stage, ctx->stage_cap, stage))) return rc;
-    size_t at = 0;
-    for (int i = 0; i < n; i++) {
-        rt_ctx* c = ctxs[i];
-        const size_t cpx = (size_t)W * c->last_rows;
-        const float* src = c->last_rgb;
-        const int* src_hit = c->last_hit;
-        // after the source's last render (an event on its own stream; cross-device waits are legal)
-        if (c != ctx) HIPC(hipStreamWaitEvent(ctx->stream, c->ev1, 0));
-        if (c->device != ctx->device) {  // peer copy over xGMI into the root's staging area
-            int can = 0;
-            (void)hipDeviceCanAccessPeer(&can, ctx->device, c->device);
-            if (can) {
-                const hipError_t e = hipDeviceEnablePeerAccess(c->device, 0);
-                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return fail(ctx, e, "hipDeviceEnablePeerAccess");
-                (void)hipGetLastError();
-            }
-            float* dst = (float*)(ctx->d_stage + at);
-            HIPC(hipMemcpyPeerAsync(dst, ctx->device, src, c->device, sizeof(float) * 3 * cpx, ctx->stream));
-            at += sizeof(float) * 3 * cpx;
-            int* dst_hit = nullptr;
-            if (all_hit) {
-                dst_hit = (int*)(ctx->d_stage + at);
-                HIPC(hipMemcpyPeerAsync(dst_hit, ctx->device, src_hit, c->device, sizeof(int) * cpx, ctx->stream));
-                at += sizeof(int) * cpx;
-            }
-            src = dst;
-            src_hit = dst_hit;
-        }
-        const int grid = (int)std::max<size_t>(1, std::min<size_t>((cpx + 255) / 256, 4096));
-        rtd::k_unshuffle<<<grid, 256, 0, ctx->stream>>>(src, all_hit ? src_hit : nullptr, ctx->d_full,
-                                                         all_hit ? ctx->d_full_hit : nullptr, W, c->last_off,
-                                                         c->last_stride, c->last_rows, c->last_block);
-        HIPC(hipGetLastError());
+    if (user) *dst = user;
+    else if (a.words == 1) {
+        if ((rc = grow(ctx, &ctx->d_full_bgra, ctx->full_bgra_cap, px))) return rc;
+        *dst = ctx->d_full_bgra;
+    } else {
+        if ((rc = grow(ctx, &ctx->d_full, ctx->full_cap, 3 * px))) return rc;
+        *dst = ctx->d_full;
     }
+    *dst_hit = nullptr;
+    if (want_hit) {
+        if ((rc = grow(ctx, &ctx->d_full_hit, ctx->full_hit_cap, px))) return rc;
+        *dst_hit = ctx->d_full_hit;
+    }
+    return RT_OK;
+}
+
+int finish_gather(rt_ctx* ctx, const Part& a, void* dst, int* dst_hit) {
     // the gather's completion has its own event: ev0s / ev1s stay the render launches' (rt_kernel_times)
     if (!ctx->gather_ev) HIPC(hipEventCreateWithFlags(&ctx->gather_ev, hipEventDisableTiming));
     HIPC(hipEventRecord(ctx->gather_ev, ctx->stream));
-    ctx->last_rgb = ctx->d_full;
-    ctx->last_hit = all_hit ? ctx->d_full_hit : nullptr;
-    ctx->last_pixels = px;
+    ctx->last_rgb = a.words == 3 ? (float*)dst : nullptr;
+    ctx->last_bgra = a.words == 1 ? (unsigned*)dst : nullptr;
+    ctx->last_hit = dst_hit;
+    ctx->last_pixels = (size_t)a.frames * a.W * a.H;
     ctx->last_off = 0;
     ctx->last_stride = 1;
-    ctx->last_rows = H;
+    ctx->last_rows = a.H;
     ctx->last_block = 1;
+    ctx->last_shift = 0;
     return RT_OK;
+}
+}  // namespace
+
+extern "C" int rt_gather(rt_ctx* const* ctxs, int n, int root) { return rt_gather_to(ctxs, n, root, nullptr); }
+
+extern "C" int rt_gather_to(rt_ctx* const* ctxs, int n, int root, void* d_dst) {
+    if (!ctxs || n <= 0 || root < 0 || root >= n || !ctxs[root]) return RT_E_ARG;
+    rt_ctx* ctx = ctxs[root];
+    std::vector<Part> ps;
+    bool all_hit = true;
+    for (int i = 0; i < n; i++) {
+        rt_ctx* c = ctxs[i];
+        if (!c || !c->rendered) return arg_err(ctx, "rt_gather: a context has not rendered");
+        ps.push_back(part_of(c));
+        all_hit = all_hit && c->last_hit;
+    }
+    const std::string why = check_parts(ps);
+    if (!why.empty()) return arg_err(ctx, ("rt_gather: " + why).c_str());
+    const Part& a = ps[0];
+    const int words = a.words;
+    // staging on the root for the parts of other devices, in rank order: payload, then hit
+    size_t stage = 0;
+    for (int i = 0; i < n; i++)
+        if (ctxs[i]->device != ctx->device) stage += part_px(ps[i]) * 4 * (words + (all_hit ? 1 : 0));
+    HIPC(hipSetDevice(ctx->device));
+    int rc;
+    if (stage && (rc = grow(ctx, &ctx->d_stage, ctx->stage_cap, stage))) return rc;
+    void* dst;
+    int* dst_hit;
+    if ((rc = full_target(ctx, a, d_dst, &dst, &dst_hit, all_hit))) return rc;
+    size_t at = 0;
+    for (int i = 0; i < n; i++) {
+        rt_ctx* c = ctxs[i];
+        const size_t cpx = part_px(ps[i]);
+        const void* src = payload_of(c);
+        const int* src_hit = c->last_hit;
+        if (c->device != ctx->device) {
+            // xGMI peer copies issued on the SOURCE's stream (after its render; the copies of different sources
+            // run on their own devices' engines at once), then the root waits for them
+            void* d1 = ctx->d_stage + at;
+            at += cpx * 4 * words;
+            HIPC(hipSetDevice(c->device));
+            int can = 0;
+            (void)hipDeviceCanAccessPeer(&can, c->device, ctx->device);
+            if (can) {  // direct xGMI copies (else the runtime stages through the host)
+                const hipError_t e = hipDeviceEnablePeerAccess(ctx->device, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return fail(ctx, e, "hipDeviceEnablePeerAccess");
+                (void)hipGetLastError();
+            }
+            HIPC(hipMemcpyPeerAsync(d1, ctx->device, src, c->device, cpx * 4 * words, c->stream));
+            src = d1;
+            if (all_hit) {
+                int* d2 = (int*)(ctx->d_stage + at);
+                at += cpx * 4;
+                HIPC(hipMemcpyPeerAsync(d2, ctx->device, src_hit, c->device, cpx * 4, c->stream));
+                src_hit = d2;
+            }
+            if (!c->copy_ev) HIPC(hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming));
+            HIPC(hipEventRecord(c->copy_ev, c->stream));
+            HIPC(hipSetDevice(ctx->device));
+            HIPC(hipStreamWaitEvent(ctx->stream, c->copy_ev, 0));
+        } else if (c != ctx) {
+            HIPC(hipStreamWaitEvent(ctx->stream, c->ev1, 0));  // after the source's last render
+        }
+        if ((rc = unshuffle(ctx, src, dst, ps[i], words, ctx->stream))) return rc;
+        if (all_hit && (rc = unshuffle(ctx, src_hit, dst_hit, ps[i], 1, ctx->stream))) return rc;
+    }
+    return finish_gather(ctx, a, dst, dst_hit);
+}
+
+// ---------------------------------------------------------------- RCCL communicator (rt_comm_*)
+struct rt_comm {
+    std::vector<rt_ctx*> ctxs;       // the local ranks: ranks rank0 .. rank0 + ctxs.size() - 1
+    std::vector<ncclComm_t> comms;
+    int nranks = 0, rank0 = 0;
+    Part* d_desc = nullptr;  // multi-process: every rank's descriptor (ncclAllGather), on ctxs[0]'s device
+    Part* h_desc = nullptr;  // pinned
+    std::string err;
+};
+
+namespace {
+int comm_fail(rt_comm* cm, ncclResult_t r, const char* what) {
+    cm->err = std::string(what) + ": " + ncclGetErrorString(r);
+    if (!cm->ctxs.empty() && cm->ctxs[0]) cm->ctxs[0]->err = cm->err;
+    return RT_E_HIP;
+}
+int comm_arg(rt_comm* cm, const std::string& what) {
+    cm->err = what;
+    for (rt_ctx* c : cm->ctxs) c->err = what;
+    return RT_E_ARG;
+}
+#define NCCLC(call)                                       \
+    do {                                                  \
+        ncclResult_t r_ = (call);                         \
+        if (r_ != ncclSuccess) return comm_fail(cm, r_, #call); \
+    } while (0)
+}  // namespace
+
+extern "C" int rt_comm_get_id(unsigned char* id) {
+    if (!id) return RT_E_ARG;
+    static_assert(sizeof(ncclUniqueId) == RT_COMM_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return RT_E_HIP;
+    std::memcpy(id, &u, sizeof u);
+    return RT_OK;
+}
+
+extern "C" int rt_comm_init(rt_ctx* const* ctxs, int n, rt_comm** out) {
+    if (!ctxs || n <= 0 || !out) return RT_E_ARG;
+    *out = nullptr;
+    std::vector<int> devs;
+    for (int i = 0; i < n; i++) {
+        if (!ctxs[i]) return RT_E_ARG;
+        for (int d : devs)
+            if (d == ctxs[i]->device) {
+                ctxs[i]->err = "rt_comm_init: RCCL takes one rank per device (two contexts share a device: use rt_gather)";
+                return RT_E_ARG;
+            }
+        devs.push_back(ctxs[i]->device);
+    }
+    rt_comm* cm = new rt_comm;
+    cm->ctxs.assign(ctxs, ctxs + n);
+    cm->comms.resize(n);
+    cm->nranks = n;
+    const ncclResult_t r = ncclCommInitAll(cm->comms.data(), n, devs.data());
+    if (r != ncclSuccess) {
+        comm_fail(cm, r, "ncclCommInitAll");
+        delete cm;
+        return RT_E_HIP;
+    }
+    *out = cm;
+    return RT_OK;
+}
+
+extern "C" int rt_comm_init_rank(rt_ctx* ctx, int nranks, int rank, const unsigned char* id, rt_comm** out) {
+    if (!ctx || !id || !out || nranks <= 0 || rank < 0 || rank >= nranks) return RT_E_ARG;
+    *out = nullptr;
+    HIPC(hipSetDevice(ctx->device));
+    rt_comm* cm = new rt_comm;
+    cm->ctxs = {ctx};
+    cm->comms.resize(1);
+    cm->nranks = nranks;
+    cm->rank0 = rank;
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof u);
+    ncclResult_t r = ncclCommInitRank(&cm->comms[0], nranks, u, rank);
+    if (r != ncclSuccess) {
+        comm_fail(cm, r, "ncclCommInitRank");
+        delete cm;
+        return RT_E_HIP;
+    }
+    hipError_t e = hipMalloc((void**)&cm->d_desc, sizeof(Part) * (nranks + 1));
+    if (e == hipSuccess) e = hipHostMalloc((void**)&cm->h_desc, sizeof(Part) * (nranks + 1));
+    if (e != hipSuccess) {
+        fail(ctx, e, "rt_comm_init_rank: descriptor buffers");
+        rt_comm_destroy(cm);
+        return RT_E_HIP;
+    }
+    *out = cm;
+    return RT_OK;
+}
+
+extern "C" int rt_comm_gather(rt_comm* cm, int root, void* d_dst) {
+    if (!cm || root < 0 || root >= cm->nranks) return RT_E_ARG;
+    const int nl = (int)cm->ctxs.size();
+    for (rt_ctx* c : cm->ctxs)
+        if (!c->rendered) return comm_arg(cm, "rt_comm_gather: a context has not rendered");
+    // every rank's descriptor: at hand in one process, exchanged over RCCL (8 B x 16 per rank) otherwise
+    std::vector<Part> ps(cm->nranks);
+    if (nl == cm->nranks) {
+        for (int i = 0; i < nl; i++) ps[i] = part_of(cm->ctxs[i]);
+    } else {
+        rt_ctx* ctx = cm->ctxs[0];
+        HIPC(hipSetDevice(ctx->device));
+        cm->h_desc[cm->nranks] = part_of(ctx);
+        HIPC(hipMemcpyAsync(cm->d_desc + cm->nranks, cm->h_desc + cm->nranks, sizeof(Part), hipMemcpyHostToDevice, ctx->stream));
+        NCCLC(ncclAllGather(cm->d_desc + cm->nranks, cm->d_desc, sizeof(Part) / 4, ncclInt32, cm->comms[0], ctx->stream));
+        HIPC(hipMemcpyAsync(cm->h_desc, cm->d_desc, sizeof(Part) * cm->nranks, hipMemcpyDeviceToHost, ctx->stream));
+        HIPC(hipStreamSynchronize(ctx->stream));
+        for (int i = 0; i < cm->nranks; i++) ps[i] = cm->h_desc[i];
+    }
+    const std::string why = check_parts(ps);
+    if (!why.empty()) return comm_arg(cm, "rt_comm_gather: " + why);
+    const Part& a = ps[0];
+    const int words = a.words;
+    // the root (when it is local): a staging slot per peer, in rank order
+    const int lroot = root - cm->rank0;
+    rt_ctx* rctx = lroot >= 0 && lroot < nl ? cm->ctxs[lroot] : nullptr;
+    std::vector<size_t> at(cm->nranks, 0);
+    void* dst = nullptr;
+    int* dst_hit = nullptr;
+    if (rctx) {
+        rt_ctx* ctx = rctx;
+        size_t stage = 0;
+        for (int q = 0; q < cm->nranks; q++) {
+            at[q] = stage;
+            if (q != root) stage += part_px(ps[q]) * 4 * words;
+        }
+        HIPC(hipSetDevice(ctx->device));
+        int rc;
+        if (stage && (rc = grow(ctx, &ctx->d_stage, ctx->stage_cap, stage))) return rc;
+        if ((rc = full_target(ctx, a, d_dst, &dst, &dst_hit, false))) return rc;
+    }
+    // one group: every local non-root rank sends its compact frames (on its stream: after its render), the root
+    // receives every peer's into its staging slot
+    NCCLC(ncclGroupStart());
+    for (int l = 0; l < nl; l++) {
+        const int r = cm->rank0 + l;
+        rt_ctx* c = cm->ctxs[l];
+        if (r != root) {
+            NCCLC(ncclSend(payload_of(c), part_px(ps[r]) * words, ncclUint32, root, cm->comms[l], c->stream));
+        } else {
+            for (int q = 0; q < cm->nranks; q++)
+                if (q != root)
+                    NCCLC(ncclRecv(rctx->d_stage + at[q], part_px(ps[q]) * words, ncclUint32, q, cm->comms[l], c->stream));
+        }
+    }
+    NCCLC(ncclGroupEnd());
+    if (!rctx) return RT_OK;
+    rt_ctx* ctx = rctx;
+    HIPC(hipSetDevice(ctx->device));
+    int rc;
+    for (int q = 0; q < cm->nranks; q++) {
+        const void* src = q == root ? payload_of(ctx) : (const void*)(ctx->d_stage + at[q]);
+        if ((rc = unshuffle(ctx, src, dst, ps[q], words, ctx->stream))) return rc;
+    }
+    return finish_gather(ctx, a, dst, dst_hit);
+}
+
+extern "C" const char* rt_comm_last_error(rt_comm* cm) { return cm ? cm->err.c_str() : "null communicator"; }
+
+extern "C" void rt_comm_destroy(rt_comm* cm) {
+    if (!cm) return;
+    for (size_t l = 0; l < cm->comms.size(); l++) {
+        if (cm->ctxs[l]) {
+            (void)hipSetDevice(cm->ctxs[l]->device);
+            (void)hipStreamSynchronize(cm->ctxs[l]->stream);
+        }
+        if (cm->comms[l]) (void)ncclCommDestroy(cm->comms[l]);
+    }
+    if (cm->d_desc) (void)hipFree(cm->d_desc);
+    if (cm->h_desc) (void)hipHostFree(cm->h_desc);
+    delete cm;
 }
 
 extern "C" int rt_download_bmp(rt_ctx* ctx, unsigned char* h_bmp, size_t cap) {
@@ -1142,7 +1419,7 @@ extern "C" int rt_download_bmp(rt_ctx* ctx, unsigned char* h_bmp, size_t cap) {
         return RT_E_STATE;
     }
     if (ctx->last_frames != 1) return arg_err(ctx, "rt_download_bmp: the last render was a frame batch");
-    if (!ctx->last_rgb) return arg_err(ctx, "rt_download_bmp: the last render had a bgra output only");
+    if (!ctx->last_rgb && !ctx->last_bgra) return arg_err(ctx, "rt_download_bmp: no pixels in the last render");
     const int W = ctx->last_W, H = ctx->last_H;
     if (ctx->last_off != 0 || ctx->last_stride != ctx->last_block || ctx->last_rows != H) {
         ctx->err = "rt_download_bmp: the last frame is not a full frame (gather it first)";
@@ -1154,7 +1431,8 @@ extern "C" int rt_download_bmp(rt_ctx* ctx, unsigned char* h_bmp, size_t cap) {
     int rc;
     if ((rc = grow(ctx, &ctx->d_bmp, ctx->bmp_cap, px))) return rc;
     const int grid = (int)std::max<size_t>(1, std::min<size_t>((px + 255) / 256, 4096));
-    rtd::k_bgra<<<grid, 256, 0, ctx->stream>>>(ctx->last_rgb, ctx->d_bmp, W, H);
+    if (ctx->last_rgb) rtd::k_bgra<<<grid, 256, 0, ctx->stream>>>(ctx->last_rgb, ctx->d_bmp, W, H);
+    else rtd::k_flip_rows<<<grid, 256, 0, ctx->stream>>>(ctx->last_bgra, ctx->d_bmp, W, H);  // already quantised
     HIPC(hipGetLastError());
     if (rth_bmp_header(W, H, h_bmp) != RT_OK) return arg_err(ctx, "rt_download_bmp: bad frame size");
     HIPC(hipMemcpyAsync(h_bmp + 54, ctx->d_bmp, 4 * px, hipMemcpyDeviceToHost, ctx->stream));
@@ -1200,6 +1478,7 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     free_scene(ctx);
     if (ctx->gather_ev) (void)hipEventDestroy(ctx->gather_ev);
+    if (ctx->copy_ev) (void)hipEventDestroy(ctx->copy_ev);
     if (ctx->d_rgb_own) (void)hipFree(ctx->d_rgb_own);
     if (ctx->d_cams) (void)hipFree(ctx->d_cams);
     if (ctx->d_pathbuf) (void)hipFree(ctx->d_pathbuf);
@@ -1208,7 +1487,7 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     for (auto& o : ctx->orders) (void)hipFree(o.second);
     for (void* p : {(void*)ctx->d_full, (void*)ctx->d_full_hit, (void*)ctx->d_stage, (void*)ctx->d_bmp,
-                    (void*)ctx->d_srec, (void*)ctx->d_spinfo, (void*)ctx->d_svis, (void*)ctx->d_sbatch})
+                    (void*)ctx->d_full_bgra, (void*)ctx->d_srec, (void*)ctx->d_spinfo, (void*)ctx->d_svis, (void*)ctx->d_sbatch})
         if (p) (void)hipFree(p);
     if (ctx->d_work) (void)hipFree(ctx->d_work);
     for (int i = 0; i < rt_ctx::NEV; i++) {

@@ -4,20 +4,30 @@
 
 namespace rtd {
 
-// Compact rows of one context's frame (row k = image row off + (k / block) * stride + k % block, rt_frame)
-// into the full frame. One thread per float4 of a row would need W % 4 == 0; rows are f32 x 3, so one
-// thread per pixel.
-__global__ __launch_bounds__(256) void k_unshuffle(const float* __restrict__ src, const int* __restrict__ src_hit,
-                                                   float* __restrict__ dst, int* __restrict__ dst_hit, int W,
-                                                   int off, int stride, int rows, int block) {
-    const size_t n = (size_t)W * rows;
+// Compact frames of one rank, [frames][rows][W][words] 32-bit words per pixel (3: f32 rgb, 1: BGRA8 or a
+// hit index), into full frames [frames][H][W][words]: compact row k of frame f is image row
+// start_f + (k / block) * stride + k % block with start_f = (off + f * shift) % stride when the rows rotate
+// (rt_frame.frame_shift), else off; rows at or past H (a rotated rank's padding) are skipped.
+__global__ __launch_bounds__(256) void k_unshuffle_frames(const unsigned* __restrict__ src, unsigned* __restrict__ dst,
+                                                          int W, int H, int frames, int rows, int off, int stride,
+                                                          int block, int shift, int words) {
+    const size_t per = (size_t)rows * W, n = per * frames;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t k = i / W, x = i % W;
-        const size_t o = ((size_t)off + (k / block) * stride + k % block) * W + x;
-        dst[3 * o] = src[3 * i];
-        dst[3 * o + 1] = src[3 * i + 1];
-        dst[3 * o + 2] = src[3 * i + 2];
-        if (dst_hit) dst_hit[o] = src_hit[i];
+        const size_t f = i / per, r = i % per, k = r / W, x = r % W;
+        const size_t start = shift ? ((size_t)off + f * shift) % stride : (size_t)off;
+        const size_t y = start + (k / block) * stride + k % block;
+        if (y >= (size_t)H) continue;
+        const size_t o = (f * H + y) * W + x;
+        for (int e = 0; e < words; e++) dst[o * words + e] = src[i * words + e];
+    }
+}
+
+// top-down BGRA8 rows -> the BMP file's bottom-up order (cpu/src/bmp_writer.c:131-143)
+__global__ __launch_bounds__(256) void k_flip_rows(const unsigned* __restrict__ in, unsigned* __restrict__ out, int W, int H) {
+    const size_t n = (size_t)W * H;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t y = i / W, x = i % W;
+        out[(size_t)(H - 1 - y) * W + x] = in[i];
     }
 }
 

@@ -132,6 +132,17 @@ def hip():
         L.rt_last_error.restype = ctypes.c_char_p
         L.rt_destroy.argtypes = [ctypes.c_void_p]
         L.rt_destroy.restype = None
+        L.rt_gather.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.rt_gather_to.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        L.rt_comm_get_id.argtypes = [ctypes.c_void_p]
+        L.rt_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_void_p)]
+        L.rt_comm_init_rank.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                        P(ctypes.c_void_p)]
+        L.rt_comm_gather.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        L.rt_comm_last_error.argtypes = [ctypes.c_void_p]
+        L.rt_comm_last_error.restype = ctypes.c_char_p
+        L.rt_comm_destroy.argtypes = [ctypes.c_void_p]
+        L.rt_comm_destroy.restype = None
         L.rt_device_count.argtypes = []
         L.rt_version.restype = ctypes.c_char_p
         _hip = L

@@ -42,15 +42,79 @@ def device_count():
     return _L.rt_device_count()
 
 
-def gather(renderers, root=0):
-    """rt_gather: the last frames of several Renderers (rows partitioning one frame) -> renderers[root]'s
-    device frame; afterwards renderers[root].download() / download_bmp() return the full frame."""
+def gather(renderers, root=0, out=None):
+    """rt_gather: the last renders of several Renderers (frames or frame batches whose rows partition each
+    frame) -> renderers[root]'s device frames; afterwards renderers[root].download() / download_bmp() return
+    the full frame. out: a contiguous device tensor for the full frames instead (rt_gather_to), e.g. a batch
+    [frames, H, W, 3] f32 or [frames, H, W] int32 (BGRA8)."""
     arr = (ctypes.c_void_p * len(renderers))(*[r._ctx.value for r in renderers])
-    rc = _L.rt_gather(arr, len(renderers), root)
+    if out is not None:
+        assert out.is_cuda and out.is_contiguous()
+        rc = _L.rt_gather_to(arr, len(renderers), root, ctypes.c_void_p(out.data_ptr()))
+    else:
+        rc = _L.rt_gather(arr, len(renderers), root)
     r = renderers[root]
     r._chk(rc, "rt_gather")
     W, H = r._size
     r._last = (W, H)
+
+
+COMM_ID_BYTES = 128  # RT_COMM_ID_BYTES
+
+
+def comm_id():
+    """rt_comm_get_id: a fresh RCCL unique id (bytes) for rt_comm_init_rank; rank 0 makes it, every rank gets it"""
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    if _L.rt_comm_get_id(buf) != 0:
+        raise RtError("rt_comm_get_id failed")
+    return buf.raw
+
+
+class Comm:
+    """rt_comm: an RCCL communicator over Renderers (SURVEY §8e's framebuffer gather over xGMI).
+    Comm(renderers): one process, one Renderer per device (rt_comm_init); Comm([renderer], nranks, rank, id):
+    one rank of a multi-process job (rt_comm_init_rank)."""
+
+    def __init__(self, renderers, nranks=None, rank=None, uid=None):
+        self._r = list(renderers)
+        self._c = ctypes.c_void_p()
+        if nranks is None:
+            arr = (ctypes.c_void_p * len(self._r))(*[r._ctx.value for r in self._r])
+            rc = _L.rt_comm_init(arr, len(self._r), ctypes.byref(self._c))
+        else:
+            assert len(self._r) == 1 and uid is not None and len(uid) == COMM_ID_BYTES
+            rc = _L.rt_comm_init_rank(self._r[0]._ctx, nranks, rank, ctypes.create_string_buffer(uid, COMM_ID_BYTES),
+                                      ctypes.byref(self._c))
+        if rc != 0:
+            raise RtError(f"rt_comm_init: {rc} ({_L.rt_last_error(self._r[0]._ctx).decode()})")
+        self.rank0 = 0 if rank is None else rank
+
+    def gather(self, root=0, out=None):
+        """rt_comm_gather: every rank's last render -> the root's full frames; `out` (root only): a contiguous
+        device tensor [frames, H, W, 3] f32 or [frames, H, W] int32 (BGRA8), else the root Renderer's own
+        buffer (its download() / download_bmp() then read the full frame)."""
+        ptr = None
+        if out is not None:
+            assert out.is_cuda and out.is_contiguous()
+            ptr = ctypes.c_void_p(out.data_ptr())
+        rc = _L.rt_comm_gather(self._c, root, ptr)
+        if rc != 0:
+            raise RtError(f"rt_comm_gather: {rc} ({_L.rt_comm_last_error(self._c).decode()})")
+        lr = root - self.rank0
+        if 0 <= lr < len(self._r):
+            r = self._r[lr]
+            r._last = r._size
+
+    def close(self):
+        if self._c:
+            _L.rt_comm_destroy(self._c)
+            self._c = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def _ptr(x, what="", n=0, dtypes=(), device=None):
