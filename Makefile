@@ -1,6 +1,6 @@
 # Build recipe for the MI355X ray tracer (no cmake): `make -j8` (what __graft_entry__.build() runs).
 #   parallel-ray-tracer_amd/lib/librt_host.so   host half: loader, camera, BVH, BMP (g++, strict FP)
-#   parallel-ray-tracer_amd/lib/librt_hip.so    device half: HIP kernels for gfx950 + the rt_* C-ABI (+ RCCL)
+#   parallel-ray-tracer_amd/lib/librt_hip.so    device half: HIP kernels for gfx950 + the rt_* C-ABI (RCCL dlopen'ed on first use)
 #   parallel-ray-tracer_amd/bin/raytracer       CLI drop-in for cpu/raytracer (links both)
 #   oracle/liboracle*.so, oracle/_ref/*         test infrastructure (oracle/Makefile)
 PKG      := parallel-ray-tracer_amd
@@ -34,8 +34,7 @@ HIP_HDRS := $(wildcard $(CSRC)/hip/*.hpp) include/rt_hip.h include/rt_types.h
 
 $(LIB)/librt_hip.so: $(HIP_SRCS) $(HIP_HDRS) $(LIB)/librt_host.so
 	@mkdir -p $(LIB)
-	$(HIPCC) $(HIP_FLAGS) -shared -o $@ $(HIP_SRCS) -L$(LIB) -lrt_host -L/opt/rocm/lib -lrccl -Wl,-rpath,'$$ORIGIN' \
-	    -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) $(HIP_FLAGS) -shared -o $@ $(HIP_SRCS) -L$(LIB) -lrt_host -ldl -Wl,-rpath,'$$ORIGIN'
 
 
 $(BIN)/raytracer: $(CSRC)/cli/raytracer.cpp $(LIB)/librt_host.so $(LIB)/librt_hip.so

@@ -388,9 +388,9 @@ def main():
             try:
                 tj = json.load(open(args.traffic_json))
                 key = f"{args.scene}_{W}x{H}_{args.kernel}_{args.bvh}" + ("_bgra8" if bgra else "")
-                if key in tj:
-                    traffic = tj[key]["hbm_bytes_per_launch"]
+                if key in tj:  # measured on 16-frame launches (tools/profile.sh): per frame x this launch's frames
                     pmc = tj[key]
+                    traffic = pmc["hbm_bytes_per_frame"] * F if "hbm_bytes_per_frame" in pmc else pmc["hbm_bytes_per_launch"]
             except Exception:
                 traffic = None
         achieved = bytes_launch / (k_avg_ms / 1e3) / 1e9
@@ -428,7 +428,13 @@ def main():
                          # measured by rocprofv3 PMC passes of this command (profiles/pmc_traffic.json)
                          "hbm_frac_measured": (traffic / (k_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
                          "valu_issue_frac": pmc.get("valu_issue_frac"),
-                         "l2_read_bytes_per_launch": pmc.get("l2_read_bytes_per_launch"),
+                         "wave_wait_frac": pmc.get("wave_wait_frac"),
+                         "l2_hit_rate": pmc.get("l2_hit_rate"),
+                         "l2_read_bytes_per_launch": (pmc["l2_read_bytes_per_launch"] / pmc.get("frames_per_launch", 16) * F)
+                                                     if pmc.get("l2_read_bytes_per_launch") else None,
+                         "pmc_source": pmc.get("source"),
+                         # what binds the kernel, measured (the contract's `bound` names the priced roofline)
+                         "bound_measured": ("latency/VALU" if traffic and traffic < 0.05 * bytes_launch else "hbm"),
                          "limiter": ("dependent-load latency and VALU issue (HBM traffic is ~1 % of the algorithmic "
                                      "bytes: the scene is L2/MALL-resident)") if traffic and traffic < 0.05 * bytes_launch
                                     else "see DESIGN.md §5",

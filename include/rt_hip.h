@@ -83,7 +83,10 @@ enum {
     RT_VARIANT_COOP8 = 6,    /* k_coop: 8 lanes per ray */
     RT_VARIANT_FAN = 7,      /* k_fan: 1 + lights lanes per pixel (shadow fan-out; 1..7 lights) */
     RT_VARIANT_CHAIN = 8,    /* k_chain: one lane per pixel path, each lane's walks back to back, 3 waves per SIMD */
-    RT_VARIANT_CHAIN4 = 9    /* k_chain at 4 waves per SIMD */
+    RT_VARIANT_CHAIN4 = 9,   /* k_chain at 4 waves per SIMD */
+    RT_VARIANT_POOL = 10     /* k_pool: 16x16-pixel tile per workgroup, each bounce level's closest-hit and shadow rays
+                                compacted into tile-local LDS queues and traced with dynamic fetch (rt_frame.regroup =
+                                idle lanes per refill), 4 waves per SIMD */
 };
 
 /* rt_frame.dealing: order in which persistent waves take 8x8 tiles (k_persist, k_chain) */
@@ -120,7 +123,7 @@ typedef struct rt_frame {
     int waves_cap; /* persistent grids: at most this many workgroups (4 waves each) per CU; 0 = occupancy limit */
     int dealing;   /* RT_DEAL_* */
     int regroup;   /* k_chain: lanes whose walk ended wait until this many wait (or no lane walks), then advance
-                      together; 0 = the default (16) */
+                      together; k_pool: idle lanes of a wave that trigger a refill from the tile's queue; 0 = 16 */
 } rt_frame;
 
 /* Device output pointers (all nullable). rgb: [n_rows][width][3] f32 in [0,1] = vec_t pixels

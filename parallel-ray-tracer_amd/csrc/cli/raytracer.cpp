@@ -4,7 +4,7 @@
 //             [--bounces B] [--iterations K] [--warmup W] [--bvh-heuristic H] [--seed S]
 //             [--gpus N] [--gather auto|rccl|peer] [--spp S] [--kernel fast|strict|VARIANT] [--tune]
 //             [--out FILE.bmp] [--cache DIR]
-//   VARIANT: persist, persist4, split, coop2, coop4, coop8, fan, chain, chain4 (rt_frame.variant; the fast
+//   VARIANT: persist, persist4, split, coop2, coop4, coop8, fan, chain, chain4, pool (rt_frame.variant; the fast
 //   kernel's launch configurations, all rendering the same bits); --tune: measure the candidates on the
 //   first frame and keep the fastest (rt_frame.tune)
 //
@@ -159,10 +159,10 @@ int main(int argc, char** argv) {
             return EXIT_FAILURE;
         }
     }
-    static const char* variants[] = {"fast", "persist", "persist4", "split", "coop2",
-                                     "coop4", "coop8", "fan", "chain", "chain4"};
+    static const char* variants[] = {"fast",  "persist", "persist4", "split",  "coop2", "coop4",
+                                     "coop8", "fan",     "chain",    "chain4", "pool"};
     int kern = a.kernel == "strict" ? RT_KERNEL_STRICT : -1, variant = RT_VARIANT_DEFAULT;
-    for (int v = 0; v < 10 && kern < 0; v++)
+    for (int v = 0; v < 11 && kern < 0; v++)
         if (a.kernel == variants[v]) {
             kern = RT_KERNEL_FAST;
             variant = v;

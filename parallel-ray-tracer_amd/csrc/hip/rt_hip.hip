@@ -4,7 +4,10 @@
 // and the CPU render_frame (cpu/src/main.c:214-264). All state is per context; every call returns a
 // status; HIP errors are captured into rt_last_error() instead of being printed and ignored.
 #include <hip/hip_runtime.h>
+#include <dlfcn.h>
 #include <rccl/rccl.h>
+
+#include <type_traits>
 
 #include <algorithm>
 #include <cmath>
@@ -22,6 +25,7 @@
 #include "rt_output.hpp"
 #include "rt_split.hpp"
 #include "rt_chain.hpp"
+#include "rt_pool.hpp"
 
 #include <cstdlib>
 
@@ -474,6 +478,9 @@ void launch_paths(const rtd::KArgs& A, int variant, bool count, int device, hipS
                       : rtd::k_persist<MAXB, false, false, true, 4, false, false, 2, true>;
             if (batch) k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, 2, true>
                                  : rtd::k_persist<MAXB, false, false, true, 4, false, true, 2, true>;
+            if (batch && A.spp <= 1)  // the bench's kernel: spp = 1 build
+                k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, 2, true, true>
+                          : rtd::k_persist<MAXB, false, false, true, 4, false, true, 2, true, true>;
         } else {
             k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, false, true>
                       : rtd::k_persist<MAXB, false, false, true, 4, false, false, true>;
@@ -490,6 +497,18 @@ rtd::DBvh dview(const DevView& v) { return rtd::DBvh{v.nodes, v.leaves, v.tris, 
 }  // namespace
 
 namespace {
+// k_pool (rt_pool.hpp): one 16 x 16 tile per workgroup, tile-local ray queues with dynamic fetch; dynamic LDS =
+// the wide stack + ray slots + queue (rtd::pool_lds_bytes); cap = workgroups per CU (0: the occupancy limit)
+template <int MAXB>
+int launch_pool(const rtd::KArgs& A, bool count, int device, hipStream_t s, int cap) {
+    auto k = count ? rtd::k_pool<MAXB, true, 4, false> : rtd::k_pool<MAXB, false, 4, false>;
+    if (A.n_frames > 1) k = count ? rtd::k_pool<MAXB, true, 4, true> : rtd::k_pool<MAXB, false, 4, true>;
+    const size_t dyn = rtd::pool_lds_bytes(A.wcap);
+    const int blocks = std::max(1, std::min(resident(k, device, cap > 0 ? cap : 8, dyn), A.n_tiles * A.n_frames));
+    k<<<blocks, rtd::BLOCK, dyn, s>>>(A);
+    return RT_OK;
+}
+
 // k_fan (rt_fan.hpp): R lanes per pixel (closest chain + R - 1 shadow lanes), 64 / R-pixel tiles
 template <int MAXB>
 int launch_fan(const rtd::KArgs& A, int R, bool count, int device, hipStream_t s, int cap) {
@@ -560,7 +579,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     while (g * g < f->spp) g++;
     if (f->spp < 1 || g * g != f->spp || g > 16) return arg_err(ctx, "rt_render: spp must be a square 1..256");
     if (f->kernel < RT_KERNEL_AUTO || f->kernel > RT_KERNEL_FAST) return arg_err(ctx, "rt_render: bad kernel");
-    if (f->variant < RT_VARIANT_DEFAULT || f->variant > RT_VARIANT_CHAIN4 || f->tune < 0 || f->tune > 1 ||
+    if (f->variant < RT_VARIANT_DEFAULT || f->variant > RT_VARIANT_POOL || f->tune < 0 || f->tune > 1 ||
         f->waves_cap < 0 || f->waves_cap > 8 || f->dealing < RT_DEAL_DEFAULT || f->dealing > RT_DEAL_ROW_MAJOR ||
         f->regroup < 0 || f->regroup > 64)
         return arg_err(ctx, "rt_render: bad launch configuration (variant / tune / waves_cap / dealing / regroup)");
@@ -738,8 +757,9 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                          : f->dealing == RT_DEAL_COLUMNS ? 2
                          : f->dealing == RT_DEAL_BLOCKS  ? 3
                                                          : 0;
-    if (centre_out && xcd_mode >= 1 && xcd_mode <= 3) {
-        const int tx = A.tiles_x, ty = A.n_tiles / A.tiles_x;
+    auto regions_for = [&](int tx, int ty, const int*& roff, const int*& rord) -> int {
+        roff = rord = nullptr;
+        if (!(centre_out && xcd_mode >= 1 && xcd_mode <= 3)) return RT_OK;
         const long long key = ((long long)xcd_mode << 58) | ((long long)tx << 32) | (unsigned)ty;
         auto it = ctx->orders.find(key);
         if (it == ctx->orders.end()) {
@@ -770,9 +790,11 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             HIPC(hipMemcpy(d, dev.data(), sizeof(int) * dev.size(), hipMemcpyHostToDevice));
             it = ctx->orders.emplace(key, d).first;
         }
-        region_off = it->second;
-        region_order = it->second + 9;
-    }
+        roff = it->second;
+        rord = it->second + 9;
+        return RT_OK;
+    };
+    if (int rc = regions_for(A.tiles_x, A.n_tiles / A.tiles_x, region_off, region_order)) return rc;
     // RT_KERNEL_FAST launch configurations (rt_frame.variant; every one renders the same bits):
     //   PERSIST / PERSIST4  k_persist, one lane per pixel path, walks in lockstep, 8x8 tiles;
     //   CHAIN / CHAIN4      k_chain (rt_chain.hpp), one lane per pixel path, each lane's walks back to back;
@@ -794,6 +816,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         if (v == RT_VARIANT_FAN) return fan_ok;
         if (v >= RT_VARIANT_COOP2 && v <= RT_VARIANT_COOP8) return wide_ok;
         if (v == RT_VARIANT_CHAIN || v == RT_VARIANT_CHAIN4) return wide_ok && !A.tile_trace;
+        if (v == RT_VARIANT_POOL) return wide_ok && !A.tile_trace && A.wcap > 0;
         return true;
     };
     int mode = f->variant;
@@ -863,8 +886,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             T.choice = best;
             T.pending = false;
             if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1) {
-                static const char* names[] = {"default", "persist", "persist4", "split", "coop2",
-                                              "coop4",   "coop8",   "fan",      "chain", "chain4"};
+                static const char* names[] = {"default", "persist", "persist4", "split", "coop2", "coop4",
+                                              "coop8",   "fan",     "chain",    "chain4", "pool"};
                 std::fprintf(stderr, "[prt tune] %dx%d b%d spp%d f%d:", T.W, T.rows, T.bounces, T.spp, T.frames);
                 for (int c = 0; c < T.n; c++) std::fprintf(stderr, " %s/%d %.3f ms", names[T.mode[c]], T.cap[c], T.ms[c]);
                 std::fprintf(stderr, " -> %d\n", best);
@@ -904,6 +927,24 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                                        : launch_fan<8>(B, gr, count, ctx->device, ctx->stream, cp);
             return f->bounces <= 4 ? launch_coop<4>(B, gr, count, ctx->device, ctx->stream, cp)
                                    : launch_coop<8>(B, gr, count, ctx->device, ctx->stream, cp);
+        }
+        if (md == RT_VARIANT_POOL) {  // k_pool (rt_pool.hpp): 16 x 16 pixel tiles per workgroup
+            rtd::KArgs B = A;
+            B.tiles_x = (f->width + 15) / 16;
+            const int ty = (f->n_rows + 15) / 16;
+            B.n_tiles = B.tiles_x * ty;
+            const int* roff = nullptr;
+            const int* rord = nullptr;
+            if (int rc = regions_for(B.tiles_x, ty, roff, rord)) return rc;
+            if (roff) {
+                B.region_off = roff;
+                B.tile_order = rord;
+            } else if (int rc = order_for(B.tiles_x, ty, B.tile_order)) {
+                return rc;
+            }
+            trace_n = (size_t)B.n_tiles;
+            return f->bounces <= 4 ? launch_pool<4>(B, count, ctx->device, ctx->stream, cp)
+                                   : launch_pool<8>(B, count, ctx->device, ctx->stream, cp);
         }
         rtd::KArgs P = A;
         if (region_off) {
@@ -1248,8 +1289,55 @@ struct rt_comm {
 };
 
 namespace {
+// RCCL is opened on first use (dlopen of librccl.so.1), not linked: a process that never builds a communicator
+// never loads it, and one that already has it (torch.distributed's RCCL) gets that same library (matched by
+// soname) instead of a second copy next to it.
+struct Rccl {
+    bool tried = false, ok = false;
+    std::string why;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+Rccl& rccl() {
+    static Rccl R;
+    if (R.tried) return R;
+    R.tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+        R.why = std::string("cannot load librccl.so.1: ") + dlerror();
+        return R;
+    }
+    bool all = true;
+    auto sym = [&](auto& fp, const char* name) {
+        fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+        if (!fp) all = false;
+    };
+    sym(R.GetUniqueId, "ncclGetUniqueId");
+    sym(R.CommInitAll, "ncclCommInitAll");
+    sym(R.CommInitRank, "ncclCommInitRank");
+    sym(R.CommDestroy, "ncclCommDestroy");
+    sym(R.AllGather, "ncclAllGather");
+    sym(R.Send, "ncclSend");
+    sym(R.Recv, "ncclRecv");
+    sym(R.GroupStart, "ncclGroupStart");
+    sym(R.GroupEnd, "ncclGroupEnd");
+    sym(R.GetErrorString, "ncclGetErrorString");
+    R.ok = all;
+    if (!all) R.why = "librccl.so.1 lacks a symbol";
+    return R;
+}
+
 int comm_fail(rt_comm* cm, ncclResult_t r, const char* what) {
-    cm->err = std::string(what) + ": " + ncclGetErrorString(r);
+    cm->err = std::string(what) + ": " + (rccl().GetErrorString ? rccl().GetErrorString(r) : "RCCL error");
     if (!cm->ctxs.empty() && cm->ctxs[0]) cm->ctxs[0]->err = cm->err;
     return RT_E_HIP;
 }
@@ -1268,8 +1356,9 @@ int comm_arg(rt_comm* cm, const std::string& what) {
 extern "C" int rt_comm_get_id(unsigned char* id) {
     if (!id) return RT_E_ARG;
     static_assert(sizeof(ncclUniqueId) == RT_COMM_ID_BYTES, "ncclUniqueId size");
+    if (!rccl().ok) return RT_E_STATE;
     ncclUniqueId u;
-    if (ncclGetUniqueId(&u) != ncclSuccess) return RT_E_HIP;
+    if (rccl().GetUniqueId(&u) != ncclSuccess) return RT_E_HIP;
     std::memcpy(id, &u, sizeof u);
     return RT_OK;
 }
@@ -1287,11 +1376,15 @@ extern "C" int rt_comm_init(rt_ctx* const* ctxs, int n, rt_comm** out) {
             }
         devs.push_back(ctxs[i]->device);
     }
+    if (!rccl().ok) {
+        ctxs[0]->err = "rt_comm_init: " + rccl().why;
+        return RT_E_STATE;
+    }
     rt_comm* cm = new rt_comm;
     cm->ctxs.assign(ctxs, ctxs + n);
     cm->comms.resize(n);
     cm->nranks = n;
-    const ncclResult_t r = ncclCommInitAll(cm->comms.data(), n, devs.data());
+    const ncclResult_t r = rccl().CommInitAll(cm->comms.data(), n, devs.data());
     if (r != ncclSuccess) {
         comm_fail(cm, r, "ncclCommInitAll");
         delete cm;
@@ -1304,6 +1397,10 @@ extern "C" int rt_comm_init(rt_ctx* const* ctxs, int n, rt_comm** out) {
 extern "C" int rt_comm_init_rank(rt_ctx* ctx, int nranks, int rank, const unsigned char* id, rt_comm** out) {
     if (!ctx || !id || !out || nranks <= 0 || rank < 0 || rank >= nranks) return RT_E_ARG;
     *out = nullptr;
+    if (!rccl().ok) {
+        ctx->err = "rt_comm_init_rank: " + rccl().why;
+        return RT_E_STATE;
+    }
     HIPC(hipSetDevice(ctx->device));
     rt_comm* cm = new rt_comm;
     cm->ctxs = {ctx};
@@ -1312,7 +1409,7 @@ extern "C" int rt_comm_init_rank(rt_ctx* ctx, int nranks, int rank, const unsign
     cm->rank0 = rank;
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
-    ncclResult_t r = ncclCommInitRank(&cm->comms[0], nranks, u, rank);
+    ncclResult_t r = rccl().CommInitRank(&cm->comms[0], nranks, u, rank);
     if (r != ncclSuccess) {
         comm_fail(cm, r, "ncclCommInitRank");
         delete cm;
@@ -1343,7 +1440,7 @@ extern "C" int rt_comm_gather(rt_comm* cm, int root, void* d_dst) {
         HIPC(hipSetDevice(ctx->device));
         cm->h_desc[cm->nranks] = part_of(ctx);
         HIPC(hipMemcpyAsync(cm->d_desc + cm->nranks, cm->h_desc + cm->nranks, sizeof(Part), hipMemcpyHostToDevice, ctx->stream));
-        NCCLC(ncclAllGather(cm->d_desc + cm->nranks, cm->d_desc, sizeof(Part) / 4, ncclInt32, cm->comms[0], ctx->stream));
+        NCCLC(rccl().AllGather(cm->d_desc + cm->nranks, cm->d_desc, sizeof(Part) / 4, ncclInt32, cm->comms[0], ctx->stream));
         HIPC(hipMemcpyAsync(cm->h_desc, cm->d_desc, sizeof(Part) * cm->nranks, hipMemcpyDeviceToHost, ctx->stream));
         HIPC(hipStreamSynchronize(ctx->stream));
         for (int i = 0; i < cm->nranks; i++) ps[i] = cm->h_desc[i];
@@ -1372,19 +1469,19 @@ extern "C" int rt_comm_gather(rt_comm* cm, int root, void* d_dst) {
     }
     // one group: every local non-root rank sends its compact frames (on its stream: after its render), the root
     // receives every peer's into its staging slot
-    NCCLC(ncclGroupStart());
+    NCCLC(rccl().GroupStart());
     for (int l = 0; l < nl; l++) {
         const int r = cm->rank0 + l;
         rt_ctx* c = cm->ctxs[l];
         if (r != root) {
-            NCCLC(ncclSend(payload_of(c), part_px(ps[r]) * words, ncclUint32, root, cm->comms[l], c->stream));
+            NCCLC(rccl().Send(payload_of(c), part_px(ps[r]) * words, ncclUint32, root, cm->comms[l], c->stream));
         } else {
             for (int q = 0; q < cm->nranks; q++)
                 if (q != root)
-                    NCCLC(ncclRecv(rctx->d_stage + at[q], part_px(ps[q]) * words, ncclUint32, q, cm->comms[l], c->stream));
+                    NCCLC(rccl().Recv(rctx->d_stage + at[q], part_px(ps[q]) * words, ncclUint32, q, cm->comms[l], c->stream));
         }
     }
-    NCCLC(ncclGroupEnd());
+    NCCLC(rccl().GroupEnd());
     if (!rctx) return RT_OK;
     rt_ctx* ctx = rctx;
     HIPC(hipSetDevice(ctx->device));
@@ -1405,7 +1502,7 @@ extern "C" void rt_comm_destroy(rt_comm* cm) {
             (void)hipSetDevice(cm->ctxs[l]->device);
             (void)hipStreamSynchronize(cm->ctxs[l]->stream);
         }
-        if (cm->comms[l]) (void)ncclCommDestroy(cm->comms[l]);
+        if (cm->comms[l]) (void)rccl().CommDestroy(cm->comms[l]);
     }
     if (cm->d_desc) (void)hipFree(cm->d_desc);
     if (cm->h_desc) (void)hipHostFree(cm->h_desc);

@@ -821,7 +821,8 @@ __device__ __forceinline__ v3 primary_dir(const KArgs& A, float fx, float fy) {
 }
 
 // Pixel (x, compact row k) of frame `frame` of the launch (outputs at frame * frame_px).
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0>
+// SPP1: a build for spp = 1 only (the stratified-sample loop compiled out, fewer live values around the path)
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0, bool SPP1 = false>
 __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int frame, int x, int k,
                                              int* __restrict__ stk, Ctr& c, unsigned q = 0,
                                              int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
@@ -833,7 +834,7 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
     v3 col;
     if (A.bounce_hit)
         for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
-    if (A.spp <= 1) {
+    if (SPP1 || A.spp <= 1) {
         col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB>(A, C.pos, primary_dir(C, (float)x, (float)y), stk,
                                                                   c, hit0, t0, (int)o, q, sstk, wcap));
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples
@@ -920,7 +921,7 @@ __device__ __forceinline__ bool next_item(const KArgs& A, int lane, int& reg, in
 // of STACK = 34) and the binary walks' (rare strict fallbacks) in global memory, so that more workgroups
 // fit a CU's LDS: the kernels with OCC > 4 waves per SIMD.
 template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int OCC = 3, bool TRACE = false, bool BATCH = false,
-          int PB = 0, bool DYN = false>
+          int PB = 0, bool DYN = false, bool SPP1 = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(OCC > 0 ? OCC : 1)))
 void k_persist(KArgs A) {
     static_assert(PB != 2 || DYN, "an LDS path buffer lives in the DYN kernels' dynamic LDS");
@@ -950,7 +951,7 @@ void k_persist(KArgs A) {
         unsigned long long t0 = 0;
         const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
         if (TRACE) t0 = __builtin_amdgcn_s_memrealtime();
-        if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT, REG, 1, PB>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, 0u,
+        if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT, REG, 1, PB, SPP1>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, 0u,
                                                                               sstk, wcap);
         if (TRACE) {  // {begin, end, wave | fallbacks << 32, wave steps | lane node visits << 32} (COUNT)
             const unsigned fb = wave_sum(c.fb - fb0), ws = wave_sum(c.ws - ws0), nv = wave_sum(c.chi + c.shi - nd0);

@@ -19,8 +19,9 @@ RGB_TOL = 1e-5
 # every kernel and launch configuration the C-ABI exposes (rt_frame.kernel / rt_frame.variant): STRICT, FAST
 # with its default rule ("fast"), and each variant forced: k_persist at 4 waves/SIMD ("persist4"), k_chain
 # ("chain", "chain4": each lane's walks back to back), k_coop ("coopG": G lanes per ray), k_fan ("fan":
-# 1 + lights lanes per pixel). The split pipeline has its own tests.
-KERNELS = ["strict", "fast", "persist4", "chain", "chain4", "coop2", "coop4", "coop8", "fan"]
+# 1 + lights lanes per pixel), k_pool ("pool": tile-local ray queues with dynamic fetch). The split
+# pipeline has its own tests.
+KERNELS = ["strict", "fast", "persist4", "chain", "chain4", "coop2", "coop4", "coop8", "fan", "pool"]
 
 
 def select(kernel):
@@ -176,7 +177,7 @@ def test_strict_traversal_counters_match_reference_order(dev, scenes):
         assert st[k] == c[k], k
 
 
-@pytest.mark.parametrize("kernel", ["fast", "chain4", "coop4", "fan"])
+@pytest.mark.parametrize("kernel", ["fast", "chain4", "coop4", "fan", "pool"])
 @pytest.mark.parametrize("spp", [4, 16])
 def test_spp_matches_oracle(dev, scenes, spp, kernel):
     from tests.oracle_bind import OracleScene
@@ -192,7 +193,7 @@ def test_spp_matches_oracle(dev, scenes, spp, kernel):
 _SPP64 = {}
 
 
-@pytest.mark.parametrize("kernel", ["fast", "persist4", "chain4", "coop4", "fan"])
+@pytest.mark.parametrize("kernel", ["fast", "persist4", "chain4", "coop4", "fan", "pool"])
 def test_car_boxed_64spp_matches_oracle(dev, scenes, kernel):
     """BASELINE config 5 (car_boxed 3840x2160, 64 spp, multi-bounce): the reference has one corner ray per
     pixel (cpu/src/main.c:228-239); SURVEY §8d defines spp = s x s stratified sub-pixel samples, mean of the
@@ -433,7 +434,7 @@ def moved_camera(W, H, dx, dz):
     return c
 
 
-@pytest.mark.parametrize("kernel", ["fast", "chain4", "coop4", "fan", "strict"])
+@pytest.mark.parametrize("kernel", ["fast", "chain4", "coop4", "fan", "strict", "pool"])
 @pytest.mark.parametrize("name", ["car_boxed", "dragon"])
 def test_frame_batch_equals_single_frames(dev, name, kernel):
     """rt_render_frames: a batch of frames (different cameras, one persistent launch on the fast paths)
@@ -586,7 +587,7 @@ def test_path_level_placements_render_the_same_frames(dev, name):
         assert a0["stats"]["rays"] == a1["stats"]["rays"], v
 
 
-@pytest.mark.parametrize("kernel", ["fast", "chain4", "coop4", "fan"])
+@pytest.mark.parametrize("kernel", ["fast", "chain4", "coop4", "fan", "pool"])
 def test_rotated_row_blocks_cover_every_frame(dev, kernel):
     """rt_frame.frame_shift: frame f of rank q renders block residue (q + f) % N (prt.dist rotate), rows
     past the image skipped — over the N ranks every frame of the batch is rendered exactly once, bit for

@@ -16,8 +16,10 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # production instantiation of the bench: k_persist, no counters, 4 waves/SIMD, no trace, frame batch,
-# path buffer in LDS (PB = 2) after the DYN wide stack
-PROD = "k_persist<4, false, false, true, 4, false, true, 2, true>"
+# path buffer in LDS (PB = 2) after the DYN wide stack, the spp = 1 build (round 2)
+PROD = "k_persist<4, false, false, true, 4, false, true, 2, true, true>"
+N_SIMD, N_XCD = 1024, 8
+FRAMES = 16  # tools/profile.sh: bench.py --steps 64 = 4 launches of 16 frames  # MI355X: 256 CUs x 4 SIMDs, 8 XCDs (GRBM_GUI_ACTIVE counts every XCD)
 
 
 def rows(path):
@@ -82,7 +84,7 @@ def main():
         hbm = 2 * f_kb * 1024 + w_kb * 1024
         _, avg = find({r["Name"]: float(r["AverageNs"]) for r in stats}, PROD)
         res = {"kernel": kf, "launches": len(vf), "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
-               "hbm_bytes_per_launch": hbm, "trace_avg_ms": avg / 1e6 if avg else None,
+               "hbm_bytes_per_launch": hbm, "frames_per_launch": FRAMES, "hbm_bytes_per_frame": hbm / FRAMES, "trace_avg_ms": avg / 1e6 if avg else None,
                "trace_median_ms_production_grid": statistics.median(groups[prod_grid]) if groups else None,
                "production_grid_workgroups": prod_grid,
                "hbm_gbs_at_trace_avg": hbm / (avg / 1e9) / 1e9 if avg else None,
@@ -92,10 +94,6 @@ def main():
                   f"- FETCH_SIZE median {f_kb:.0f} kB/launch, WRITE_SIZE median {w_kb:.0f} kB/launch",
                   f"- traffic = 2 x FETCH + WRITE = {hbm / 1e6:.1f} MB/launch"
                   + (f" = {res['hbm_gbs_at_trace_avg']:.1f} GB/s at the trace average" if avg else "")]
-        tj_path = os.path.join(pdir, "pmc_traffic.json")
-        tj = json.load(open(tj_path)) if os.path.exists(tj_path) else {}
-        tj[key] = res
-        json.dump(tj, open(tj_path, "w"), indent=1)
     # other PMC passes, if present: per-kernel medians
     for sub in ("pmc_sq", "pmc_l2", "pmc_valu"):
         p = os.path.join(prof, sub, "run_counter_collection.csv")
@@ -108,6 +106,23 @@ def main():
         if agg:
             lines += ["", f"### {sub} (`{PROD}`, median per launch)", ""]
             lines += [f"- {k}: {statistics.median(v):.4g}" for k, v in sorted(agg.items())]
+            med = {k: statistics.median(v) for k, v in agg.items()}
+            if res is not None and "SQ_ACTIVE_INST_VALU" in med and "GRBM_GUI_ACTIVE" in med:
+                # SQ_ACTIVE_INST_VALU counts quad-cycles per SIMD; GRBM_GUI_ACTIVE the cycles of every XCD
+                cyc = med["GRBM_GUI_ACTIVE"] / N_XCD
+                # a wave64 fp32 VALU instruction issues in 2 cycles on a CDNA4 SIMD (32 lanes per clock: 157 TF fp32
+                # vector = 256 CUs x 4 SIMDs x 32 lanes x 2 flops x 2.4 GHz)
+                res["valu_issue_frac"] = med["SQ_INSTS_VALU"] * 2 / (N_SIMD * cyc)
+                res["valu_issue_rule"] = "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)"
+                res["sq_insts_valu_per_launch"] = med.get("SQ_INSTS_VALU")
+            if res is not None and "TCP_TCC_READ_REQ_sum" in med:
+                res["l2_read_requests_per_launch"] = med["TCP_TCC_READ_REQ_sum"]
+                res["l2_read_bytes_per_launch"] = 64 * med["TCP_TCC_READ_REQ_sum"]
+                res["l2_read_rule"] = "TCP_TCC_READ_REQ_sum x 64 B (L1 -> L2 read requests)"
+                if "TCC_HIT_sum" in med and "TCC_MISS_sum" in med:
+                    res["l2_hit_rate"] = med["TCC_HIT_sum"] / max(1.0, med["TCC_HIT_sum"] + med["TCC_MISS_sum"])
+            if res is not None and "SQ_WAIT_ANY" in med and "SQ_WAVE_CYCLES" in med:
+                res["wave_wait_frac"] = med["SQ_WAIT_ANY"] / max(1.0, med["SQ_WAVE_CYCLES"])
     # CSV copies under profiles/<tag>/: the trace stats as rocprofv3 wrote them, the PMC passes as
     # per-kernel medians (kernel, counter, launches, median, min, max)
     cdir = os.path.join(pdir, tag)
@@ -125,6 +140,11 @@ def main():
             w.writerow(["kernel", "counter", "launches", "median", "min", "max"])
             for (k, c), v in sorted(agg.items()):
                 w.writerow([k, c, len(v), statistics.median(v), min(v), max(v)])
+    if res:
+        tj_path = os.path.join(pdir, "pmc_traffic.json")
+        tj = json.load(open(tj_path)) if os.path.exists(tj_path) else {}
+        tj[key] = res
+        json.dump(tj, open(tj_path, "w"), indent=1)
     with open(os.path.join(pdir, f"{tag}_kernel_stats.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
