@@ -204,7 +204,9 @@ def main():
     ap.add_argument("--bounces", type=int, default=4)
     ap.add_argument("--spp", type=int, default=1)
     ap.add_argument("--bvh", default="random", help="bvh_build heuristic handed over (reference default: 3 = random)")
-    ap.add_argument("--accel", default="auto", help="auto: the library builds a binned-SAH BVH for the fast walk")
+    ap.add_argument("--accel", default="auto", help="auto / gpu: the library builds the fast walk's BVH on the GPU "
+                    "(PLOC, rt_build.hpp; auto falls back to host); host: binned SAH on the host; reference: the "
+                    "handed-over BVH")
     ap.add_argument("--no-single-thread", action="store_true", help="skip the 1-thread CPU baseline sample")
     ap.add_argument("--kernel", default="fast")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -264,6 +266,7 @@ def main():
     rends = [device.Renderer(local, stream=s.cuda_stream) for s in streams]
     for rr_ in rends:
         rr_.upload(scene, accel=args.accel)
+    info = rends[0].scene_info()  # what the upload built (rt_get_scene_info): accel, wide depth, build time
     cam = host.camera(W, H)
     K = args.steps
     # launches covering exactly K frames, as few as --frames allows and of (nearly) equal size: K = 20 at 16
@@ -413,7 +416,9 @@ def main():
                        "scene": args.scene, "triangles": scene.n_triangles, "lights": len(scene.lights),
                        "width": W, "height": H, "bvh": args.bvh, "accel": args.accel, "kernel": args.kernel,
                        "rays_per_frame": rays_frame, "output": args.output, "parallelism": f"{B}-row blocks cyclic x{world} + RCCL gather"
-                       if world > 1 else "single GPU", "frames_per_launch": F},
+                       if world > 1 else "single GPU", "frames_per_launch": F,
+                       "accel_built": info["accel_built"], "accel_build_ms": info["build_ms"],
+                       "wide_depth": info["wide_depth"]},
             "frame_latency_ms": lat.item(),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

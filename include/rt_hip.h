@@ -58,9 +58,23 @@ typedef struct rt_scene {
 
 /* rt_scene.accel */
 enum {
-    RT_ACCEL_AUTO = 0,     /* build a binned-SAH BVH on upload for the fast walk; `bvh` serves the strict walk */
-    RT_ACCEL_REFERENCE = 1 /* traverse the given `bvh` in both walks */
+    RT_ACCEL_AUTO = 0,      /* the library builds the fast walk's BVH: RT_ACCEL_GPU, falling back to RT_ACCEL_HOST;
+                               `bvh` serves the strict walk */
+    RT_ACCEL_REFERENCE = 1, /* traverse the given `bvh` in both walks */
+    RT_ACCEL_GPU = 2,       /* build the fast walk's BVH on the GPU (PLOC over Morton-sorted triangles, rt_build.hpp),
+                               then collapse it to the 8-wide quantised layout; falls back to RT_ACCEL_HOST when the
+                               tree is too deep for the wide walk (rt_scene_info.accel_built says which) */
+    RT_ACCEL_HOST = 3       /* build it on the host: binned SAH (librt_host.so), then the same collapse */
 };
+
+/* what rt_upload_scene built (rt_get_scene_info) */
+typedef struct rt_scene_info {
+    int n_triangles, n_lights;
+    int wide_nodes, wide_depth; /* the fast walk's 8-wide BVH (0: none, the binary fast walk) */
+    int accel_built;            /* RT_ACCEL_* of the fast walk's BVH as built (RT_ACCEL_AUTO = host binned SAH) */
+    float build_ms;             /* host wall time of the acceleration build (binary tree + wide collapse) */
+    float gpu_build_ms;         /* of which the GPU tree build (RT_ACCEL_GPU; incl. transfers) */
+} rt_scene_info;
 
 /* rt_frame.kernel */
 enum {
@@ -166,6 +180,7 @@ const char* rt_version(void);
 int rt_create(const rt_opts* opts, rt_ctx** out);
 /* load_to_gpu(): converts the reference layouts into the device layout and uploads */
 int rt_upload_scene(rt_ctx* ctx, const rt_scene* scene);
+int rt_get_scene_info(rt_ctx* ctx, rt_scene_info* info);
 /* render_frame(): enqueues ONE kernel on the context stream (asynchronous) */
 int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* frame, const rt_outputs* out);
 /* A batch of n_frames frames of the same shape (a camera sequence; main.c:141-160's ITERATIONS loop when

@@ -75,6 +75,12 @@ class Stats(ctypes.Structure):
     _fields_ = [(f, ctypes.c_ulonglong) for f in STAT_FIELDS]
 
 
+class SceneInfo(ctypes.Structure):  # rt_scene_info
+    _fields_ = [("n_triangles", ctypes.c_int), ("n_lights", ctypes.c_int), ("wide_nodes", ctypes.c_int),
+                ("wide_depth", ctypes.c_int), ("accel_built", ctypes.c_int), ("build_ms", ctypes.c_float),
+                ("gpu_build_ms", ctypes.c_float)]
+
+
 _host = None
 _hip = None
 
@@ -133,6 +139,7 @@ def hip():
         L.rt_destroy.argtypes = [ctypes.c_void_p]
         L.rt_destroy.restype = None
         L.rt_gather.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.rt_get_scene_info.argtypes = [ctypes.c_void_p, P(SceneInfo)]
         L.rt_gather_to.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.rt_comm_get_id.argtypes = [ctypes.c_void_p]
         L.rt_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_void_p)]

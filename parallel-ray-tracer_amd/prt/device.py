@@ -18,7 +18,8 @@ KERNELS = {"auto": 0, "strict": 1, "fast": 2}
 VARIANTS = {"default": 0, "persist": 1, "persist4": 2, "split": 3, "coop2": 4, "coop4": 5, "coop8": 6, "fan": 7,
             "chain": 8, "chain4": 9, "pool": 10}
 DEALING = {"default": 0, "global": 1, "rows": 2, "columns": 3, "blocks": 4, "row_major": 5}
-ACCEL = {"auto": 0, "reference": 1}
+ACCEL = {"auto": 0, "reference": 1, "gpu": 2, "host": 3}
+ACCEL_NAMES = {v: k for k, v in ACCEL.items()}
 FLAG_COUNTERS = 1
 
 
@@ -165,8 +166,10 @@ class Renderer:
 
     def upload(self, scene, accel="auto"):
         """load_to_gpu(): scene = prt.host.Scene with a built BVH (the reference's bvh_build output).
-        accel="auto": the library also builds its own binned-SAH BVH for the fast kernel;
-        accel="reference": the fast kernel traverses the given BVH too."""
+        accel="auto" / "gpu": the library builds the fast kernel's BVH on the GPU (PLOC, rt_build.hpp) and
+        collapses it to the 8-wide layout ("host": a binned SAH on the host instead; "auto" falls back to it
+        when the GPU tree is too deep for the wide walk); accel="reference": the fast kernel traverses the given
+        BVH too."""
         if scene.nodes is None:
             raise RtError("upload: build the BVH first")
         tris = np.ascontiguousarray(scene.triangles)
@@ -256,6 +259,15 @@ class Renderer:
         buf = np.zeros(54 + 4 * W * H, np.uint8)
         self._chk(_L.rt_download_bmp(self._ctx, buf.ctypes.data, buf.size), "rt_download_bmp")
         return buf.tobytes()
+
+    def scene_info(self):
+        """rt_get_scene_info: what the last upload built (accel_built: "auto" = host binned SAH, "gpu" = PLOC on
+        the device), the wide BVH's size and depth, build times"""
+        i = _lib.SceneInfo()
+        self._chk(_L.rt_get_scene_info(self._ctx, ctypes.byref(i)), "rt_get_scene_info")
+        d = {f: getattr(i, f) for f, _ in _lib.SceneInfo._fields_}
+        d["accel_built"] = ACCEL_NAMES.get(d["accel_built"], d["accel_built"])
+        return d
 
     def stats(self):
         s = Stats()
