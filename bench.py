@@ -207,6 +207,7 @@ def main():
     ap.add_argument("--accel", default="auto", help="auto / gpu: the library builds the fast walk's BVH on the GPU "
                     "(PLOC, rt_build.hpp; auto falls back to host); host: binned SAH on the host; reference: the "
                     "handed-over BVH")
+    ap.add_argument("--ploc-radius", type=int, default=0, help="the GPU BVH build's neighbourhood (0: library default)")
     ap.add_argument("--no-single-thread", action="store_true", help="skip the 1-thread CPU baseline sample")
     ap.add_argument("--kernel", default="fast")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -265,7 +266,7 @@ def main():
     streams = [torch.cuda.Stream() for _ in range(n_streams)]
     rends = [device.Renderer(local, stream=s.cuda_stream) for s in streams]
     for rr_ in rends:
-        rr_.upload(scene, accel=args.accel)
+        rr_.upload(scene, accel=args.accel, ploc_radius=args.ploc_radius)
     info = rends[0].scene_info()  # what the upload built (rt_get_scene_info): accel, wide depth, build time
     cam = host.camera(W, H)
     K = args.steps
@@ -364,7 +365,7 @@ def main():
 
     # algorithmic bytes of this rank's full-batch launch: one extra untimed launch with traversal counters
     rc = device.Renderer(local, counters=True, stream=stream)
-    rc.upload(scene, accel=args.accel)
+    rc.upload(scene, accel=args.accel, ploc_radius=args.ploc_radius)
     rc.render_frames([cam] * F, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
                      kernel=args.kernel, variant=args.variant, **out(fg.target(0)))
     stc = rc.stats()
@@ -375,7 +376,7 @@ def main():
     k_avg_ms = sum(kfull) / len(kfull)
     # single-frame latency of this rank's rows (one launch, one frame; autotuned: its trial launch first)
     rl = device.Renderer(local, stream=stream)
-    rl.upload(scene, accel=args.accel)
+    rl.upload(scene, accel=args.accel, ploc_radius=args.ploc_radius)
     for _ in range(3):
         rl.render(cam, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp, kernel=args.kernel, tune=True,
                   **out(fg.target(0)[0] if F > 1 else fg.target(0)))
@@ -452,7 +453,7 @@ def main():
             def gpu_rays_for_rows(stride):
                 nr = (H + stride - 1) // stride
                 rr = device.Renderer(local, stream=stream)
-                rr.upload(scene, accel=args.accel)
+                rr.upload(scene, accel=args.accel, ploc_radius=args.ploc_radius)
                 tmp = torch.empty((nr, W, 3), dtype=torch.float32, device="cuda")
                 rr.render(cam, W, H, rows=(0, stride, nr), bounces=args.bounces, kernel=args.kernel, rgb=tmp)
                 n = rr.stats()["rays"]

@@ -19,7 +19,8 @@
 
 namespace rtb {
 
-constexpr int PLOC_R = 16;  // neighbourhood radius of the nearest-neighbour search
+constexpr int PLOC_R = 32;      // default neighbourhood radius (rt_scene.ploc_radius); 8 / 16 / 32 / 64 measured, DESIGN.md
+constexpr int PLOC_R_MAX = 64;
 
 __device__ __forceinline__ int f2o(float f) {  // float -> int with the same order (for atomicMin / atomicMax)
     const int i = __float_as_int(f);
@@ -103,10 +104,10 @@ __device__ __forceinline__ float merged_area(float4 alo, float4 ahi, float4 blo,
 // nearest neighbour of cluster i among positions [i - R, i + R] (the smallest merged area; ties: the lower
 // position). Each block stages its clusters' boxes plus a halo of R on either side in LDS.
 __global__ __launch_bounds__(256) void k_nn(const int* __restrict__ C, int m, const float4* __restrict__ nlo,
-                                            const float4* __restrict__ nhi, int* __restrict__ nn) {
-    __shared__ float4 slo[256 + 2 * PLOC_R], shi[256 + 2 * PLOC_R];
-    const int base = blockIdx.x * 256 - PLOC_R;
-    for (int s = threadIdx.x; s < 256 + 2 * PLOC_R; s += 256) {
+                                            const float4* __restrict__ nhi, int* __restrict__ nn, int R) {
+    __shared__ float4 slo[256 + 2 * PLOC_R_MAX], shi[256 + 2 * PLOC_R_MAX];
+    const int base = blockIdx.x * 256 - R;
+    for (int s = threadIdx.x; s < 256 + 2 * R; s += 256) {
         const int j = base + s;
         if (j >= 0 && j < m) {
             const int c = C[j];
@@ -117,11 +118,11 @@ __global__ __launch_bounds__(256) void k_nn(const int* __restrict__ C, int m, co
     __syncthreads();
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= m) return;
-    const int si = threadIdx.x + PLOC_R;
+    const int si = threadIdx.x + R;
     const float4 alo = slo[si], ahi = shi[si];
     float best = INFINITY;
     int bj = -1;
-    const int j0 = i - PLOC_R < 0 ? 0 : i - PLOC_R, j1 = i + PLOC_R >= m ? m - 1 : i + PLOC_R;
+    const int j0 = i - R < 0 ? 0 : i - R, j1 = i + R >= m ? m - 1 : i + R;
     for (int j = j0; j <= j1; j++) {
         if (j == i) continue;
         const float a = merged_area(alo, ahi, slo[j - base], shi[j - base]);

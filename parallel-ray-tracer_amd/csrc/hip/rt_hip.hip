@@ -328,7 +328,7 @@ namespace {
 // GPU-built acceleration BVH (rt_build.hpp, PLOC) in the reference layout: children of a node at child and
 // child + 1, single-triangle leaves numbered depth-first (every subtree's triangles are one range of idx).
 // Returns RT_OK, or RT_E_STATE when the tree is unusable (the caller falls back to the host build).
-int gpu_ploc(rt_ctx* ctx, const rt_triangle* T, int n, std::vector<rt_bvh_node>& out, std::vector<int>& idx,
+int gpu_ploc(rt_ctx* ctx, const rt_triangle* T, int n, int R, std::vector<rt_bvh_node>& out, std::vector<int>& idx,
              int& depth_out) {
     hipStream_t st = ctx->stream;
     std::vector<float> hv(9 * (size_t)n);
@@ -393,7 +393,7 @@ int gpu_ploc(rt_ctx* ctx, const rt_triangle* T, int n, std::vector<rt_bvh_node>&
     PLOC(hipHostMalloc((void**)&tot, sizeof(int) * 4, hipHostMallocDefault));
     while (m > 1) {
         const int gm = (m + 255) / 256;
-        rtb::k_nn<<<gm, 256, 0, st>>>(C, m, nlo, nhi, nnb);
+        rtb::k_nn<<<gm, 256, 0, st>>>(C, m, nlo, nhi, nnb, R);
         rtb::k_flags<<<gm, 256, 0, st>>>(nnb, m, mflag, keep);
         size_t b1 = tmp_bytes, b2 = tmp_bytes;
         PLOC(hipcub::DeviceScan::ExclusiveSum(tmp, b1, mflag, moff, m, st));
@@ -495,7 +495,8 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     if (sc->accel == RT_ACCEL_GPU || sc->accel == RT_ACCEL_AUTO) {  // PLOC on the device; its binary tree is not traversed
         int gdepth = 0;
         const auto t0 = std::chrono::steady_clock::now();
-        rc = gpu_ploc(ctx, sc->triangles, n, gnodes, gidx, gdepth);
+        const int R = sc->ploc_radius > 0 ? std::min(sc->ploc_radius, rtb::PLOC_R_MAX) : rtb::PLOC_R;
+        rc = gpu_ploc(ctx, sc->triangles, n, R, gnodes, gidx, gdepth);
         gpu_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (rc == RT_E_HIP) return rc;
         if (rc == RT_OK) built = RT_ACCEL_GPU;
