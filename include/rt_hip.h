@@ -55,6 +55,7 @@ typedef struct rt_scene {
     rt_vec3 amb; /* amb_light (cpu/src/main.c:37): 0.5, 0.5, 0.5 */
     int accel;   /* RT_ACCEL_*: acceleration structure of the fast kernel */
     int ploc_radius; /* RT_ACCEL_GPU / AUTO: the GPU build's nearest-neighbour radius (0 = 32, at most 64) */
+    float collapse_node_cost; /* the 8-wide collapse's price of a wide-node visit in triangle tests (0 = 2) */
 } rt_scene;
 
 /* rt_scene.accel */

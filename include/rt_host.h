@@ -77,6 +77,9 @@ typedef struct rth_wbvh_info {
 } rth_wbvh_info;
 int rth_wbvh_build(const rt_bvh_node* bvh, int n_nodes, const int* tri_idx, const rt_triangle* tris, int n_tris,
                    float inflate, uint32_t** nodes, int** tri_order, rth_wbvh_info* info);
+/* the same with the collapse's price of a wide-node visit in triangle tests (c_node <= 0: the default, 2) */
+int rth_wbvh_build_cost(const rt_bvh_node* bvh, int n_nodes, const int* tri_idx, const rt_triangle* tris, int n_tris,
+                        float inflate, float c_node, uint32_t** nodes, int** tri_order, rth_wbvh_info* info);
 
 /* ---- camera: cam_init + cam.rot.x + cam_calculate_screen_coords + inc_x/inc_y
  * (cpu/src/cam.c:5-48, main.c:105-106, main.c:243-250) for a width x height frame:

@@ -534,7 +534,8 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
         uint32_t* words = nullptr;
         int* order = nullptr;
         rth_wbvh_info wi{};
-        if (!rc && rth_wbvh_build(nodes, nlen, idx, sc->triangles, n, inflate, &words, &order, &wi) == RT_OK &&
+        if (!rc && rth_wbvh_build_cost(nodes, nlen, idx, sc->triangles, n, inflate, sc->collapse_node_cost, &words, &order, &wi) ==
+                       RT_OK &&
             wi.depth <= rtd::WSTACK) {
             wide_nodes.resize(5 * (size_t)wi.n_nodes);
             std::memcpy(wide_nodes.data(), words, sizeof(uint32_t) * 20 * (size_t)wi.n_nodes);

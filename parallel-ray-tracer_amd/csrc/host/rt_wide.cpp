@@ -248,6 +248,12 @@ int quantise_axis(const float* lo, const float* hi, int k, float& p, int* qlo, i
 extern "C" int rth_wbvh_build(const rt_bvh_node* bvh, int n_nodes, const int* tri_idx, const rt_triangle* tris,
                               int n_tris, float inflate, uint32_t** nodes_out, int** tri_order_out,
                               rth_wbvh_info* info) {
+    return rth_wbvh_build_cost(bvh, n_nodes, tri_idx, tris, n_tris, inflate, 0.0f, nodes_out, tri_order_out, info);
+}
+
+extern "C" int rth_wbvh_build_cost(const rt_bvh_node* bvh, int n_nodes, const int* tri_idx, const rt_triangle* tris,
+                                   int n_tris, float inflate, float c_node, uint32_t** nodes_out, int** tri_order_out,
+                                   rth_wbvh_info* info) {
     if (!bvh || n_nodes <= 0 || !tri_idx || !tris || n_tris <= 0 || !nodes_out || !tri_order_out ||
         !(inflate >= 0.0f))
         return RT_E_ARG;
@@ -265,7 +271,7 @@ extern "C" int rth_wbvh_build(const rt_bvh_node* bvh, int n_nodes, const int* tr
     // collapse policy: SAH-optimal, a wide-node visit priced at 2 triangle tests (the best of 2 / 3 / 4 in the
     // measured sweep — dragon -3.5 % vs 4, car_boxed even; the greedy largest-area collapse: +1.6 % / +3 %;
     // DESIGN.md §3)
-    w.sah_costs(2.0f);
+    w.sah_costs(c_node > 0.0f ? c_node : 2.0f);
 
     // breadth-first: interior children of a wide node get consecutive indices
     struct Item {

@@ -51,7 +51,7 @@ class SceneDesc(ctypes.Structure):
                 ("bvh", ctypes.POINTER(BvhNode)), ("n_nodes", ctypes.c_int),
                 ("tri_idx", ctypes.POINTER(ctypes.c_int)),
                 ("lights", ctypes.POINTER(Light)), ("n_lights", ctypes.c_int), ("amb", Vec3),
-                ("accel", ctypes.c_int), ("ploc_radius", ctypes.c_int)]
+                ("accel", ctypes.c_int), ("ploc_radius", ctypes.c_int), ("collapse_node_cost", ctypes.c_float)]
 
 
 class Frame(ctypes.Structure):

@@ -164,7 +164,7 @@ class Renderer:
         if rc != 0:
             raise RtError(f"{what}: status {rc}: {_L.rt_last_error(self._ctx).decode()}")
 
-    def upload(self, scene, accel="auto", ploc_radius=0):
+    def upload(self, scene, accel="auto", ploc_radius=0, collapse_node_cost=0.0):
         """load_to_gpu(): scene = prt.host.Scene with a built BVH (the reference's bvh_build output).
         accel="auto" / "gpu": the library builds the fast kernel's BVH on the GPU (PLOC, rt_build.hpp) and
         collapses it to the 8-wide layout ("host": a binned SAH on the host instead; "auto" falls back to it
@@ -179,7 +179,7 @@ class Renderer:
         d = SceneDesc(tris.ctypes.data_as(P(Triangle)), len(tris), nodes.ctypes.data_as(P(BvhNode)), len(nodes),
                       idx.ctypes.data_as(P(ctypes.c_int)),
                       lights.ctypes.data_as(P(Light)) if len(lights) else None, len(lights), Vec3(*scene.amb),
-                      ACCEL.get(accel, accel), ploc_radius)
+                      ACCEL.get(accel, accel), ploc_radius, collapse_node_cost)
         self._chk(_L.rt_upload_scene(self._ctx, ctypes.byref(d)), "rt_upload_scene")
         self.scene = scene
         return self

@@ -37,7 +37,8 @@ def main():
         kw = {k: (int(v) if v.lstrip("-").isdigit() else v) for k, v in (o.split("=") for o in opts.split(",") if o)}
         kw_up = {k[3:]: v for k, v in kw.items() if k.startswith("up_")}  # e.g. persist4:up_ploc_radius=32
         kw = {k: v for k, v in kw.items() if not k.startswith("up_")}
-        up = dict(accel=kw_up.pop("accel", a.accel), ploc_radius=kw_up.pop("ploc_radius", a.ploc_radius))
+        up = dict(accel=kw_up.pop("accel", a.accel), ploc_radius=kw_up.pop("ploc_radius", a.ploc_radius),
+                  collapse_node_cost=float(kw_up.pop("cnode", 0)) / 10.0)  # up_cnode=15: c_node 1.5
         r = device.Renderer(0, counters=True)
         r.upload(s, **up)
         info = r.scene_info()
