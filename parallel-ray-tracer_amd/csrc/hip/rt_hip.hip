@@ -700,6 +700,9 @@ void launch_paths(const rtd::KArgs& A, int variant, bool count, int device, hipS
                       : rtd::k_persist<MAXB, false, false, true, 4, false, false, true>;
             if (batch) k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, true>
                                  : rtd::k_persist<MAXB, false, false, true, 4, false, true, true>;
+            if (batch && A.spp <= 1)  // spp = 1 build (deep trees: the LDS holds no path buffer next to the stack)
+                k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, 1, false, true>
+                          : rtd::k_persist<MAXB, false, false, true, 4, false, true, 1, false, true>;
         }
     }
     const int blocks = std::max(1, std::min(resident(k, device, cu_cap, dyn), (A.n_tiles + 3) / 4));
