@@ -198,6 +198,9 @@ def main():
     ap.add_argument("--no-rotate", action="store_true",
                     help="N > 1: keep each rank on its own block residue in every frame (default: frame f of rank "
                          "q renders residue (q + f) %% N, so every rank's batch costs the same)")
+    ap.add_argument("--orbit", type=float, default=0.02,
+                    help="camera path: frame i of a launch is the reference camera moved by i * ORBIT along x (0: the "
+                         "reference's ITERATIONS loop of one camera, main.c:141-160)")
     ap.add_argument("--scene", default="dragon")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -269,6 +272,16 @@ def main():
         rr_.upload(scene, accel=args.accel, ploc_radius=args.ploc_radius)
     info = rends[0].scene_info()  # what the upload built (rt_get_scene_info): accel, wide depth, build time
     cam = host.camera(W, H)
+    # a camera path: frame i of every launch is the reference camera moved by i * orbit along x (frame 0 IS the
+    # reference's camera), so a batch's frames are all different (no identical rays in flight sharing caches)
+    def path(nf):
+        out = []
+        for i in range(nf):
+            c = host.camera(W, H)
+            c.pos.x += i * args.orbit
+            c.ul.x += i * args.orbit
+            out.append(c)
+        return out
     K = args.steps
     # launches covering exactly K frames, as few as --frames allows and of (nearly) equal size: K = 20 at 16
     # frames per launch is 10 + 10, not 16 + 4 (a 4-frame launch is tail-bound: 1.3 vs 0.93 ms per frame)
@@ -300,7 +313,7 @@ def main():
         with torch.cuda.stream(streams[c]):  # block b is rendered by context c on its stream
             if fg.pending(b):
                 fg.finish(b)
-            rends[c].render_frames([cam] * nf, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
+            rends[c].render_frames(path(nf), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
                                    kernel=args.kernel, variant=args.variant, tune=args.tune, **out(fg.target(b)))
             fg.start(b)
 
@@ -314,9 +327,11 @@ def main():
     # launch-autotuning launch (every candidate configuration timed, rt_hip.hip) and the next launch of
     # that shape reads the timings; each batch size of the plan goes through that here (without --tune
     # these are plain warm-up launches), then `warmup` frames run untimed.
+    rays_of = {}  # this rank's rays of a launch of nf frames (the same camera path every launch: deterministic)
     for nf in sorted(set(plan)):
         for _ in range(2 * n_streams):  # per context: the tuning launch, then the launch reading its timings
             launch(nf)
+        rays_of[nf] = rends[(launch_no[0] - 1) % n_streams].stats()["rays"]
     for _ in range(max(1, -(-args.warmup // F))):
         launch(F)
     drain()
@@ -343,15 +358,14 @@ def main():
         ts_ = rr_.kernel_times(len(mine)) if mine else []
         kfull += [t for t, nf in zip(ts_, mine) if nf == F]
     kfull = kfull or [float("nan")]
-    last = rends[timed[-1][0]]
-    st = last.stats()
-    # whole-job ray count per frame (identical every frame: the render is deterministic), from the last
-    # launch's counters (a batch: the sum over its frames), summed over the ranks before dividing by the
-    # frames (rotated rows: a rank's share differs frame by frame, the frame's total does not)
-    rays_local = st["rays"]
-    if args.bmp and rank == 0:  # the BMP written from the root rank (untimed)
+    # whole-job rays of the timed launches: each launch's count (the counters of a launch of that many frames of
+    # the camera path) summed over the plan and over the ranks (rotated rows: a rank's share differs frame by
+    # frame, the frames' totals do not)
+    assert rends[timed[-1][0]].stats()["rays"] == rays_of[plan[-1]]  # (deterministic: the same launch, again)
+    rays_local = sum(rays_of[nf] for nf in plan)
+    if args.bmp and rank == 0:  # the BMP written from the root rank (untimed): frame 0 = the reference camera
         frames = fg.frame if world > 1 else fg.target(latest[0])
-        px = (frames if frames.dim() == 3 else frames[latest[1] - 1]).cpu().numpy()
+        px = (frames if frames.dim() == 3 else frames[0]).cpu().numpy()
         data = host.bmp_from_bgra(px) if bgra else host.bmp_encode(px)
         with open(args.bmp, "wb") as fbmp:
             fbmp.write(data)
@@ -361,12 +375,13 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(rays_t, op=dist.ReduceOp.SUM)
     elapsed = el.item()
-    rays_frame = int(rays_t.item()) // plan[-1]
+    rays_total = int(rays_t.item())
+    rays_frame = rays_total / K
 
     # algorithmic bytes of this rank's full-batch launch: one extra untimed launch with traversal counters
     rc = device.Renderer(local, counters=True, stream=stream)
     rc.upload(scene, accel=args.accel, ploc_radius=args.ploc_radius)
-    rc.render_frames([cam] * F, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
+    rc.render_frames(path(F), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
                      kernel=args.kernel, variant=args.variant, **out(fg.target(0)))
     stc = rc.stats()
     rc.close()
@@ -400,7 +415,7 @@ def main():
         achieved = bytes_launch / (k_avg_ms / 1e3) / 1e9
         result = {
             "metric": METRIC,
-            "value": rays_frame * K / elapsed / 1e6,
+            "value": rays_total / elapsed / 1e6,
             "unit": "Mrays/s",
             "n_gpus": world,
             "steps": K,

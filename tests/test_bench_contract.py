@@ -1,8 +1,9 @@
 """bench.py's output contract on the GPU, on a small frame: one JSON line with every key the task's
 contract names, the metric string of BASELINE.json, value = rays per frame / ms per step, the
 roofline's frac = achieved / peak, a plan that covers --steps exactly (6 frames in batches of at most 4: 3 + 3),
-and rays per frame equal to the oracle's count for the same frame (the reference's definition:
-primary + traced reflection + traced shadow rays)."""
+and rays per frame equal to the oracle's count for the same frame with --orbit 0 (the reference's definition:
+primary + traced reflection + traced shadow rays); with the default camera path (frame i moved by
+i * 0.02) the BMP of frame 0 is still the reference camera's."""
 import json
 import os
 import subprocess
@@ -22,14 +23,14 @@ def oracle_frame(W, H):
     return o.render(W, H, threads=16)
 
 
-@pytest.mark.parametrize("output", ["bgra8", "rgb"])
-def test_bench_prints_the_contract_line(output, tmp_path):
+@pytest.mark.parametrize("output,orbit", [("bgra8", "0"), ("rgb", "0"), ("bgra8", "0.02")])
+def test_bench_prints_the_contract_line(output, orbit, tmp_path):
     W, H = 320, 180
     bmp = tmp_path / "frame.bmp"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "6", "--warmup", "2",
                         "--frames", "4", "--width", str(W), "--height", str(H), "--no-cpu-baseline",
-                        "--output", output, "--bmp", str(bmp)], capture_output=True, text=True, timeout=240,
-                       cwd=ROOT)
+                        "--output", output, "--bmp", str(bmp), "--orbit", orbit], capture_output=True, text=True,
+                       timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]
@@ -50,9 +51,12 @@ def test_bench_prints_the_contract_line(output, tmp_path):
     assert rf["frames_per_launch"] == 3
     ref = oracle_frame(W, H)
     c = ref["counters"]
-    assert rays == c["primary"] + c["reflection"] + c["shadow"]
+    if orbit == "0":  # the reference's loop of one camera: every frame is the oracle's frame
+        assert rays == c["primary"] + c["reflection"] + c["shadow"]
+    else:  # a camera path (the default): frame 0 is the reference camera, the others moved a little
+        assert abs(rays / (c["primary"] + c["reflection"] + c["shadow"]) - 1) < 0.05
     from prt import host
-    assert bmp.read_bytes() == host.bmp_encode(ref["rgb"])  # the last timed frame, as bmp_write_file writes it
+    assert bmp.read_bytes() == host.bmp_encode(ref["rgb"])  # frame 0 of the last launch, as bmp_write_file writes it
 
 
 def test_bench_two_ranks_on_one_gpu_count_the_whole_frame(tmp_path):
