@@ -98,14 +98,13 @@ enum {
     RT_VARIANT_COOP4 = 5,    /* k_coop: 4 lanes per ray */
     RT_VARIANT_COOP8 = 6,    /* k_coop: 8 lanes per ray */
     RT_VARIANT_FAN = 7,      /* k_fan: 1 + lights lanes per pixel (shadow fan-out; 1..7 lights) */
-    RT_VARIANT_CHAIN = 8,    /* k_chain: one lane per pixel path, each lane's walks back to back, 3 waves per SIMD */
-    RT_VARIANT_CHAIN4 = 9,   /* k_chain at 4 waves per SIMD */
+    /* 8, 9: k_chain (each lane's walks back to back), measured slower and removed in round 2: refused */
     RT_VARIANT_POOL = 10     /* k_pool: 16x16-pixel tile per workgroup, each bounce level's closest-hit and shadow rays
                                 compacted into tile-local LDS queues and traced with dynamic fetch (rt_frame.regroup =
                                 idle lanes per refill), 4 waves per SIMD */
 };
 
-/* rt_frame.dealing: order in which persistent waves take 8x8 tiles (k_persist, k_chain) */
+/* rt_frame.dealing: order in which persistent waves take their tiles (k_persist 8x8, k_pool 16x16) */
 enum {
     RT_DEAL_DEFAULT = 0,  /* XCD-aware: 4 x 2 regions for batches of full frames, 8 row bands otherwise */
     RT_DEAL_GLOBAL = 1,   /* one counter over the centre-out order */
@@ -138,8 +137,7 @@ typedef struct rt_frame {
                       HIP-event times and the fastest renders from then on; 0: the default rule, no trial launches */
     int waves_cap; /* persistent grids: at most this many workgroups (4 waves each) per CU; 0 = occupancy limit */
     int dealing;   /* RT_DEAL_* */
-    int regroup;   /* k_chain: lanes whose walk ended wait until this many wait (or no lane walks), then advance
-                      together; k_pool: idle lanes of a wave that trigger a refill from the tile's queue; 0 = 16 */
+    int regroup;   /* k_pool: idle lanes of a wave that trigger a refill from the tile's queue; 0 = 16 */
 } rt_frame;
 
 /* Device output pointers (all nullable). rgb: [n_rows][width][3] f32 in [0,1] = vec_t pixels

@@ -4,7 +4,7 @@
 //             [--bounces B] [--iterations K] [--warmup W] [--bvh-heuristic H] [--seed S]
 //             [--gpus N] [--gather auto|rccl|peer] [--spp S] [--kernel fast|strict|VARIANT] [--tune]
 //             [--out FILE.bmp] [--cache DIR]
-//   VARIANT: persist, persist4, split, coop2, coop4, coop8, fan, chain, chain4, pool (rt_frame.variant; the fast
+//   VARIANT: persist, persist4, split, coop2, coop4, coop8, fan, pool (rt_frame.variant; the fast
 //   kernel's launch configurations, all rendering the same bits); --tune: measure the candidates on the
 //   first frame and keep the fastest (rt_frame.tune)
 //
@@ -159,13 +159,17 @@ int main(int argc, char** argv) {
             return EXIT_FAILURE;
         }
     }
-    static const char* variants[] = {"fast",  "persist", "persist4", "split",  "coop2", "coop4",
-                                     "coop8", "fan",     "chain",    "chain4", "pool"};
+    static const struct {
+        const char* name;
+        int variant;
+    } variants[] = {{"fast", RT_VARIANT_DEFAULT}, {"persist", RT_VARIANT_PERSIST}, {"persist4", RT_VARIANT_PERSIST4},
+                    {"split", RT_VARIANT_SPLIT},  {"coop2", RT_VARIANT_COOP2},     {"coop4", RT_VARIANT_COOP4},
+                    {"coop8", RT_VARIANT_COOP8},  {"fan", RT_VARIANT_FAN},         {"pool", RT_VARIANT_POOL}};
     int kern = a.kernel == "strict" ? RT_KERNEL_STRICT : -1, variant = RT_VARIANT_DEFAULT;
-    for (int v = 0; v < 11 && kern < 0; v++)
-        if (a.kernel == variants[v]) {
+    for (const auto& v : variants)
+        if (kern < 0 && a.kernel == v.name) {
             kern = RT_KERNEL_FAST;
-            variant = v;
+            variant = v.variant;
         }
     if (kern < 0) {
         std::fprintf(stderr, "unknown --kernel %s\n", a.kernel.c_str());

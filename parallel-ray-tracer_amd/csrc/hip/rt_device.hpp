@@ -72,7 +72,7 @@ struct KArgs {
     unsigned long long* counters;  // RT_NCOUNT slots (rt_stats order)
     unsigned int* work;            // persistent-kernel tile / pixel counter
     int n_tiles, tiles_x;
-    int regroup;                   // k_chain: lanes whose walk ended advance together once this many wait
+    int regroup;                   // k_pool: idle lanes of a wave that trigger a refill (rt_frame.regroup)
     unsigned long long* tile_trace;  // diagnostics (PRT_TILE_TRACE): per-tile timeline (rt_kernels.hpp)
     const int* tile_order;           // nullable: k-th dealt tile = tile_order[k] (default: row-major)
     // split pipeline (rt_split.hpp): per (level, tile slot) records, path info, visibility bytes, batches

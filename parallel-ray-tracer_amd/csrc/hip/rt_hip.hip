@@ -24,7 +24,6 @@
 #include "rt_fan.hpp"
 #include "rt_output.hpp"
 #include "rt_split.hpp"
-#include "rt_chain.hpp"
 #include "rt_pool.hpp"
 #include "rt_build.hpp"
 
@@ -643,33 +642,18 @@ int resident(K kernel, int device, int cap = 8, size_t dyn_lds = 0) {
     return std::max(1, std::min(per_cu, cap)) * cus;
 }
 
-// k_persist / k_chain (the persistent one-lane-per-path kernels) in configuration `variant`:
+// k_persist (the persistent one-lane-per-path kernel) in configuration `variant`:
 //   RT_VARIANT_PERSIST   k_persist, <= 168 VGPRs (3 waves per SIMD), path levels in registers;
 //   RT_VARIANT_PERSIST4  k_persist, <= 128 VGPRs (4 waves per SIMD), path levels in a path buffer: in LDS after
 //                        the wide stack sized to the scene's wide depth when 4 workgroups of that fit a CU (LDS
 //                        measured 1.2 % faster than the global slab on dragon, 2.3 % on car_boxed), else global;
-//   RT_VARIANT_CHAIN(4)  k_chain (rt_chain.hpp), 3 (4) waves per SIMD, path levels in LDS.
 // `cap`: workgroups per CU at most (0: the occupancy limit); the grid never exceeds the tiles / 4.
 template <int MAXB>
 void launch_paths(const rtd::KArgs& A, int variant, bool count, int device, hipStream_t s, int cap) {
     const bool batch = A.n_frames > 1;
-    const bool chain = (variant == RT_VARIANT_CHAIN || variant == RT_VARIANT_CHAIN4) && A.s.wide.nodes && A.gstack &&
-                       A.wcap > 0;
     const size_t lds_wide = sizeof(int) * 2 * (size_t)A.wcap * rtd::BLOCK;
     const size_t lds_pb = sizeof(float4) * rtd::BLOCK * MAXB;
     const int cu_cap = cap > 0 ? cap : 8;
-    if (chain) {
-        auto k = count ? rtd::k_chain<MAXB, true, 3, false> : rtd::k_chain<MAXB, false, 3, false>;
-        if (variant == RT_VARIANT_CHAIN4) k = count ? rtd::k_chain<MAXB, true, 4, false> : rtd::k_chain<MAXB, false, 4, false>;
-        if (batch) {
-            k = count ? rtd::k_chain<MAXB, true, 3, true> : rtd::k_chain<MAXB, false, 3, true>;
-            if (variant == RT_VARIANT_CHAIN4) k = count ? rtd::k_chain<MAXB, true, 4, true> : rtd::k_chain<MAXB, false, 4, true>;
-        }
-        const size_t dyn = lds_wide + lds_pb;
-        const int blocks = std::max(1, std::min(resident(k, device, cu_cap, dyn), (A.n_tiles * A.n_frames + 3) / 4));
-        k<<<blocks, rtd::BLOCK, dyn, s>>>(A);
-        return;
-    }
     if (A.tile_trace) {  // diagnostics (PRT_TILE_TRACE): the 3-wave kernel with per-tile timestamps
         auto k = count ? rtd::k_persist<MAXB, false, true, true, 3, true> : rtd::k_persist<MAXB, false, false, true, 3, true>;
         k<<<std::max(1, std::min(resident(k, device, cu_cap), (A.n_tiles + 3) / 4)), rtd::BLOCK, 0, s>>>(A);
@@ -796,7 +780,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     while (g * g < f->spp) g++;
     if (f->spp < 1 || g * g != f->spp || g > 16) return arg_err(ctx, "rt_render: spp must be a square 1..256");
     if (f->kernel < RT_KERNEL_AUTO || f->kernel > RT_KERNEL_FAST) return arg_err(ctx, "rt_render: bad kernel");
-    if (f->variant < RT_VARIANT_DEFAULT || f->variant > RT_VARIANT_POOL || f->tune < 0 || f->tune > 1 ||
+    if (f->variant < RT_VARIANT_DEFAULT || f->variant > RT_VARIANT_POOL || f->variant == 8 || f->variant == 9 ||
+        f->tune < 0 || f->tune > 1 ||
         f->waves_cap < 0 || f->waves_cap > 8 || f->dealing < RT_DEAL_DEFAULT || f->dealing > RT_DEAL_ROW_MAJOR ||
         f->regroup < 0 || f->regroup > 64)
         return arg_err(ctx, "rt_render: bad launch configuration (variant / tune / waves_cap / dealing / regroup)");
@@ -957,7 +942,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         return RT_OK;
     };
     if (int rc = order_for(A.tiles_x, A.n_tiles / A.tiles_x, A.tile_order)) return rc;
-    // XCD-aware dealing of k_persist / k_chain: the centre-out order split into 8 spatial regions, region r
+    // XCD-aware dealing of k_persist / k_pool: the centre-out order split into 8 spatial regions, region r
     // drained first by the workgroups on XCD r (rtd::next_item), so each XCD's L2 holds the part of the scene
     // its region's rays touch. rt_frame.dealing: BLOCKS = 4 x 2 blocks of tiles, ROWS = 8 bands of tile
     // rows, COLUMNS = 8 bands of tile columns, GLOBAL = one counter. Same-box, ms per frame: 16-frame
@@ -1014,7 +999,6 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     if (int rc = regions_for(A.tiles_x, A.n_tiles / A.tiles_x, region_off, region_order)) return rc;
     // RT_KERNEL_FAST launch configurations (rt_frame.variant; every one renders the same bits):
     //   PERSIST / PERSIST4  k_persist, one lane per pixel path, walks in lockstep, 8x8 tiles;
-    //   CHAIN / CHAIN4      k_chain (rt_chain.hpp), one lane per pixel path, each lane's walks back to back;
     //   SPLIT               (1 spp, single frames) closest chains, shadow batches, resolve (rt_split.hpp);
     //   COOP2/4/8           k_coop (rt_coop.hpp): G lanes per ray, 64/G-pixel tiles — shorter chains per tile,
     //                       which is what a frame split over many GPUs (few tiles per wave) is bound by;
@@ -1032,7 +1016,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         if (v == RT_VARIANT_SPLIT) return split_ok;
         if (v == RT_VARIANT_FAN) return fan_ok;
         if (v >= RT_VARIANT_COOP2 && v <= RT_VARIANT_COOP8) return wide_ok;
-        if (v == RT_VARIANT_CHAIN || v == RT_VARIANT_CHAIN4) return wide_ok && !A.tile_trace;
+        if (v == 8 || v == 9) return false;  // (k_chain, removed in round 2)
         if (v == RT_VARIANT_POOL) return wide_ok && !A.tile_trace && A.wcap > 0;
         return true;
     };
@@ -1074,10 +1058,10 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         T.dealing = f->dealing;
         T.cap_req = f->waves_cap;
         // candidates (COOP8 is 3x slower than COOP4 everywhere measured: a variant, not a candidate)
-        const int md[9] = {RT_VARIANT_CHAIN4, RT_VARIANT_CHAIN, RT_VARIANT_PERSIST, RT_VARIANT_PERSIST4,
-                           RT_VARIANT_PERSIST, RT_VARIANT_SPLIT, RT_VARIANT_COOP4, RT_VARIANT_COOP2, RT_VARIANT_FAN};
-        const int cp[9] = {0, 0, 0, 0, 2, 2, 0, 0, 0};
-        for (int i = 0; i < 9 && T.n < rt_ctx::TUNE_MAX; i++)
+        const int md[7] = {RT_VARIANT_PERSIST, RT_VARIANT_PERSIST4, RT_VARIANT_PERSIST, RT_VARIANT_SPLIT,
+                           RT_VARIANT_COOP4,   RT_VARIANT_COOP2,    RT_VARIANT_FAN};
+        const int cp[7] = {0, 0, 2, 2, 0, 0, 0};
+        for (int i = 0; i < 7 && T.n < rt_ctx::TUNE_MAX; i++)
             if (usable(md[i])) {
                 T.mode[T.n] = md[i];
                 T.cap[T.n] = f->waves_cap > 0 ? f->waves_cap : cp[i];
@@ -1104,7 +1088,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             T.pending = false;
             if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1) {
                 static const char* names[] = {"default", "persist", "persist4", "split", "coop2", "coop4",
-                                              "coop8",   "fan",     "chain",    "chain4", "pool"};
+                                              "coop8",   "fan",     "-",        "-",      "pool"};
                 std::fprintf(stderr, "[prt tune] %dx%d b%d spp%d f%d:", T.W, T.rows, T.bounces, T.spp, T.frames);
                 for (int c = 0; c < T.n; c++) std::fprintf(stderr, " %s/%d %.3f ms", names[T.mode[c]], T.cap[c], T.ms[c]);
                 std::fprintf(stderr, " -> %d\n", best);

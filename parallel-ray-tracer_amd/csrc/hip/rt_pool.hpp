@@ -3,8 +3,8 @@
 // k_persist traces one pixel path per lane and runs a wave's 64 walks in lockstep: every closest-hit or shadow
 // walk lasts as long as the wave's slowest lane, and lanes whose path has ended (a miss, kr = 0) or whose shadow
 // ray was skipped (back-facing light) idle through the others' walks. Measured on the bench frame: SIMD efficiency
-// of node steps 0.56. k_chain (rt_chain.hpp) removed the idling by letting each lane run its own
-// walks back to back, but mixed walk kinds and levels in a wave (per-step bookkeeping for both, less coherent
+// of node steps 0.56. k_chain (round 2, removed) removed the idling by letting each lane run its
+// own walks back to back, but mixed walk kinds and levels in a wave (per-step bookkeeping for both, less coherent
 // node loads) and lost.
 //
 // k_pool keeps the walks of ONE kind and ONE level together, and moves the rays instead of the lanes: a
@@ -31,9 +31,35 @@
 // walks, so that only the walk's registers are live during a walk), the queue (4 x 256 ints), occlusion bits
 // (256 ints), control words.
 #pragma once
-#include "rt_chain.hpp"
+#include "rt_kernels.hpp"
 
 namespace rtd {
+
+// the rare strict walks (a zero direction component, an exact tie) out of line, so that their registers do not
+// weigh on the walk loops; counters returned by value
+struct StrictC {  // result of an out-of-line strict closest walk, counters returned by value
+    int orig, nd;
+    float best;
+    unsigned chi, chl, cht, err;
+};
+
+template <bool COUNT>
+__device__ __noinline__ StrictC strict_closest_ool(const DBvh B, v3 o, v3 d, int* __restrict__ bstk) {
+    Ctr c = {};
+    float best = FMAX;
+    int hp = -1, nd = 0;
+    bool tie = false;
+    closest_walk<true, COUNT, true>(B, o, d, best, hp, nd, tie, bstk, c);
+    return StrictC{hp >= 0 ? B.tri_orig[hp] : -1, nd, best, c.chi, c.chl, c.cht, c.err};
+}
+
+template <bool COUNT>
+__device__ __noinline__ unsigned strict_visible_ool(const DBvh B, v3 o, v3 d, float ld2, int* __restrict__ bstk) {
+    // bit 31: visible; bits 0..30: interior visits (COUNT; leaf / triangle counts are not kept)
+    Ctr c = {};
+    const bool v = visible_walk<true, COUNT, true>(B, o, d, ld2, bstk, c);
+    return (v ? 0x80000000u : 0u) | (c.shi & 0x7FFFFFFFu);
+}
 
 constexpr int POOL_QL = 4;  // lights per shadow phase (queue capacity 256 x POOL_QL)
 enum { PC_CNT = 0, PC_HEAD = 20, PC_ITEM = 21, PC_FRAME = 22, PC_N = 32 };
@@ -114,7 +140,7 @@ __device__ __forceinline__ void pool_closest(const DScene& s, const PoolLds& L, 
             sp = 0;
             if (degenerate(d)) {  // the reference's 0/0 NaN slabs: strict walk from the start (out of line)
                 c.fb++;
-                const StrictC sr = chain_strict_closest<COUNT>(s.ref, o, d, bstk);
+                const StrictC sr = strict_closest_ool<COUNT>(s.ref, o, d, bstk);
                 if (COUNT) {
                     c.chi += sr.chi;
                     c.chl += sr.chl;
@@ -168,7 +194,7 @@ __device__ __forceinline__ void pool_closest(const DScene& s, const PoolLds& L, 
                 int orig = hp >= 0 ? W.tri_orig[hp] : -1;
                 if (tie) {  // exact tie: the reference keeps the first triangle found (bvh.c:331), strict re-walk
                     c.fb++;
-                    const StrictC sr = chain_strict_closest<COUNT>(s.ref, o, d, bstk);
+                    const StrictC sr = strict_closest_ool<COUNT>(s.ref, o, d, bstk);
                     if (COUNT) {
                         c.chi += sr.chi;
                         c.chl += sr.chl;
@@ -220,7 +246,7 @@ __device__ __forceinline__ void pool_shadow(const DScene& s, const PoolLds& L, i
             sp = 0;
             if (degenerate(d)) {
                 c.fb++;
-                const unsigned sr = chain_strict_visible<COUNT>(s.ref, o, d, ld2, bstk);
+                const unsigned sr = strict_visible_ool<COUNT>(s.ref, o, d, ld2, bstk);
                 if (COUNT) {
                     c.shi += sr & 0x7FFFFFFFu;
                     c.nb += 8 * (sr & 0x7FFFFFFFu);

@@ -2,7 +2,7 @@
 """Same-box A/B of the fast kernel's launch configurations (rt_frame.variant): bit-exactness against the
 first variant, ray counts, and ms per frame (single frames and frame batches, HIP-event kernel times).
 
-usage: python tools/ab_variants.py [--scene dragon] [--frames 16] [--rounds 3] persist chain4 chain4:regroup=8 ...
+usage: python tools/ab_variants.py [--scene dragon] [--frames 16] [--rounds 3] persist persist4 pool pool:regroup=8 ...
        persist4:up_accel=host persist4:up_ploc_radius=32 (up_*: upload options: the fast walk's BVH)
 """
 import argparse
