@@ -88,8 +88,8 @@ enum {
 
 /* rt_frame.variant: launch configuration of RT_KERNEL_FAST */
 enum {
-    RT_VARIANT_DEFAULT = 0,  /* the library's rule: RT_VARIANT_PERSIST4 for frame batches, RT_VARIANT_PERSIST for single
-                                frames, RT_VARIANT_SPLIT for single 1-spp frames of scenes with >= 3 lights; with
+    RT_VARIANT_DEFAULT = 0,  /* the library's rule: RT_VARIANT_PERSIST4 for frame batches and spp > 1, RT_VARIANT_PERSIST
+                                for single 1-spp frames, RT_VARIANT_SPLIT for single 1-spp frames of scenes with >= 3 lights; with
                                 rt_frame.tune = 1 the measured fastest candidate instead */
     RT_VARIANT_PERSIST = 1,  /* k_persist: one lane per pixel path, walks in lockstep, 3 waves per SIMD */
     RT_VARIANT_PERSIST4 = 2, /* k_persist at 4 waves per SIMD (path levels in LDS) */

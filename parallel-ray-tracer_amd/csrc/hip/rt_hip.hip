@@ -1003,7 +1003,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     //   COOP2/4/8           k_coop (rt_coop.hpp): G lanes per ray, 64/G-pixel tiles — shorter chains per tile,
     //                       which is what a frame split over many GPUs (few tiles per wave) is bound by;
     //   FAN                 k_fan (rt_fan.hpp): 1 + lights lanes per pixel.
-    // Default rule (measured): PERSIST4 for frame batches, PERSIST for single frames, SPLIT for
+    // Default rule (measured): PERSIST4 for frame batches and spp > 1, PERSIST for single frames, SPLIT for
     // single 1-spp frames of scenes with >= 3 lights. rt_frame.tune = 1 measures instead: the first frame of a (scene upload, frame shape) runs each
     // candidate TUNE_REPS times (all into the same outputs), the next frame of that shape reads the timings
     // and keeps the fastest; PRT_TUNE_LOG=1 prints them.
@@ -1022,7 +1022,10 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     };
     int mode = f->variant;
     if (mode == RT_VARIANT_DEFAULT)
-        mode = split_ok && ctx->n_lights >= 3 ? RT_VARIANT_SPLIT : n_frames > 1 ? RT_VARIANT_PERSIST4 : RT_VARIANT_PERSIST;
+        // (a multi-sample frame fills the chip like a batch: car_boxed 4K 64 spp 195 ms at 4 waves vs 219 at 3)
+        mode = split_ok && ctx->n_lights >= 3 ? RT_VARIANT_SPLIT
+               : (n_frames > 1 || f->spp > 1) ? RT_VARIANT_PERSIST4
+                                               : RT_VARIANT_PERSIST;
     if (!usable(mode)) mode = RT_VARIANT_PERSIST;  // (no wide view, or a diagnostics trace)
     int cap = f->waves_cap > 0 ? f->waves_cap : (mode == RT_VARIANT_SPLIT ? 2 : 0);
     const bool tunable = kernel == RT_KERNEL_FAST && f->tune == 1 && f->variant == RT_VARIANT_DEFAULT && !A.tile_trace;
