@@ -270,6 +270,12 @@ __device__ __forceinline__ bool visible_walk(const DBvh& B, v3 o, v3 d, float ld
 // Same result semantics as closest_walk<false>: min t over all triangles, boxes pruned at
 // best * PRUNE_SLACK so that exact ties are always met and reported.
 constexpr int WSTACK = 16;  // node-group entries (2 ints) in the STACK-int LDS column; builder depth <= 16
+// Shadow walks visit a node's hit children FAR first (visiting order k ^ (octant ^ 7): from the light's side
+// toward the ray origin; the closest walks stay near-first). An any-hit walk's result does not depend on the
+// order; far-first meets an occluder sooner on average — a shadow ray leaves a surface whose own neighbourhood
+// (first in near-first order) cannot occlude it. Same box, 16-frame batches: dragon 0.810 -> 0.804 ms per
+// frame, car_boxed 0.922 -> 0.884, sportscar 1.374 -> 1.334; wave steps -2 / -5 / -4 %.
+constexpr unsigned SHADOW_ORDER_XOR = 7u;
 
 // 1 in the lowest active lane of the wave, 0 elsewhere (wave-level step counting)
 __device__ __forceinline__ unsigned first_active_lane() {
@@ -291,7 +297,8 @@ __device__ __forceinline__ WNode wload(const DWide& W, int node) {
 
 template <bool COUNT>
 __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsigned oct, float lim, unsigned& nh,
-                                          unsigned& th, int& cbase, int& tbase, unsigned& imask, unsigned& nleaf) {
+                                          unsigned& th, int& cbase, int& tbase, unsigned& imask, unsigned& nleaf,
+                                          unsigned ord_xor = 0u) {
     const float4 f0 = nd.f0, f1 = nd.f1, f2 = nd.f2, f3 = nd.f3, f4 = nd.f4;
     const unsigned e = __float_as_uint(f0.w);
     const float sx = __uint_as_float((e & 0xFFu) << 23), sy = __uint_as_float(((e >> 8) & 0xFFu) << 23),
@@ -332,9 +339,10 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
     // interior hits, permuted into visiting order: bit k = slot k ^ oct (XOR by oct swaps bits, pairs and
     // nibbles of the 8-bit mask)
     unsigned x = hit8 & imask;
-    x = (oct & 1u) ? (((x & 0x55u) << 1) | ((x >> 1) & 0x55u)) : x;
-    x = (oct & 2u) ? (((x & 0x33u) << 2) | ((x >> 2) & 0x33u)) : x;
-    x = (oct & 4u) ? (((x & 0x0Fu) << 4) | ((x >> 4) & 0x0Fu)) : x;
+    const unsigned ord = oct ^ ord_xor;  // visiting order k ^ ord (ord_xor 7: far children first)
+    x = (ord & 1u) ? (((x & 0x55u) << 1) | ((x >> 1) & 0x55u)) : x;
+    x = (ord & 2u) ? (((x & 0x33u) << 2) | ((x >> 2) & 0x33u)) : x;
+    x = (ord & 4u) ? (((x & 0x0Fu) << 4) | ((x >> 4) & 0x0Fu)) : x;
     nh = x;
     // triangles of the hit leaf slots (meta = count << 5 | offset; an empty slot's inverted box never
     // passes the test above except through underflow, and its meta 0 adds nothing then)
@@ -464,14 +472,14 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
     for (;;) {
         unsigned nh, th, imask, nl;
         int cb, tb;
-        wide_node<COUNT>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nl);
+        wide_node<COUNT>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nl, SHADOW_ORDER_XOR);
         if (COUNT) {
             c.shi++;
             c.shl += nl;
             c.nb += 10;
             c.ws += first_active_lane();
         }
-        const int next = wide_next(nh, cb, imask, oct, sp, stk, wcap);
+        const int next = wide_next(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
         if (next >= 0) N = wload(W, next);
         if (!PIPE) {
             while (th) {

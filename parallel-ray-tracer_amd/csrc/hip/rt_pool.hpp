@@ -267,14 +267,14 @@ __device__ __forceinline__ void pool_shadow(const DScene& s, const PoolLds& L, i
         if (r >= 0) {  // visible_wide's step
             unsigned nh, th, imask, nl;
             int cb, tb;
-            wide_node<COUNT>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nl);
+            wide_node<COUNT>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nl, SHADOW_ORDER_XOR);
             if (COUNT) {
                 c.shi++;
                 c.shl += nl;
                 c.nb += 10;
                 c.ws += first_active_lane();
             }
-            const int next = wide_next(nh, cb, imask, oct, sp, L.stk + threadIdx.x, wcap);
+            const int next = wide_next(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, L.stk + threadIdx.x, wcap);
             if (next >= 0) N = wload(W, next);
             bool occl = false;
             while (th) {
