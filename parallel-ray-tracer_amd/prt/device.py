@@ -50,14 +50,25 @@ def gather(renderers, root=0, out=None):
     [frames, H, W, 3] f32 or [frames, H, W] int32 (BGRA8)."""
     arr = (ctypes.c_void_p * len(renderers))(*[r._ctx.value for r in renderers])
     if out is not None:
-        assert out.is_cuda and out.is_contiguous()
-        rc = _L.rt_gather_to(arr, len(renderers), root, ctypes.c_void_p(out.data_ptr()))
+        rc = _L.rt_gather_to(arr, len(renderers), root, ctypes.c_void_p(_gather_out(renderers[root], out)))
     else:
         rc = _L.rt_gather(arr, len(renderers), root)
     r = renderers[root]
     r._chk(rc, "rt_gather")
     W, H = r._size
     r._last = (W, H)
+
+
+def _gather_out(r, out):
+    """device pointer of a gather's full-frame output tensor: contiguous, f32 (rgb) or int32 (BGRA8), on the
+    root's device, and at least one full frame of that format (rt_gather_to / rt_comm_gather write the
+    root's last render's frame count; a short tensor is refused here rather than overrun on the device)"""
+    import torch
+    W, H = r._size
+    per = {torch.float32: 3, torch.int32: 1}.get(getattr(out, "dtype", None))
+    if per is None:
+        raise RtError("gather out: expected a float32 (rgb) or int32 (bgra8) torch tensor")
+    return _ptr(out, "gather out", W * H * per, (out.dtype,), r.device)
 
 
 COMM_ID_BYTES = 128  # RT_COMM_ID_BYTES
@@ -96,8 +107,8 @@ class Comm:
         buffer (its download() / download_bmp() then read the full frame)."""
         ptr = None
         if out is not None:
-            assert out.is_cuda and out.is_contiguous()
-            ptr = ctypes.c_void_p(out.data_ptr())
+            ptr = ctypes.c_void_p(_gather_out(self._r[root - self.rank0] if 0 <= root - self.rank0 < len(self._r)
+                                              else self._r[0], out))
         rc = _L.rt_comm_gather(self._c, root, ptr)
         if rc != 0:
             raise RtError(f"rt_comm_gather: {rc} ({_L.rt_comm_last_error(self._c).decode()})")

@@ -25,6 +25,19 @@ def test_output_tensors_are_checked_before_any_launch():
     assert device._ptr(1234, "rgb", 12, f32, 0) == 1234  # a raw device pointer is the caller's responsibility
 
 
+def test_gather_output_tensor_is_checked():
+    """rt_gather_to / rt_comm_gather's full-frame output: one W*H frame of rgb f32 or BGRA8 int32 at least"""
+    class Root:  # the root Renderer's size and device, as prt.device.Renderer keeps them
+        _size, device = (4, 2), 0
+
+    with pytest.raises(device.RtError, match="elements"):
+        device._gather_out(Root(), torch.zeros(4 * 2 * 3 - 1, dtype=torch.float32))
+    with pytest.raises(device.RtError, match="float32 .rgb. or int32"):
+        device._gather_out(Root(), torch.zeros(4 * 2, dtype=torch.int64))
+    with pytest.raises(device.RtError, match="expected cuda:0"):
+        device._gather_out(Root(), torch.zeros(4 * 2, dtype=torch.int32))
+
+
 def test_variant_and_dealing_names_match_the_header():
     """prt.device's names for rt_frame.variant / rt_frame.dealing follow include/rt_hip.h's enums"""
     import os
