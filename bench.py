@@ -181,7 +181,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=64, help="timed frames")
     ap.add_argument("--warmup", type=int, default=16, help="untimed frames (after the tuning launches)")
-    ap.add_argument("--frames", type=int, default=16, help="frames per launch (at most --steps)")
+    ap.add_argument("--frames", type=int, default=0,
+                    help="frames per launch, at most --steps (0: 32 at N = 1, 16 at N > 1, where two streams' "
+                         "alternating launches and the ping-pong gathers want at least two launches)")
     ap.add_argument("--streams", type=int, default=0, help="contexts on their own streams, launches alternating "
                     "(0: 1 at N = 1, 2 at N > 1)")
     ap.add_argument("--row-block", type=int, default=0,
@@ -285,7 +287,10 @@ def main():
     K = args.steps
     # launches covering exactly K frames, as few as --frames allows and of (nearly) equal size: K = 20 at 16
     # frames per launch is 10 + 10, not 16 + 4 (a 4-frame launch is tail-bound: 1.3 vs 0.93 ms per frame)
-    n_launch = -(-K // max(1, min(args.frames, K)))
+    # (N = 1, K = 20, same box: one 20-frame launch 0.813 ms per frame vs 10 + 10 0.845: the launch tail, its
+    # longest reflection chains, is paid once)
+    frames_cap = args.frames or (32 if world == 1 else 16)
+    n_launch = -(-K // max(1, min(frames_cap, K)))
     plan = [K // n_launch + (1 if i < K % n_launch else 0) for i in range(n_launch)]
     F = plan[0]
     # rows: 8-row blocks dealt cyclically to the ranks (an 8x8 tile of a rank's rows is an 8x8 tile of the
