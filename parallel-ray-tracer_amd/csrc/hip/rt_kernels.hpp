@@ -409,7 +409,7 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
                 const int i = tb + __builtin_ctz(th);
                 th &= th - 1u;
                 int k;
-                const float tt = hit_triangle(o, d, W.tris + 3 * i, k);
+                const float tt = hit_triangle<true>(o, d, W.tris + 3 * i, k);
                 if (COUNT) c.cht++;
                 if (tt < best) {
                     best = tt;
