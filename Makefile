@@ -48,3 +48,9 @@ oracle:
 clean:
 	rm -rf $(LIB) $(BIN)
 	$(MAKE) -C oracle clean
+
+# exhaustive check of rtd::rcp_ieee against IEEE division (test infrastructure, tests/test_gpu_rcp.py)
+RCP_CHECK := tools/rcp/rcp_exhaustive
+hip: $(RCP_CHECK)
+$(RCP_CHECK): tools/rcp/rcp_exhaustive.hip $(CSRC)/hip/rt_device.hpp
+	$(HIPCC) $(HIP_FLAGS) -o $@ $<

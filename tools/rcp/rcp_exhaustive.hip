@@ -1,23 +1,27 @@
-// Exhaustive check (every finite normal float, both signs) that rcp_ieee(x) -- v_rcp_f32 plus one FMA
-// Newton-Markstein correction -- equals the correctly rounded 1.0f / x (the reference's division in
-// hit_triangle, raytracer.c:35-59). Reports the mismatches per exponent range. Test infrastructure only.
-#include <hip/hip_runtime.h>
+// Exhaustive check (every finite normal float, both signs) of the fast reciprocal: (a) the bare
+// v_rcp_f32 + one FMA (Markstein) correction against the correctly rounded 1.0f / x (the reference's
+// division in hit_triangle, raytracer.c:35-59), reporting the mismatches per exponent field, and (b) the
+// product's rtd::rcp_ieee (which divides above 2^125), which must have none. Exit 0 iff (b) has none.
+// Built by the Makefile (tools/rcp/rcp_exhaustive), run by tests/test_gpu_rcp.py. Test infrastructure only.
 #include <cstdio>
 #include <cstdint>
 
-__device__ __forceinline__ float rcp_fast(float x) {
+#include "hip/rt_device.hpp"  // rtd::rcp_ieee, the product's function itself
+
+__device__ __forceinline__ float rcp_bare(float x) {
     const float r = __builtin_amdgcn_rcpf(x);
-    const float e = __builtin_fmaf(-x, r, 1.0f);
-    return __builtin_fmaf(e, r, r);
+    return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
 }
 
-__global__ void k(uint32_t base, unsigned long long* bad, uint32_t* first, unsigned* hist) {
+__global__ void k(uint32_t base, unsigned long long* bad, uint32_t* first, unsigned* hist,
+                  unsigned long long* bad_product) {
     const uint32_t i = base + blockIdx.x * 256u + threadIdx.x;
     const uint32_t bits = i;
     const uint32_t ex = (bits >> 23) & 0xFF;
     if (ex == 0 || ex == 0xFF) return;  // denormals, inf/nan: outside the kernel's |det| >= EPS range
     const float x = __uint_as_float(bits);
-    const float a = 1.0f / x, b = rcp_fast(x);
+    const float a = 1.0f / x, b = rcp_bare(x), c = rtd::rcp_ieee(x);
+    if (__float_as_uint(a) != __float_as_uint(c)) atomicAdd(bad_product, 1ull);
     if (__float_as_uint(a) != __float_as_uint(b)) {
         const unsigned long long n = atomicAdd(bad, 1ull);
         atomicAdd(hist + ex, 1u);
@@ -29,23 +33,29 @@ int main() {
     unsigned long long* bad;
     uint32_t* first;
     unsigned* hist;
-    hipMalloc(&bad, 8);
-    hipMalloc(&first, 64);
-    hipMalloc(&hist, 256 * 4);
-    hipMemset(bad, 0, 8);
-    hipMemset(first, 0, 64);
-    hipMemset(hist, 0, 1024);
+    unsigned long long* badp;
+    (void)hipMalloc(&badp, 8);
+    (void)hipMemset(badp, 0, 8);
+    (void)hipMalloc(&bad, 8);
+    (void)hipMalloc(&first, 64);
+    (void)hipMalloc(&hist, 256 * 4);
+    (void)hipMemset(bad, 0, 8);
+    (void)hipMemset(first, 0, 64);
+    (void)hipMemset(hist, 0, 1024);
     const uint32_t chunk = 1u << 28;
-    for (uint64_t b = 0; b < (1ull << 32); b += chunk) k<<<chunk / 256, 256>>>((uint32_t)b, bad, first, hist);
+    for (uint64_t b = 0; b < (1ull << 32); b += chunk) k<<<chunk / 256, 256>>>((uint32_t)b, bad, first, hist, badp);
     if (hipDeviceSynchronize() != hipSuccess) { printf("hip error\n"); return 2; }
     unsigned long long nb;
     uint32_t f[16];
     unsigned h[256];
-    hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost);
-    hipMemcpy(f, first, 64, hipMemcpyDeviceToHost);
-    hipMemcpy(h, hist, 1024, hipMemcpyDeviceToHost);
-    printf("mismatches %llu of all normal floats (both signs)\n", nb);
+    (void)hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(f, first, 64, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(h, hist, 1024, hipMemcpyDeviceToHost);
+    unsigned long long np_;
+    (void)hipMemcpy(&np_, badp, 8, hipMemcpyDeviceToHost);
+    printf("rcp_ieee (product) mismatches %llu of all normal floats (both signs)\n", np_);
+    printf("bare rcp + FMA mismatches %llu of all normal floats (both signs)\n", nb);
     for (int i = 0; i < 16 && i < (int)nb; i++) printf("  0x%08x %g\n", f[i], (double)*(float*)&f[i]);
     for (int e = 0; e < 256; e++) if (h[e]) printf("  exponent field %d: %u\n", e, h[e]);
-    return nb ? 1 : 0;
+    return np_ ? 1 : 0;
 }
