@@ -149,7 +149,8 @@ __device__ __forceinline__ void store_px(float* __restrict__ rgb, unsigned* __re
 // rcp_exhaustive.hip: the only mismatches are |x| >= 2^126, denormal results) -- in 3 instructions instead of
 // the division's scale / fmas / fixup sequence; above 2^125 the division itself. Used by the closest walks'
 // triangle tests (FAST_RCP): same box, dragon 0.801 vs 0.803 ms per frame, car_boxed 0.870 vs 0.882, sportscar
-// 1.328 vs 1.332; in the shadow walks too it cost dragon 2.5 % (profiles/r2l/ab_fast_reciprocal*.txt).
+// 1.328 vs 1.332; in the shadow walks too it cost dragon 2.5 % (profiles/r2l/ab_fast_reciprocal*.txt). Also
+// ray_pre's 1/d of every walk: dragon 0.796 vs 0.803, car_boxed 0.864 vs 0.871.
 __device__ __forceinline__ float rcp_ieee(float x) {
     if (__builtin_fabsf(x) > 0x1p125f) return 1.0f / x;
     const float r = __builtin_amdgcn_rcpf(x);
@@ -200,9 +201,9 @@ struct RayPre {
 __device__ __forceinline__ float safe_dir(float x) { return __builtin_fabsf(x) < 1e-20f ? 1e-20f : x; }
 __device__ __forceinline__ RayPre ray_pre(v3 o, v3 d) {
     RayPre p;
-    p.ix = 1.0f / safe_dir(d.x);
-    p.iy = 1.0f / safe_dir(d.y);
-    p.iz = 1.0f / safe_dir(d.z);
+    p.ix = rcp_ieee(safe_dir(d.x));
+    p.iy = rcp_ieee(safe_dir(d.y));
+    p.iz = rcp_ieee(safe_dir(d.z));
     p.ox = o.x * p.ix;
     p.oy = o.y * p.iy;
     p.oz = o.z * p.iz;
