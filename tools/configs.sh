@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 run() {  # name args...
     local n=$1; shift
-    PRT_TUNE_LOG=1 timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > gpurun_out/cfg_$n.log 2>&1
+    PRT_TUNE_LOG=1 timeout -k 10 300 python bench.py --no-cpu-baseline --frames 16 "$@" > gpurun_out/cfg_$n.log 2>&1
     local rc=$?
     echo "$n rc=$rc"
     [ $rc -eq 0 ] || exit $rc
