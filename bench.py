@@ -50,6 +50,11 @@ def alg_bytes(st, pixels, n_lights, px_bytes=12):
     return nodes + 48 * tri + (84 + 32 * n_lights) * st["hits"] + px_bytes * pixels
 
 
+def pmc_key(scene, W, H, spp, kernel, bvh, output, frames, world):
+    """profiles/pmc_traffic.json key of one bench configuration (tools/pmc_traffic.py writes the same)"""
+    return f"{scene}_{W}x{H}_spp{spp}_{kernel}_{bvh}_{output}_f{frames}_n{world}"
+
+
 def data_note(name, n_tris, is_standin):
     if name.startswith("random"):
         return (f"synthetic: the reference's random-triangle mode (cpu/src/main.c:115-131, srand(1)), {n_tris} "
@@ -176,6 +181,18 @@ def cpu_baseline(scene_files, W, H, gpu_rays_for_rows, args, threads):
     return out
 
 
+def spawn_ranks(n):
+    """torch.distributed.run with n ranks on this node (rendezvous on 127.0.0.1, a free port) as a child
+    process running this same command line; returns its exit status (non-zero if any rank failed)"""
+    import socket
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -224,16 +241,25 @@ def main():
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--bmp", default="", help="after timing, rank 0 writes the last frame (gathered) as a BMP "
                     "(bmp_write_file's bytes; from the device-quantised pixels with --output bgra8)")
+    ap.add_argument("--gather", choices=("auto", "native", "torch"), default="auto",
+                    help="N > 1: how frames reach rank 0 — native: the library's RCCL gather (rt_comm_init_rank / "
+                         "rt_comm_gather, one communicator per context; torch.distributed only hands out the ids); "
+                         "torch: torch.distributed.gather of the compact blocks (prt.dist.FrameGather); auto: native "
+                         "on RCCL, torch on gloo (the one-GPU rehearsal: RCCL refuses two ranks on one device)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` without a launcher: start the N ranks as CHILD processes (one per GPU, before
+        # this process touches any GPU) and relay their exit status; rank 0 prints the line on the shared stdout
+        sys.exit(spawn_ranks(args.gpus))
 
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if args.gpus != world:  # never a silent one-GPU run labelled N: N ranks come from the launcher
-        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N ranks with "
-                 f"`python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}`")
+    if args.gpus != world:  # never a silent one-GPU run labelled N
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal of the multi-rank flow on a one-GPU box (never set by the driver): PRT_DIST_ONE_GPU=1 puts
     # every rank on device 0, PRT_DIST_BACKEND=gloo replaces RCCL (which refuses two ranks on one GPU)
@@ -251,7 +277,7 @@ def main():
             dist.init_process_group(backend)
 
     from prt import device, host
-    from prt.dist import FrameGather
+    from prt.dist import FrameGather, NativeGather
     from prt.scenes import is_standin, scene_paths
 
     W, H = args.width, args.height
@@ -303,18 +329,49 @@ def main():
                      like=torch.empty(0, dtype=torch.int32 if bgra else torch.float32, device="cuda"),
                      frames=F, buffers=2, block=B, rotate=not args.no_rotate)
 
+    # N > 1: the frames reach rank 0 through the library's own RCCL gather (rt_comm_gather) unless --gather torch or
+    # the gloo rehearsal; a native gather that cannot start, or whose frames differ from one GPU's at setup, is
+    # replaced by torch.distributed's and the line says so (config.gather)
+    gmode = ("native" if args.gather == "native" else "none") if world == 1 else \
+        (args.gather if args.gather != "auto" else ("native" if backend == "nccl" else "torch"))
+    gather_note = {"none": "single GPU", "torch": "torch.distributed.gather of the compact row blocks (prt.dist."
+                   "FrameGather)", "native": "rt_comm_gather (the library's RCCL send/recv group, one communicator per "
+                   "context; prt.dist.NativeGather)"}[gmode]
+    ng = None
+    if gmode == "native":
+        err = ""
+        try:
+            ng = NativeGather(rends, H, W, 1 if bgra else 3, rank, world, dist, like=fg.blocks[0], frames=F, block=B,
+                              rotate=not args.no_rotate)
+        except Exception as e:  # e.g. RCCL not loadable: every rank sees the same
+            err = repr(e)
+        errs = [err]
+        if dist:
+            errs = [None] * world
+            dist.all_gather_object(errs, err)
+        if any(errs):
+            if ng:
+                ng.close()
+            ng, gmode = None, "torch"
+            gather_note = "torch.distributed.gather (native rt_comm_init_rank failed: " + next(e for e in errs if e) + ")"
+
     def out(blk):  # the kernel's output argument for a gather block
         return {"bgra": blk} if bgra else {"rgb": blk}
     my_rows = fg.rows()
     n_r = my_rows[2]
     launch_no = [0]
-    latest = [0, 0]  # (block, frames) of the latest launch
+    latest = [0, 0, 0]  # (block, frames, context) of the latest launch
 
     def launch(nf):
         b = launch_no[0] % 2
         c = launch_no[0] % n_streams
         launch_no[0] += 1
-        latest[:] = [b, nf]
+        latest[:] = [b, nf, c]
+        if gmode == "native":  # render, then the gather on the context's stream (ordered after the render)
+            rends[c].render_frames(path(nf), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
+                                   kernel=args.kernel, variant=args.variant, tune=args.tune, **out(ng.target(c)[:nf]))
+            ng.gather(c, nf)
+            return
         with torch.cuda.stream(streams[c]):  # block b is rendered by context c on its stream
             if fg.pending(b):
                 fg.finish(b)
@@ -323,6 +380,8 @@ def main():
             fg.start(b)
 
     def drain():
+        if gmode == "native":
+            return  # ordered on the contexts' streams (the caller synchronises)
         for b in ((latest[0] + 1) % 2, latest[0]):  # launch order: rank 0's frame ends as the latest batch
             with torch.cuda.stream(streams[b % n_streams]):
                 if fg.pending(b):
@@ -337,6 +396,30 @@ def main():
         for _ in range(2 * n_streams):  # per context: the tuning launch, then the launch reading its timings
             launch(nf)
         rays_of[nf] = rends[(launch_no[0] - 1) % n_streams].stats()["rays"]
+    if gmode == "native":  # untimed check of the native gather: rank 0's gathered frames == one GPU's frames
+        drain()
+        torch.cuda.synchronize()
+        same = True
+        if rank == 0:
+            nf, c = latest[1], latest[2]
+            rv = device.Renderer(local, stream=stream)
+            rv.upload(scene, accel=args.accel, ploc_radius=args.ploc_radius)
+            ref = torch.zeros_like(ng.frames_of(c)[:nf])
+            rv.render_frames(path(nf), W, H, bounces=args.bounces, spp=args.spp, kernel=args.kernel, **out(ref))
+            torch.cuda.synchronize()
+            rv.close()
+            same = bool(torch.equal(ref, ng.frames_of(c)[:nf]))
+        flag = [same]
+        if dist:
+            dist.broadcast_object_list(flag, src=0)
+        if not flag[0]:
+            ng.close()
+            ng, gmode = None, "torch"
+            gather_note = "torch.distributed.gather (native rt_comm_gather's frames differed from one GPU's at setup)"
+            for nf in sorted(set(plan)):
+                launch(nf)
+        else:
+            gather_note += "; checked at setup: rank 0's gathered frames equal one GPU's"
     for _ in range(max(1, -(-args.warmup // F))):
         launch(F)
     drain()
@@ -369,7 +452,7 @@ def main():
     assert rends[timed[-1][0]].stats()["rays"] == rays_of[plan[-1]]  # (deterministic: the same launch, again)
     rays_local = sum(rays_of[nf] for nf in plan)
     if args.bmp and rank == 0:  # the BMP written from the root rank (untimed): frame 0 = the reference camera
-        frames = fg.frame if world > 1 else fg.target(latest[0])
+        frames = ng.frames_of(latest[2]) if gmode == "native" else (fg.frame if world > 1 else fg.target(latest[0]))
         px = (frames if frames.dim() == 3 else frames[0]).cpu().numpy()
         data = host.bmp_from_bgra(px) if bgra else host.bmp_encode(px)
         with open(args.bmp, "wb") as fbmp:
@@ -407,17 +490,33 @@ def main():
         dist.all_reduce(lat, op=dist.ReduceOp.MAX)
 
     if rank == 0:
-        traffic, pmc = None, {}
+        # PMC counters of THIS configuration, measured by tools/profile.sh on launches of THIS many frames with
+        # THIS library build (pmc_key / lib_md5); anything else is reported under pmc_stale, never as measured
+        pmc, pmc_stale = {}, None
+        key = pmc_key(args.scene, W, H, args.spp, args.kernel, args.bvh, args.output, F, world)
         if os.path.exists(args.traffic_json):
             try:
-                tj = json.load(open(args.traffic_json))
-                key = f"{args.scene}_{W}x{H}_{args.kernel}_{args.bvh}" + ("_bgra8" if bgra else "")
-                if key in tj:  # measured on 16-frame launches (tools/profile.sh): per frame x this launch's frames
-                    pmc = tj[key]
-                    traffic = pmc["hbm_bytes_per_frame"] * F if "hbm_bytes_per_frame" in pmc else pmc["hbm_bytes_per_launch"]
-            except Exception:
-                traffic = None
+                ent = json.load(open(args.traffic_json)).get(key)
+            except (OSError, ValueError):
+                ent = None
+            if ent is not None:
+                if ent.get("lib_md5") == device.lib_md5():
+                    pmc = ent
+                else:
+                    pmc_stale = {"source": ent.get("source"), "reason": "measured on another librt_hip.so build"}
+        traffic = pmc.get("hbm_bytes_per_launch")
         achieved = bytes_launch / (k_avg_ms / 1e3) / 1e9
+        valu = pmc.get("valu_issue_frac")
+        if traffic is None:
+            bound_measured, limiter = None, "unmeasured: no PMC profile of this configuration and build (tools/profile.sh)"
+        elif traffic < 0.05 * bytes_launch and valu is not None:
+            bound_measured = "latency/VALU"
+            limiter = (f"dependent-load latency and VALU issue: HBM traffic is {traffic / bytes_launch:.1%} of the "
+                       "algorithmic bytes (the scene is L2/MALL-resident), VALU issues "
+                       f"{valu:.0%} of the cycles, of which {simd_eff:.0%} of the lanes do node work")
+        else:
+            bound_measured = "hbm" if traffic / (k_avg_ms / 1e3) / 1e9 > 0.5 * HBM_PEAK_GBS else "mixed"
+            limiter = "see DESIGN.md §5"
         result = {
             "metric": METRIC,
             "value": rays_total / elapsed / 1e6,
@@ -437,7 +536,7 @@ def main():
                        "scene": args.scene, "triangles": scene.n_triangles, "lights": len(scene.lights),
                        "width": W, "height": H, "bvh": args.bvh, "accel": args.accel, "kernel": args.kernel,
                        "rays_per_frame": rays_frame, "output": args.output, "parallelism": f"{B}-row blocks cyclic x{world} + RCCL gather"
-                       if world > 1 else "single GPU", "frames_per_launch": F,
+                       if world > 1 else "single GPU", "frames_per_launch": F, "gather": gather_note,
                        "accel_built": info["accel_built"], "accel_build_ms": info["build_ms"],
                        "wide_depth": info["wide_depth"]},
             "frame_latency_ms": lat.item(),
@@ -451,22 +550,36 @@ def main():
                          "survey_achieved": survey_launch / (k_avg_ms / 1e3) / 1e9,
                          "survey_frac": survey_launch / (k_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                          "simd_efficiency": simd_eff,
+                         # the launch's work per ray (RT_FLAG_COUNTERS): wide-node visits, leaf slots and
+                         # triangle tests of the closest (primary + reflection) and the shadow walks
+                         "per_ray": {"closest_nodes": stc["ch_inner"] / max(1, stc["primary"] + stc["reflection"]),
+                                     "closest_leaves": stc["ch_leaf"] / max(1, stc["primary"] + stc["reflection"]),
+                                     "closest_tris": stc["ch_tri"] / max(1, stc["primary"] + stc["reflection"]),
+                                     "shadow_nodes": stc["sh_inner"] / max(1, stc["shadow"]),
+                                     "shadow_leaves": stc["sh_leaf"] / max(1, stc["shadow"]),
+                                     "shadow_tris": stc["sh_tri"] / max(1, stc["shadow"]),
+                                     "wave_steps_per_frame": stc["wave_steps"] / F,
+                                     "strict_fallbacks": stc["fallbacks"]},
                          # measured by rocprofv3 PMC passes of this command (profiles/pmc_traffic.json)
                          "hbm_frac_measured": (traffic / (k_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                         "valu_issue_frac": pmc.get("valu_issue_frac"),
+                         "traffic_over_pixels": (traffic / (F * W * n_r * (4 if bgra else 12))) if traffic else None,
+                         "valu_issue_frac": valu,
+                         # the measured bound: the share of the SIMDs' peak lane-issue that does useful node work
+                         "issue_frac": (valu * simd_eff) if valu is not None else None,
                          "wave_wait_frac": pmc.get("wave_wait_frac"),
                          "l2_hit_rate": pmc.get("l2_hit_rate"),
-                         "l2_read_bytes_per_launch": (pmc["l2_read_bytes_per_launch"] / pmc.get("frames_per_launch", 16) * F)
-                                                     if pmc.get("l2_read_bytes_per_launch") else None,
-                         "pmc_source": pmc.get("source"),
+                         "fetch_bytes_per_launch": pmc.get("fetch_bytes_per_launch"),
+                         "write_bytes_per_launch": pmc.get("write_bytes_per_launch"),
+                         "l2_read_bytes_per_launch": pmc.get("l2_read_bytes_per_launch"),
+                         "pmc_key": key, "pmc_source": pmc.get("source"), "pmc_stale": pmc_stale,
+                         "pmc_trace_avg_ms": pmc.get("trace_avg_ms"),
                          # what binds the kernel, measured (the contract's `bound` names the priced roofline)
-                         "bound_measured": ("latency/VALU" if traffic and traffic < 0.05 * bytes_launch else "hbm"),
-                         "limiter": ("dependent-load latency and VALU issue (HBM traffic is ~1 % of the algorithmic "
-                                     "bytes: the scene is L2/MALL-resident)") if traffic and traffic < 0.05 * bytes_launch
-                                    else "see DESIGN.md §5",
+                         "bound_measured": bound_measured, "limiter": limiter,
                          "note": "achieved / frac: algorithmic bytes (the node / triangle / shading records the kernel "
-                                 "reads, DESIGN.md §5) of one launch / its HIP-event duration. These are cache bytes, "
-                                 "not HBM bytes: hbm_frac_measured is the HBM share (FETCH_SIZE x 2 + WRITE_SIZE)"},
+                                 "reads, DESIGN.md §5) of one launch / its HIP-event duration. They are served by L1/L2/"
+                                 "MALL, not HBM, so frac is not a bound: it exceeds 1 on scenes with more bytes per ray "
+                                 "(car_boxed, 64 spp). hbm_frac_measured is the HBM share (2 x FETCH_SIZE + WRITE_SIZE, "
+                                 "PMC); issue_frac = valu_issue_frac x simd_efficiency is the measured bound"},
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, usable_cpus())
@@ -492,6 +605,8 @@ def main():
             except Exception as e:  # reported, never silently replaced
                 result["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(result), flush=True)
+    if ng:
+        ng.close()
     for rr_ in rends:
         rr_.close()
     if dist:

@@ -73,7 +73,7 @@ enum {
 typedef struct rt_scene_info {
     int n_triangles, n_lights;
     int wide_nodes, wide_depth; /* the fast walk's 8-wide BVH (0: none, the binary fast walk) */
-    int accel_built;            /* RT_ACCEL_* of the fast walk's BVH as built (RT_ACCEL_AUTO = host binned SAH) */
+    int accel_built;            /* RT_ACCEL_* of the fast walk's BVH as built (RT_ACCEL_HOST = host binned SAH, RT_ACCEL_GPU = PLOC on the device) */
     float build_ms;             /* host wall time of the acceleration build (binary tree + wide collapse) */
     float gpu_build_ms;         /* of which the GPU tree build (RT_ACCEL_GPU; incl. transfers) */
 } rt_scene_info;

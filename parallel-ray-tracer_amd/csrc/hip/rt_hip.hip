@@ -345,8 +345,11 @@ int gpu_ploc(rt_ctx* ctx, const rt_triangle* T, int n, int R, std::vector<rt_bvh
         *keep = nullptr, *moff = nullptr, *koff = nullptr, *left = nullptr, *right = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
+    int* tot = nullptr;  // pinned: a merge round's merge and survivor totals
     int rc = RT_OK;
     auto done = [&]() {
+        if (tot) (void)hipHostFree(tot);
+        tot = nullptr;
         for (void* p : {(void*)dv, (void*)plo, (void*)phi, (void*)nlo, (void*)nhi, (void*)keys, (void*)keys2, (void*)vals,
                         (void*)sorted, (void*)cb, (void*)C, (void*)C2, (void*)nnb, (void*)mflag, (void*)keep, (void*)moff,
                         (void*)koff, (void*)left, (void*)right, tmp})
@@ -388,7 +391,6 @@ int gpu_ploc(rt_ctx* ctx, const rt_triangle* T, int n, int R, std::vector<rt_bvh
     rtb::k_leaves<<<g, 256, 0, st>>>(sorted, plo, phi, n, nlo, nhi, C);
     PLOC(hipGetLastError());
     int m = n, next = n;
-    int* tot = nullptr;  // pinned: the round's merge and survivor totals
     PLOC(hipHostMalloc((void**)&tot, sizeof(int) * 4, hipHostMallocDefault));
     while (m > 1) {
         const int gm = (m + 255) / 256;
@@ -407,7 +409,6 @@ int gpu_ploc(rt_ctx* ctx, const rt_triangle* T, int n, int R, std::vector<rt_bvh
         PLOC(hipStreamSynchronize(st));
         const int merges = tot[0] + tot[1], survivors = tot[2] + tot[3];
         if (merges <= 0 || survivors != m - merges) {  // no progress: never expected (a mutual pair always exists)
-            (void)hipHostFree(tot);
             rc = RT_E_STATE;
             return done();
         }
@@ -415,7 +416,6 @@ int gpu_ploc(rt_ctx* ctx, const rt_triangle* T, int n, int R, std::vector<rt_bvh
         m = survivors;
         std::swap(C, C2);
     }
-    (void)hipHostFree(tot);
     // the tree back to the host
     const int ni = n - 1;
     std::vector<int> hl(std::max(ni, 1)), hr(std::max(ni, 1)), hs(n);
@@ -1341,8 +1341,9 @@ size_t part_px(const Part& p) { return (size_t)p.frames * p.rows * p.W; }
 // "" when the parts' rows partition every frame of the batch (rows a rotated rank renders past the image are
 // skipped), else what is wrong
 std::string check_parts(const std::vector<Part>& ps) {
+    for (const Part& p : ps)
+        if (p.W <= 0 || p.H <= 0) return "a rank has not rendered";
     const Part& a = ps[0];
-    if (a.W <= 0 || a.H <= 0) return "a rank has not rendered";
     std::vector<char> cover((size_t)a.H);
     for (const Part& p : ps) {
         if (p.W != a.W || p.H != a.H) return "frame sizes differ";
@@ -1454,6 +1455,9 @@ extern "C" int rt_gather_to(rt_ctx* const* ctxs, int n, int root, void* d_dst) {
             void* d1 = ctx->d_stage + at;
             at += cpx * 4 * words;
             HIPC(hipSetDevice(c->device));
+            // the root's staging area may still be read by the previous gather's un-interleaving (root stream):
+            // the source's copy into it waits for that gather's completion (write after read)
+            if (ctx->gather_ev) HIPC(hipStreamWaitEvent(c->stream, ctx->gather_ev, 0));
             int can = 0;
             (void)hipDeviceCanAccessPeer(&can, c->device, ctx->device);
             if (can) {  // direct xGMI copies (else the runtime stages through the host)
@@ -1489,6 +1493,12 @@ struct rt_comm {
     int nranks = 0, rank0 = 0;
     Part* d_desc = nullptr;  // multi-process: every rank's descriptor (ncclAllGather), on ctxs[0]'s device
     Part* h_desc = nullptr;  // pinned
+    // multi-process: the descriptor exchange runs on its own stream, so the host waits for the exchange only,
+    // not for the render in flight on the context's stream; it starts after the previous gather's send/recv
+    // group (`done`) so that the communicator's operations run in one order on every rank
+    hipStream_t side = nullptr;
+    hipEvent_t done = nullptr;
+    bool issued = false;
     std::string err;
 };
 
@@ -1621,6 +1631,8 @@ extern "C" int rt_comm_init_rank(rt_ctx* ctx, int nranks, int rank, const unsign
     }
     hipError_t e = hipMalloc((void**)&cm->d_desc, sizeof(Part) * (nranks + 1));
     if (e == hipSuccess) e = hipHostMalloc((void**)&cm->h_desc, sizeof(Part) * (nranks + 1));
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&cm->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&cm->done, hipEventDisableTiming);
     if (e != hipSuccess) {
         fail(ctx, e, "rt_comm_init_rank: descriptor buffers");
         rt_comm_destroy(cm);
@@ -1633,20 +1645,23 @@ extern "C" int rt_comm_init_rank(rt_ctx* ctx, int nranks, int rank, const unsign
 extern "C" int rt_comm_gather(rt_comm* cm, int root, void* d_dst) {
     if (!cm || root < 0 || root >= cm->nranks) return RT_E_ARG;
     const int nl = (int)cm->ctxs.size();
-    for (rt_ctx* c : cm->ctxs)
-        if (!c->rendered) return comm_arg(cm, "rt_comm_gather: a context has not rendered");
-    // every rank's descriptor: at hand in one process, exchanged over RCCL (8 B x 16 per rank) otherwise
+    // every rank's descriptor: at hand in one process, exchanged over RCCL (4 B x 16 per rank) otherwise. A rank
+    // whose context has not rendered still joins the exchange (with W = 0), so that every rank fails together
+    // in check_parts instead of the others waiting in the collective for it
     std::vector<Part> ps(cm->nranks);
     if (nl == cm->nranks) {
+        for (rt_ctx* c : cm->ctxs)
+            if (!c->rendered) return comm_arg(cm, "rt_comm_gather: a context has not rendered");
         for (int i = 0; i < nl; i++) ps[i] = part_of(cm->ctxs[i]);
     } else {
         rt_ctx* ctx = cm->ctxs[0];
         HIPC(hipSetDevice(ctx->device));
-        cm->h_desc[cm->nranks] = part_of(ctx);
-        HIPC(hipMemcpyAsync(cm->d_desc + cm->nranks, cm->h_desc + cm->nranks, sizeof(Part), hipMemcpyHostToDevice, ctx->stream));
-        NCCLC(rccl().AllGather(cm->d_desc + cm->nranks, cm->d_desc, sizeof(Part) / 4, ncclInt32, cm->comms[0], ctx->stream));
-        HIPC(hipMemcpyAsync(cm->h_desc, cm->d_desc, sizeof(Part) * cm->nranks, hipMemcpyDeviceToHost, ctx->stream));
-        HIPC(hipStreamSynchronize(ctx->stream));
+        cm->h_desc[cm->nranks] = ctx->rendered ? part_of(ctx) : Part{};
+        if (cm->issued) HIPC(hipStreamWaitEvent(cm->side, cm->done, 0));
+        HIPC(hipMemcpyAsync(cm->d_desc + cm->nranks, cm->h_desc + cm->nranks, sizeof(Part), hipMemcpyHostToDevice, cm->side));
+        NCCLC(rccl().AllGather(cm->d_desc + cm->nranks, cm->d_desc, sizeof(Part) / 4, ncclInt32, cm->comms[0], cm->side));
+        HIPC(hipMemcpyAsync(cm->h_desc, cm->d_desc, sizeof(Part) * cm->nranks, hipMemcpyDeviceToHost, cm->side));
+        HIPC(hipStreamSynchronize(cm->side));
         for (int i = 0; i < cm->nranks; i++) ps[i] = cm->h_desc[i];
     }
     const std::string why = check_parts(ps);
@@ -1686,6 +1701,11 @@ extern "C" int rt_comm_gather(rt_comm* cm, int root, void* d_dst) {
         }
     }
     NCCLC(rccl().GroupEnd());
+    if (nl < cm->nranks) {  // the next descriptor exchange starts after this group (one order on every rank)
+        const hipError_t e = hipEventRecord(cm->done, cm->ctxs[0]->stream);
+        if (e != hipSuccess) return fail(cm->ctxs[0], e, "rt_comm_gather: hipEventRecord");
+        cm->issued = true;
+    }
     if (!rctx) return RT_OK;
     rt_ctx* ctx = rctx;
     HIPC(hipSetDevice(ctx->device));
@@ -1708,8 +1728,11 @@ extern "C" void rt_comm_destroy(rt_comm* cm) {
         }
         if (cm->comms[l]) (void)rccl().CommDestroy(cm->comms[l]);
     }
+    if (cm->side) (void)hipStreamSynchronize(cm->side);
     if (cm->d_desc) (void)hipFree(cm->d_desc);
     if (cm->h_desc) (void)hipHostFree(cm->h_desc);
+    if (cm->side) (void)hipStreamDestroy(cm->side);
+    if (cm->done) (void)hipEventDestroy(cm->done);
     delete cm;
 }
 

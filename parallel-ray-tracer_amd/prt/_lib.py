@@ -92,6 +92,13 @@ def _load(name):
     return ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
 
 
+def lib_md5(name="librt_hip.so"):
+    """md5 of the library build in use (profiles/pmc_traffic.json records the build its counters were measured on)"""
+    import hashlib
+    with open(os.path.join(LIB_DIR, name), "rb") as f:
+        return hashlib.md5(f.read()).hexdigest()
+
+
 def host():
     global _host
     if _host is None:

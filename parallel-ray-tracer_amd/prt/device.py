@@ -39,6 +39,11 @@ _L.rt_gather.argtypes = [P(ctypes.c_void_p), ctypes.c_int, ctypes.c_int]
 _L.rt_download_bmp.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
 
 
+def lib_md5():
+    """md5 of the librt_hip.so this process loaded"""
+    return _lib.lib_md5("librt_hip.so")
+
+
 def device_count():
     return _L.rt_device_count()
 
@@ -60,15 +65,17 @@ def gather(renderers, root=0, out=None):
 
 
 def _gather_out(r, out):
-    """device pointer of a gather's full-frame output tensor: contiguous, f32 (rgb) or int32 (BGRA8), on the
-    root's device, and at least one full frame of that format (rt_gather_to / rt_comm_gather write the
-    root's last render's frame count; a short tensor is refused here rather than overrun on the device)"""
+    """device pointer of a gather's full-frame output tensor: contiguous, on the root's device, of the root's
+    last render's pixel format (float32 for rgb, int32 for BGRA8: rt_gather_to / rt_comm_gather move the bgra
+    pixels when the render wrote them) and holding every frame of that render (frames x H x W x words); a
+    short or mistyped tensor is refused here rather than overrun on the device"""
     import torch
+    if not hasattr(r, "_size"):
+        raise RtError("gather out: the root renderer has not rendered")
     W, H = r._size
-    per = {torch.float32: 3, torch.int32: 1}.get(getattr(out, "dtype", None))
-    if per is None:
-        raise RtError("gather out: expected a float32 (rgb) or int32 (bgra8) torch tensor")
-    return _ptr(out, "gather out", W * H * per, (out.dtype,), r.device)
+    words = r._words
+    want = torch.int32 if words == 1 else torch.float32
+    return _ptr(out, "gather out", r._frames * W * H * words, (want,), r.device)
 
 
 COMM_ID_BYTES = 128  # RT_COMM_ID_BYTES
@@ -226,6 +233,7 @@ class Renderer:
         self._last = (width, nr)
         self._size = (width, height)
         self._frames = 1
+        self._words = 1 if bgra is not None else 3  # the payload a gather moves (rt_hip.hip payload_of)
 
     def render_frames(self, cams, width, height, rows=None, bounces=4, spp=1, kernel="auto", rgb=None, hit=None,
                       t=None, bounce_hit=None, bgra=None, variant=None, tune=False, waves_cap=0, dealing="default",
@@ -240,6 +248,7 @@ class Renderer:
         self._last = (width, nr)
         self._size = (width, height)
         self._frames = len(cams)
+        self._words = 1 if bgra is not None else 3
 
     def sync(self):
         ms = ctypes.c_float()
@@ -272,8 +281,8 @@ class Renderer:
         return buf.tobytes()
 
     def scene_info(self):
-        """rt_get_scene_info: what the last upload built (accel_built: "auto" = host binned SAH, "gpu" = PLOC on
-        the device), the wide BVH's size and depth, build times"""
+        """rt_get_scene_info: what the last upload built (accel_built: "host" = host binned SAH, "gpu" = PLOC on
+        the device, "reference" = the handed-over BVH), the wide BVH's size and depth, build times"""
         i = _lib.SceneInfo()
         self._chk(_L.rt_get_scene_info(self._ctx, ctypes.byref(i)), "rt_get_scene_info")
         d = {f: getattr(i, f) for f, _ in _lib.SceneInfo._fields_}

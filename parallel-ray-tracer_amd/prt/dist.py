@@ -188,3 +188,51 @@ class FrameGather:
             import torch
             torch.cuda.current_stream().wait_event(self._copied[i])
         return out
+
+
+class NativeGather:
+    """The N > 1 frame gather through the boundary's own RCCL code (include/rt_hip.h rt_comm_init_rank /
+    rt_comm_gather, replacing gpu/src/gpu.cu:203-228's load_from_gpu): one communicator per context (bench.py
+    alternates contexts on their own streams), torch.distributed only hands the RCCL ids out. Each context
+    renders its rows of a frame batch into target(c) (compact rows, as rt_render_frames writes them); gather(c),
+    called on every rank right after that render, enqueues the send (or, on rank 0, the receives and the
+    un-interleaving into frames(c)) on the context's stream, so the gather of one context's batch overlaps the
+    next render of the other. Same row layout as FrameGather (8-row blocks, residues rotated per frame)."""
+
+    def __init__(self, renderers, H, W, C, rank, world, dist, like, frames=1, block=1, rotate=False):
+        import torch
+        from . import device
+        self.H, self.W, self.C, self.rank, self.world = H, W, C, rank, world
+        self.frames, self.bk = frames, max(1, block)
+        self.rotate = bool(rotate) and frames > 1 and self.bk > 1 and world > 1
+        self.n_max = padded_rows(H, world, self.bk)
+        n = self.n_max if self.rotate else rank_rows(H, rank, world, self.bk)[2]
+        self.blocks = [torch.zeros((frames, n, W, C), dtype=like.dtype, device=like.device) for _ in renderers]
+        self.full = [torch.zeros((frames, H, W, C), dtype=like.dtype, device=like.device) for _ in renderers] \
+            if rank == 0 else None
+        ids = [device.comm_id() for _ in renderers] if rank == 0 else [None] * len(renderers)
+        if dist is not None:
+            dist.broadcast_object_list(ids, src=0)
+        self.comms = [device.Comm([r], world, rank, uid) for r, uid in zip(renderers, ids)]
+
+    def rows(self):
+        r = rank_rows(self.H, self.rank, self.world, self.bk)
+        if self.rotate:
+            return r[0], r[1], self.n_max, self.bk, self.bk
+        return r if self.bk > 1 else r[:3]
+
+    def target(self, c):
+        """context c's render output: [frames, n_rows, W, C] compact rows (render nf <= frames into [:nf])"""
+        return self.blocks[c]
+
+    def gather(self, c, nf=None):
+        """collective (every rank, after context c's render of nf frames): its frames -> rank 0's frames_of(c)"""
+        out = self.full[c][:nf or self.frames] if self.rank == 0 else None
+        self.comms[c].gather(root=0, out=out)
+
+    def frames_of(self, c):
+        return self.full[c] if self.rank == 0 else None
+
+    def close(self):
+        for cm in self.comms:
+            cm.close()

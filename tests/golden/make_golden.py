@@ -17,7 +17,9 @@ scenes in assets/*.tar.gz and stores:
 
 Frame binary layout (ref_harness.c): int32 hit[N] | f32 t[N] | f32 rgb[3N], row-major idx = y*W + x.
 Only needed in the build container (where /root/reference exists); the fixtures are committed.
-usage: make_golden.py [all | cars | standin | stress ...]  (sections update golden.json in place)
+  configs (round 3): two_cars at 3840x2160 and dragon at 640x360 (BASELINE configs 4 and 1).
+
+usage: make_golden.py [all | cars | standin | stress | configs ...]  (sections update golden.json in place)
 """
 import hashlib
 import json
@@ -108,6 +110,23 @@ def stress(out, tmp):
     out["bvh"]["random1m_h3"] = {"md5": hashlib.md5(raw).hexdigest(), "nodes": int(np.frombuffer(raw[:4], np.int32)[0])}
 
 
+def configs(out, tmp):
+    """round 3: the two BASELINE configurations no fixture covered yet, at the sizes BASELINE.json names --
+    two_cars at 3840x2160 (every 97th pixel, the frame's md5, rt_ref_count's rays) and dragon at 640x360
+    (cpu/src/main.c's own WIDTH x HEIGHT: every 7th pixel, the frame's md5, rays)"""
+    out.setdefault("rays", {})
+    for scene, W, H, step, tag in (("two_cars", 3840, 2160, 97, "2160p"), ("dragon", 640, 360, 7, "360p")):
+        p = os.path.join(tmp, f"{scene}_{tag}.bin")
+        run("rt_ref_strict", "render", *scene_paths(scene), W, H, os.cpu_count() or 8, p)
+        raw, hit, t, rgb = frame(p, W, H)
+        out["standin"][scene][f"{W}x{H}_md5"] = hashlib.md5(raw).hexdigest()
+        idx = np.arange(0, W * H, step)
+        np.savez_compressed(os.path.join(HERE, f"{scene}_{tag}_strict_sample.npz"), idx=idx,
+                            hit=hit.reshape(-1)[idx], t=t.reshape(-1)[idx], rgb=rgb.reshape(-1, 3)[idx])
+        os.remove(p)
+        out["rays"][f"{scene}_{W}x{H}"] = counts(scene_paths(scene), W, H, tmp)
+
+
 def main(sections):
     gpath = os.path.join(HERE, "golden.json")
     out = json.load(open(gpath)) if os.path.exists(gpath) and "all" not in sections else {}
@@ -117,6 +136,8 @@ def main(sections):
     tmp = tempfile.mkdtemp()
     if "stress" in sections:
         stress(out, tmp)
+    if "configs" in sections:
+        configs(out, tmp)
     if "standin" in sections or "all" in sections:
         standin(out, tmp, ("dragon", "sportscar", "two_cars"))
     if "cars" not in sections and "all" not in sections:

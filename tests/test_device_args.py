@@ -26,16 +26,35 @@ def test_output_tensors_are_checked_before_any_launch():
 
 
 def test_gather_output_tensor_is_checked():
-    """rt_gather_to / rt_comm_gather's full-frame output: one W*H frame of rgb f32 or BGRA8 int32 at least"""
-    class Root:  # the root Renderer's size and device, as prt.device.Renderer keeps them
-        _size, device = (4, 2), 0
+    """rt_gather_to / rt_comm_gather's full-frame output: EVERY frame of the root's last render (frames x W x H),
+    in that render's pixel format (rgb f32 x 3 or BGRA8 int32)"""
+    class Root:  # the root Renderer's last render, as prt.device.Renderer keeps it
+        _size, device, _frames, _words = (4, 2), 0, 1, 3
 
     with pytest.raises(device.RtError, match="elements"):
         device._gather_out(Root(), torch.zeros(4 * 2 * 3 - 1, dtype=torch.float32))
-    with pytest.raises(device.RtError, match="float32 .rgb. or int32"):
-        device._gather_out(Root(), torch.zeros(4 * 2, dtype=torch.int64))
+    with pytest.raises(device.RtError, match="dtype"):
+        device._gather_out(Root(), torch.zeros(4 * 2 * 3, dtype=torch.int64))
+    with pytest.raises(device.RtError, match="dtype"):  # an rgb render gathered into a BGRA8 tensor
+        device._gather_out(Root(), torch.zeros(4 * 2 * 3, dtype=torch.int32))
     with pytest.raises(device.RtError, match="expected cuda:0"):
-        device._gather_out(Root(), torch.zeros(4 * 2, dtype=torch.int32))
+        device._gather_out(Root(), torch.zeros(4 * 2 * 3, dtype=torch.float32))
+
+    class Batch(Root):  # a 16-frame BGRA8 batch: a one-frame tensor is refused
+        _frames, _words = 16, 1
+
+    with pytest.raises(device.RtError, match="elements"):
+        device._gather_out(Batch(), torch.zeros(4 * 2, dtype=torch.int32))
+    with pytest.raises(device.RtError, match="dtype"):
+        device._gather_out(Batch(), torch.zeros(16 * 4 * 2, dtype=torch.float32))
+    with pytest.raises(device.RtError, match="expected cuda:0"):
+        device._gather_out(Batch(), torch.zeros(16 * 4 * 2, dtype=torch.int32))
+
+    class Fresh:  # nothing rendered yet
+        device = 0
+
+    with pytest.raises(device.RtError, match="not rendered"):
+        device._gather_out(Fresh(), torch.zeros(8, dtype=torch.int32))
 
 
 def test_variant_and_dealing_names_match_the_header():

@@ -19,9 +19,9 @@ RGB_TOL = 1e-5
 # every kernel and launch configuration the C-ABI exposes (rt_frame.kernel / rt_frame.variant): STRICT, FAST
 # with its default rule ("fast"), and each variant forced: k_persist at 4 waves/SIMD ("persist4"), k_coop
 # ("coopG": G lanes per ray), k_fan ("fan":
-# 1 + lights lanes per pixel), k_pool ("pool": tile-local ray queues with dynamic fetch). The split
-# pipeline has its own tests.
-KERNELS = ["strict", "fast", "persist4", "coop2", "coop4", "coop8", "fan", "pool"]
+# 1 + lights lanes per pixel). k_pool ("pool": tile-local ray queues with dynamic fetch; measured slower, never
+# a default) and the split pipeline have their own tests.
+KERNELS = ["strict", "fast", "persist4", "coop2", "coop4", "coop8", "fan"]
 
 
 def select(kernel):
@@ -79,6 +79,21 @@ def test_small_frames_vs_reference_fixture(dev, scenes, kernel, scene, W, H):
     np.testing.assert_array_equal(out["hit"], ref["hit"])
     assert same_bits(out["t"], ref["t"])
     assert same_bits(out["rgb"], ref["rgb"]), np.abs(out["rgb"] - ref["rgb"]).max()
+
+
+def test_pool_variant_vs_reference(dev, scenes):
+    """k_pool (RT_VARIANT_POOL: measured slower, never a default, so not in the KERNELS loops): the car scenes'
+    fixtures, the full 1080p car_boxed frame's md5 and its ray counts"""
+    for scene in ("car_boxed", "car_only"):
+        out = render(dev, scenes[scene], 160, 90, "pool")
+        ref = np.load(os.path.join(GOLD, f"{scene}_160x90_strict.npz"))
+        np.testing.assert_array_equal(out["hit"], ref["hit"])
+        assert same_bits(out["t"], ref["t"]) and same_bits(out["rgb"], ref["rgb"])
+    import hashlib
+    out = render(dev, scenes["car_boxed"], 1920, 1080, "pool", counters=True)
+    md5 = hashlib.md5(out["hit"].astype(np.int32).tobytes() + out["t"].tobytes() + out["rgb"].tobytes()).hexdigest()
+    assert md5 == G["frames"]["car_boxed_1920x1080_strict"]["md5"]
+    assert out["stats"]["rays"] == G["rays"]["car_boxed_1920x1080"]["total"]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -177,7 +192,7 @@ def test_strict_traversal_counters_match_reference_order(dev, scenes):
         assert st[k] == c[k], k
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "pool"])
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan"])
 @pytest.mark.parametrize("spp", [4, 16])
 def test_spp_matches_oracle(dev, scenes, spp, kernel):
     from tests.oracle_bind import OracleScene
@@ -193,7 +208,7 @@ def test_spp_matches_oracle(dev, scenes, spp, kernel):
 _SPP64 = {}
 
 
-@pytest.mark.parametrize("kernel", ["fast", "persist4", "coop4", "fan", "pool"])
+@pytest.mark.parametrize("kernel", ["fast", "persist4", "coop4", "fan"])
 def test_car_boxed_64spp_matches_oracle(dev, scenes, kernel):
     """BASELINE config 5 (car_boxed 3840x2160, 64 spp, multi-bounce): the reference has one corner ray per
     pixel (cpu/src/main.c:228-239); SURVEY §8d defines spp = s x s stratified sub-pixel samples, mean of the
@@ -434,7 +449,7 @@ def moved_camera(W, H, dx, dz):
     return c
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "strict", "pool"])
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "strict"])
 @pytest.mark.parametrize("name", ["car_boxed", "dragon"])
 def test_frame_batch_equals_single_frames(dev, name, kernel):
     """rt_render_frames: a batch of frames (different cameras, one persistent launch on the fast paths)
@@ -475,7 +490,7 @@ def test_frame_batch_equals_single_frames(dev, name, kernel):
             assert same_bits(rgb[0].cpu().numpy(), ref["rgb"])
 
 
-@pytest.mark.parametrize("kernel", ["fast", "pool"])
+@pytest.mark.parametrize("kernel", ["fast"])
 @pytest.mark.parametrize("dealing", ["global", "rows", "columns", "row_major"])
 def test_xcd_aware_dealing_renders_the_same_frames(dev, dealing, kernel):
     """the persistent kernels' tile dealing (rt_frame.dealing, rtd::next_item): one global counter, 8 row
@@ -587,7 +602,7 @@ def test_path_level_placements_render_the_same_frames(dev, name):
         assert a0["stats"]["rays"] == a1["stats"]["rays"], v
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "pool"])
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan"])
 def test_rotated_row_blocks_cover_every_frame(dev, kernel):
     """rt_frame.frame_shift: frame f of rank q renders block residue (q + f) % N (prt.dist rotate), rows
     past the image skipped — over the N ranks every frame of the batch is rendered exactly once, bit for

@@ -21,7 +21,7 @@ for s in "${@:-smoke pytest bench}"; do
   for step in $s; do
     case $step in
       smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-      pytest) run pytest_gpu 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+      pytest) run pytest_gpu 1200 python -u -m pytest tests -m gpu -x -v --durations=15 --timeout 300 --timeout-method thread ;;
       pytestall) run pytest_gpu 1200 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ;;
       bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
       benchq) run bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;

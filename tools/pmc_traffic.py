@@ -1,11 +1,16 @@
 #!/usr/bin/env python3
-"""Summarise a tools/profile.sh run into profiles/: kernel-trace stats (markdown) and the PMC HBM traffic
-of the bench's production kernel (profiles/pmc_traffic.json, read by bench.py for roofline.traffic).
+"""Summarise a tools/profile.sh run into profiles/: kernel-trace stats (markdown) and the PMC counters of the
+bench's production kernel (profiles/pmc_traffic.json, read by bench.py for its roofline fields).
+
+The production kernel is the one with the largest total time in the trace. The entry is keyed by the bench
+line's own pmc_key (scene, size, spp, output, frames per launch, ranks: read from the trace pass's JSON line,
+so nothing is rescaled to another launch size) and records the md5 of the librt_hip.so the box ran
+(profile.sh writes lib_md5.txt): bench.py reports the counters as measured only for that build.
 
 traffic per launch = 2 x FETCH_SIZE + WRITE_SIZE (kB -> bytes): MI355X_MICROARCH.md §HBM — on gfx950
 FETCH_SIZE reports half the bytes of 16-B-per-lane reads (the kernel's node/triangle loads are float4
 per lane); WRITE_SIZE reads exactly for 16-B stores. Counters come from separate --pmc passes.
-usage: tools/pmc_traffic.py gpurun_out/prof_<tag> <round-tag> [bench key]
+usage: tools/pmc_traffic.py gpurun_out/prof_<tag> <round-tag>
 """
 import csv
 import json
@@ -15,11 +20,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# production instantiation of the bench: k_persist, no counters, 4 waves/SIMD, no trace, frame batch,
-# path buffer in LDS (PB = 2) after the DYN wide stack, the spp = 1 build (round 2)
-PROD = "k_persist<4, false, false, true, 4, false, true, 2, true, true>"
-N_SIMD, N_XCD = 1024, 8
-FRAMES = 16  # tools/profile.sh: bench.py --steps 64 = 4 launches of 16 frames  # MI355X: 256 CUs x 4 SIMDs, 8 XCDs (GRBM_GUI_ACTIVE counts every XCD)
+N_SIMD, N_XCD = 1024, 8  # MI355X: 256 CUs x 4 SIMDs, 8 XCDs (GRBM_GUI_ACTIVE counts every XCD)
 
 
 def rows(path):
@@ -42,16 +43,29 @@ def find(d, sub):
     return None, None
 
 
+def bench_line(prof):
+    """the bench's JSON line of the trace pass (profile.sh keeps its stdout in trace.log)"""
+    for l in open(os.path.join(prof, "trace.log")):
+        if l.startswith("{"):
+            return json.loads(l)
+    raise SystemExit(f"{prof}/trace.log has no bench line")
+
+
 def main():
     prof, tag = sys.argv[1], sys.argv[2]
-    key = sys.argv[3] if len(sys.argv) > 3 else "dragon_1920x1080_fast_random_bgra8"
+    line = bench_line(prof)
+    rf = line["roofline"]
+    key, frames = rf["pmc_key"], rf["frames_per_launch"]
+    cmd = open(os.path.join(prof, "cmd.txt")).read().strip() if os.path.exists(os.path.join(prof, "cmd.txt")) else "bench.py"
+    lib_md5 = open(os.path.join(prof, "lib_md5.txt")).read().split()[0]
     pdir = os.path.join(ROOT, "profiles")
     os.makedirs(pdir, exist_ok=True)
     # kernel trace stats
     stats = rows(os.path.join(prof, "trace", "run_kernel_stats.csv"))
-    lines = [f"# rocprofv3 --kernel-trace --stats ({tag})", "",
-             f"command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 64 --warmup 16 --no-cpu-baseline`"
-             f" (16 frames per launch: one launch = 16 frames)",
+    PROD = max(stats, key=lambda r: float(r["TotalDurationNs"]))["Name"]
+    lines = [f"# rocprofv3 --kernel-trace --stats ({tag}, {key})", "",
+             f"command: `rocprofv3 --kernel-trace --stats -- {cmd}` ({frames} frames per launch; librt_hip.so md5 "
+             f"{lib_md5}); bench line: {line['value']:.0f} Mrays/s, HIP-event kernel {rf['kernel_ms']:.3f} ms per launch",
              "", "| kernel | calls | total ms | avg ms | min ms | max ms | % |", "|---|---|---|---|---|---|---|"]
     for r in stats:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
@@ -84,12 +98,14 @@ def main():
         hbm = 2 * f_kb * 1024 + w_kb * 1024
         _, avg = find({r["Name"]: float(r["AverageNs"]) for r in stats}, PROD)
         res = {"kernel": kf, "launches": len(vf), "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
-               "hbm_bytes_per_launch": hbm, "frames_per_launch": FRAMES, "hbm_bytes_per_frame": hbm / FRAMES, "trace_avg_ms": avg / 1e6 if avg else None,
+               "fetch_bytes_per_launch": 2 * f_kb * 1024, "write_bytes_per_launch": w_kb * 1024,
+               "hbm_bytes_per_launch": hbm, "frames_per_launch": frames, "lib_md5": lib_md5, "command": cmd,
+               "bench_kernel_ms": rf["kernel_ms"], "trace_avg_ms": avg / 1e6 if avg else None,
                "trace_median_ms_production_grid": statistics.median(groups[prod_grid]) if groups else None,
                "production_grid_workgroups": prod_grid,
                "hbm_gbs_at_trace_avg": hbm / (avg / 1e9) / 1e9 if avg else None,
                "rule": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md §HBM, gfx950 FETCH_SIZE halving)",
-               "source": f"profiles/{tag}_kernel_stats.md, gpurun_out/{os.path.basename(prof)}", "round": tag}
+               "source": f"profiles/{tag}_kernel_stats.md, profiles/{tag}/*_summary.csv", "round": tag}
         lines += ["", f"## HBM traffic of `{PROD}` (PMC, separate passes)", "",
                   f"- FETCH_SIZE median {f_kb:.0f} kB/launch, WRITE_SIZE median {w_kb:.0f} kB/launch",
                   f"- traffic = 2 x FETCH + WRITE = {hbm / 1e6:.1f} MB/launch"
@@ -126,6 +142,9 @@ def main():
     # CSV copies under profiles/<tag>/: the trace stats as rocprofv3 wrote them, the PMC passes as
     # per-kernel medians (kernel, counter, launches, median, min, max)
     cdir = os.path.join(pdir, tag)
+    os.makedirs(cdir, exist_ok=True)
+    with open(os.path.join(cdir, "bench_line.json"), "w") as f:  # the trace pass's own bench line
+        f.write(json.dumps(line) + "\n")
     os.makedirs(cdir, exist_ok=True)
     shutil.copyfile(os.path.join(prof, "trace", "run_kernel_stats.csv"), os.path.join(cdir, "kernel_stats.csv"))
     for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_l2", "pmc_valu"):

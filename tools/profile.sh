@@ -1,8 +1,9 @@
 #!/bin/bash
-# rocprofv3 passes for the bench workload (run on the GPU box): kernel trace + stats, then PMC counters
+# rocprofv3 passes for one bench configuration (run on the GPU box): kernel trace + stats, then PMC counters
 # in separate passes (FETCH_SIZE and WRITE_SIZE cannot share one pass on gfx950; no trace domains
-# are combined with --pmc). Output under gpurun_out/prof_<tag>/.
-# usage: tools/profile.sh <tag> [bench args...]
+# are combined with --pmc). Output under gpurun_out/prof_<tag>/ (+ the command and the library's md5, which
+# tools/pmc_traffic.py stamps into profiles/pmc_traffic.json).
+# usage: tools/profile.sh <tag> [bench args...]   (default: the driver's command, --steps 20 --warmup 5)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 tag=$1; shift
@@ -17,7 +18,9 @@ step() {  # name timeout cmd...
     echo "=== $name rc=$rc" | tee -a $out/session.log
     if [ $rc -ne 0 ]; then tail -20 $out/$name.log; exit $rc; fi
 }
-B="python3 bench.py --steps 64 --warmup 16 --no-cpu-baseline $args"
+B="python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline $args"
+echo "$B" > $out/cmd.txt
+md5sum parallel-ray-tracer_amd/lib/librt_hip.so > $out/lib_md5.txt
 step trace 600 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- $B
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d $out/pmc_fetch -o run --output-format csv -- $B
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d $out/pmc_write -o run --output-format csv -- $B
