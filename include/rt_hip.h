@@ -88,17 +88,22 @@ enum {
 
 /* rt_frame.variant: launch configuration of RT_KERNEL_FAST */
 enum {
-    RT_VARIANT_DEFAULT = 0,  /* the library's rule: RT_VARIANT_PERSIST4 for frame batches and spp > 1, RT_VARIANT_PERSIST
-                                for single 1-spp frames, RT_VARIANT_SPLIT for single 1-spp frames of scenes with >= 3 lights; with
-                                rt_frame.tune = 1 the measured fastest candidate instead */
+    RT_VARIANT_DEFAULT = 0,  /* the library's rule: RT_VARIANT_PERSIST4 for frame batches and spp > 1, RT_VARIANT_HYBRID
+                                for single 1-spp frames (RT_VARIANT_PERSIST where it cannot run); with rt_frame.tune = 1
+                                the measured fastest candidate instead */
     RT_VARIANT_PERSIST = 1,  /* k_persist: one lane per pixel path, walks in lockstep, 3 waves per SIMD */
     RT_VARIANT_PERSIST4 = 2, /* k_persist at 4 waves per SIMD (path levels in LDS) */
-    RT_VARIANT_SPLIT = 3,    /* closest chains / shadow batches / resolve: three launches (1 spp; one frame per launch) */
+    RT_VARIANT_SPLIT = 3,    /* closest chains / shadow batches / resolve: three launches (1 spp; a frame batch in the same three) */
     RT_VARIANT_COOP2 = 4,    /* k_coop: 2 lanes per ray (shorter chains for small row sets) */
     RT_VARIANT_COOP4 = 5,    /* k_coop: 4 lanes per ray */
     RT_VARIANT_COOP8 = 6,    /* k_coop: 8 lanes per ray */
     RT_VARIANT_FAN = 7,      /* k_fan: 1 + lights lanes per pixel (shadow fan-out; 1..7 lights) */
     /* 8, 9: k_chain (each lane's walks back to back), measured slower and removed in round 2: refused */
+    RT_VARIANT_HYBRID = 11,  /* single frames: the tiles an earlier frame of the same shape and camera measured costliest
+                                through k_coop (2 or 4 lanes per ray) on a second stream while k_persist renders the rest.
+                                The first frame of a shape / camera measures (k_persist with per-tile times), the next
+                                ones try hot thresholds and k_persist itself, and the fastest renders from then on
+                                (rt_frame.hot_pct > 0: that threshold, 4 lanes per ray, no trials) */
     RT_VARIANT_POOL = 10     /* k_pool: 16x16-pixel tile per workgroup, each bounce level's closest-hit and shadow rays
                                 compacted into tile-local LDS queues and traced with dynamic fetch (rt_frame.regroup =
                                 idle lanes per refill), 4 waves per SIMD */
@@ -138,6 +143,8 @@ typedef struct rt_frame {
     int waves_cap; /* persistent grids: at most this many workgroups (4 waves each) per CU; 0 = occupancy limit */
     int dealing;   /* RT_DEAL_* */
     int regroup;   /* k_pool: idle lanes of a wave that trigger a refill from the tile's queue; 0 = 16 */
+    int hot_pct;   /* RT_VARIANT_HYBRID: tiles whose measured time exceeds hot_pct % of the costliest tile's go to the
+                      cooperative kernel; 0 = try several thresholds and keep the fastest */
 } rt_frame;
 
 /* Device output pointers (all nullable). rgb: [n_rows][width][3] f32 in [0,1] = vec_t pixels
@@ -172,6 +179,9 @@ typedef struct rt_stats {
     unsigned long long node_bytes;     /* BVH node / leaf record bytes read (RT_FLAG_COUNTERS; fused kernels) */
     unsigned long long wave_steps;     /* wave-level wide-node steps (RT_FLAG_COUNTERS): SIMD efficiency =
                                           (ch_inner + sh_inner of the wide walk) / (64 * wave_steps) */
+    unsigned long long shadow_wave_steps; /* of which shadow walks' (k_persist's walks; RT_FLAG_COUNTERS)     */
+    unsigned long long steps_lanes_16, steps_lanes_32, steps_lanes_48, steps_lanes_64; /* k_persist's wave steps
+                                          with 1-16 / 17-32 / 33-48 / 49-64 active lanes (RT_FLAG_COUNTERS)  */
 } rt_stats;
 
 int rt_device_count(void);

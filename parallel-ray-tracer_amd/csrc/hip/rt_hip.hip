@@ -133,9 +133,46 @@ struct rt_ctx {
     // bounces, spp, frames, dealing, waves cap): a context that alternates frame shapes keeps every decision
     std::vector<Tune> tunes;
     long long scene_gen = 0;  // bumped by every upload
+    // RT_VARIANT_HYBRID (single frames): the per-tile times of a k_persist frame of the current shape and camera,
+    // and the tile lists they give (the coop tiles of the costliest 8x8 tiles; the rest for k_persist)
+    struct Hybrid {
+        long long scene = -1;
+        int W = 0, rows = 0, off = 0, stride = 0, block = 0, bounces = 0, spp = 0, dealing = 0, pct_req = 0;
+        float cam[12] = {};
+        int state = 0;  // 0: measure next; 1: a measuring frame's tile times are on their way to h_tr; 2: lists ready
+        // candidates: hot threshold (0 = k_persist), their lists at d_lists + at[c], trial launch, time, choice
+        static constexpr int NCAND = 8;
+        int nc = 0, choice = -1;
+        int pct[NCAND] = {}, lanes[NCAND] = {}, n_hot[NCAND] = {}, n_cold[NCAND] = {};
+        bool fan[NCAND] = {};  // the hot tiles through k_fan<lanes> instead of k_coop<lanes>
+        size_t at[NCAND] = {};
+        long long launch[NCAND] = {};
+        float ms[NCAND] = {};
+        unsigned long long* d_tr = nullptr;  // [tiles][4], rtd::k_persist's TRACE records
+        unsigned long long* h_tr = nullptr;  // pinned
+        size_t tr_cap = 0, n_tiles = 0;
+        int* d_lists = nullptr;  // per candidate: [hot coop tiles][cold 8x8 tiles: XCD region layout or order]
+        size_t lists_cap = 0;
+        bool cold_regions = false;
+        hipEvent_t ev = nullptr, fork = nullptr, join = nullptr;
+        hipStream_t s2 = nullptr;
+    } hy;
 };
 
 namespace {
+
+// RT_VARIANT_HYBRID candidates: tiles slower than pct % of the slowest tile of the measuring frame go to k_coop
+// with `lanes` lanes per ray (each candidate is tried once against k_persist; hybrid_pick)
+// (lanes: k_coop's lanes per ray; 0: k_fan, 1 + lights lanes per pixel)
+struct HotCand {
+    int pct, lanes;
+};
+constexpr HotCand HYBRID_CANDS[7] = {{45, 4}, {60, 4}, {75, 4}, {60, 2}, {75, 2}, {60, 0}, {75, 0}};
+// pixel tile of the hot kernel (rtd::GTile): k_coop<2> 8x4, k_coop<4> / k_fan<4> 4x4, k_fan<2> 8x4, k_fan<8> 4x2
+inline void hot_tile(int g, int& tw, int& th) {
+    tw = g == 2 ? 8 : 4;
+    th = g == 8 ? 2 : 4;
+}
 
 int fail(rt_ctx* c, hipError_t e, const char* what) {
     if (c) c->err = std::string(what) + ": " + hipGetErrorString(e);
@@ -752,6 +789,42 @@ int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count, int cap_a);  // below
 }  // namespace
 
 namespace {
+// Centre-out order of a tx x ty tile grid (the persistent kernels' default dealing order)
+std::vector<int> centre_out(int tx, int ty) {
+    const int n = tx * ty;
+    std::vector<int> ord(n);
+    for (int i = 0; i < n; i++) ord[i] = i;
+    const float cx = 0.5f * tx, cy = 0.5f * ty;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+        const float ax = a % tx + 0.5f - cx, ay = a / tx + 0.5f - cy;
+        const float bx = b % tx + 0.5f - cx, by = b / tx + 0.5f - cy;
+        return ax * ax + ay * ay < bx * bx + by * by;
+    });
+    return ord;
+}
+
+// XCD-aware layout of a dealing order (rtd::next_item): 9 region offsets into the tile part, then the tiles of
+// region 0..7, each region in the order's order. mode 1: 8 bands of tile rows, 2: 8 bands of tile columns,
+// 3: 4 x 2 blocks.
+std::vector<int> region_layout(const std::vector<int>& ord, int tx, int ty, int mode) {
+    std::vector<int> dev(9 + ord.size());
+    int at = 9;
+    for (int r = 0; r < 8; r++) {
+        dev[r] = at;
+        for (int t : ord) {
+            const int reg = mode == 1 ? (t / tx) * 8 / ty : mode == 2 ? (t % tx) * 8 / tx
+                                                                    : (t % tx) * 4 / tx + 4 * ((t / tx) * 2 / ty);
+            if (reg == r) dev[at++] = t;
+        }
+    }
+    dev[8] = at;
+    for (int r = 0; r <= 8; r++) dev[r] -= 9;  // offsets into the order part
+    return dev;
+}
+
+template <int MAXB>
+int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c);  // below
+
 // rt_render / rt_render_frames: n_frames frames of the same shape (cameras cams[0..n_frames-1]); outputs
 // [n_frames][n_rows][width]... Persistent fast configurations trace the whole batch in ONE launch (frames'
 // tiles interleaved in the dealing order); other kernels launch once per frame.
@@ -780,7 +853,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     while (g * g < f->spp) g++;
     if (f->spp < 1 || g * g != f->spp || g > 16) return arg_err(ctx, "rt_render: spp must be a square 1..256");
     if (f->kernel < RT_KERNEL_AUTO || f->kernel > RT_KERNEL_FAST) return arg_err(ctx, "rt_render: bad kernel");
-    if (f->variant < RT_VARIANT_DEFAULT || f->variant > RT_VARIANT_POOL || f->variant == 8 || f->variant == 9 ||
+    if (f->variant < RT_VARIANT_DEFAULT || f->variant > RT_VARIANT_HYBRID || f->variant == 8 || f->variant == 9 ||
+        f->hot_pct < 0 || f->hot_pct > 100 ||
         f->tune < 0 || f->tune > 1 ||
         f->waves_cap < 0 || f->waves_cap > 8 || f->dealing < RT_DEAL_DEFAULT || f->dealing > RT_DEAL_ROW_MAJOR ||
         f->regroup < 0 || f->regroup > 64)
@@ -915,25 +989,17 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     // tile does (PRT_TILE_TRACE: 8x8 tiles range from 2 us to ~1.9 ms; expensive ones are deep reflection
     // chains, usually on the object in view); dealing from the centre starts them first (bench frame
     // -7 %). RT_DEAL_ROW_MAJOR: row-major. One cached permutation per tile grid.
-    const bool centre_out = kernel == RT_KERNEL_FAST && f->dealing != RT_DEAL_ROW_MAJOR;
+    const bool dealt_centre_out = kernel == RT_KERNEL_FAST && f->dealing != RT_DEAL_ROW_MAJOR;
     auto order_for = [&](int tx, int ty, const int*& out_ord) -> int {
         out_ord = nullptr;
-        if (!centre_out) return RT_OK;
+        if (!dealt_centre_out) return RT_OK;
         const long long key = ((long long)tx << 32) | (unsigned)ty;
         auto it = ctx->orders.find(key);
         if (it != ctx->orders.end()) {
             out_ord = it->second;
             return RT_OK;
         }
-        const int n = tx * ty;
-        std::vector<int> ord(n);
-        for (int i = 0; i < n; i++) ord[i] = i;
-        const float cx = 0.5f * tx, cy = 0.5f * ty;
-        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
-            const float ax = a % tx + 0.5f - cx, ay = a / tx + 0.5f - cy;
-            const float bx = b % tx + 0.5f - cx, by = b / tx + 0.5f - cy;
-            return ax * ax + ay * ay < bx * bx + by * by;
-        });
+        const std::vector<int> ord = centre_out(tx, ty);
         int* d = nullptr;
         HIPC(hipMalloc((void**)&d, sizeof(int) * ord.size()));
         HIPC(hipMemcpy(d, ord.data(), sizeof(int) * ord.size(), hipMemcpyHostToDevice));
@@ -961,32 +1027,11 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                                                          : 0;
     auto regions_for = [&](int tx, int ty, const int*& roff, const int*& rord) -> int {
         roff = rord = nullptr;
-        if (!(centre_out && xcd_mode >= 1 && xcd_mode <= 3)) return RT_OK;
+        if (!(dealt_centre_out && xcd_mode >= 1 && xcd_mode <= 3)) return RT_OK;
         const long long key = ((long long)xcd_mode << 58) | ((long long)tx << 32) | (unsigned)ty;
         auto it = ctx->orders.find(key);
         if (it == ctx->orders.end()) {
-            const int n = tx * ty;
-            std::vector<int> ord(n);
-            for (int i = 0; i < n; i++) ord[i] = i;
-            const float cx = 0.5f * tx, cy = 0.5f * ty;
-            std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
-                const float ax = a % tx + 0.5f - cx, ay = a / tx + 0.5f - cy;
-                const float bx = b % tx + 0.5f - cx, by = b / tx + 0.5f - cy;
-                return ax * ax + ay * ay < bx * bx + by * by;
-            });
-            std::vector<int> dev(9 + n);
-            int at = 9;
-            for (int r = 0; r < 8; r++) {
-                dev[r] = at;
-                for (int t : ord) {
-                    const int reg = xcd_mode == 1 ? (t / tx) * 8 / ty
-                                    : xcd_mode == 2 ? (t % tx) * 8 / tx
-                                                    : (t % tx) * 4 / tx + 4 * ((t / tx) * 2 / ty);
-                    if (reg == r) dev[at++] = t;
-                }
-            }
-            dev[8] = at;
-            for (int r = 0; r <= 8; r++) dev[r] -= 9;  // offsets into the order part
+            const std::vector<int> dev = region_layout(centre_out(tx, ty), tx, ty, xcd_mode);
             int* d = nullptr;
             HIPC(hipMalloc((void**)&d, sizeof(int) * dev.size()));
             HIPC(hipMemcpy(d, dev.data(), sizeof(int) * dev.size(), hipMemcpyHostToDevice));
@@ -1003,12 +1048,13 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     //   COOP2/4/8           k_coop (rt_coop.hpp): G lanes per ray, 64/G-pixel tiles — shorter chains per tile,
     //                       which is what a frame split over many GPUs (few tiles per wave) is bound by;
     //   FAN                 k_fan (rt_fan.hpp): 1 + lights lanes per pixel.
-    // Default rule (measured): PERSIST4 for frame batches and spp > 1, PERSIST for single frames, SPLIT for
-    // single 1-spp frames of scenes with >= 3 lights. rt_frame.tune = 1 measures instead: the first frame of a (scene upload, frame shape) runs each
+    // Default rule (measured): PERSIST4 for frame batches and spp > 1, HYBRID for single 1-spp frames
+    // (k_persist where a frame has no costly tail, or with frame_shift / tile traces). rt_frame.tune = 1 measures instead: the first frame of a (scene upload, frame shape) runs each
     // candidate TUNE_REPS times (all into the same outputs), the next frame of that shape reads the timings
     // and keeps the fastest; PRT_TUNE_LOG=1 prints them.
-    const bool split_ok =
-        kernel == RT_KERNEL_FAST && f->spp == 1 && ctx->n_lights >= 1 && ctx->n_lights <= 32 && !A.tile_trace && n_frames == 1;
+    // (split: batch items (frame, tile) are packed into 24 bits of a shadow batch entry)
+    const bool split_ok = kernel == RT_KERNEL_FAST && f->spp == 1 && ctx->n_lights >= 1 && ctx->n_lights <= 32 &&
+                          !A.tile_trace && (long long)A.n_tiles * n_frames < (1ll << 24);
     const bool wide_ok = kernel == RT_KERNEL_FAST && ctx->wide_n > 0;
     const bool fan_ok = wide_ok && ctx->n_lights >= 1 && ctx->n_lights <= 7;
     const int fan_r = ctx->n_lights <= 1 ? 2 : ctx->n_lights <= 3 ? 4 : 8;  // lanes per pixel: 1 + lights
@@ -1018,14 +1064,15 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         if (v >= RT_VARIANT_COOP2 && v <= RT_VARIANT_COOP8) return wide_ok;
         if (v == 8 || v == 9) return false;  // (k_chain, removed in round 2)
         if (v == RT_VARIANT_POOL) return wide_ok && !A.tile_trace && A.wcap > 0;
+        if (v == RT_VARIANT_HYBRID) return wide_ok && !A.tile_trace && n_frames == 1 && fs == 0;
         return true;
     };
     int mode = f->variant;
     if (mode == RT_VARIANT_DEFAULT)
         // (a multi-sample frame fills the chip like a batch: car_boxed 4K 64 spp 195 ms at 4 waves vs 219 at 3)
-        mode = split_ok && ctx->n_lights >= 3 ? RT_VARIANT_SPLIT
-               : (n_frames > 1 || f->spp > 1) ? RT_VARIANT_PERSIST4
-                                               : RT_VARIANT_PERSIST;
+        // (single 1-spp frames: the hybrid launch, which measures and keeps k_persist where that is faster; the split
+        // pipeline lost to it on every BASELINE scene in round 3, sportscar 3.76 vs 3.04 ms)
+        mode = (n_frames > 1 || f->spp > 1) ? RT_VARIANT_PERSIST4 : RT_VARIANT_HYBRID;
     if (!usable(mode)) mode = RT_VARIANT_PERSIST;  // (no wide view, or a diagnostics trace)
     int cap = f->waves_cap > 0 ? f->waves_cap : (mode == RT_VARIANT_SPLIT ? 2 : 0);
     const bool tunable = kernel == RT_KERNEL_FAST && f->tune == 1 && f->variant == RT_VARIANT_DEFAULT && !A.tile_trace;
@@ -1104,6 +1151,172 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             cap = T.cap[T.choice];
         }
     }
+    // RT_VARIANT_HYBRID: which launch this frame of the shape and camera gets. The first frame measures (k_persist
+    // with per-tile times, copied to the host behind it); once they have arrived, the tile lists of every candidate
+    // threshold are built at once, and the next frames try the candidates one each — k_persist itself and the
+    // hybrid launch for each of HYBRID_CANDS — reading their HIP-event times without
+    // blocking once the last has finished, and keep the fastest (PRT_TUNE_LOG=1 prints them). rt_frame.hot_pct > 0
+    // fixes the threshold instead (no trials). Returns -2: measure; -1: a k_persist frame; c >= 0: candidate c's
+    // hybrid launch (lists at ctx->hy). rc: a HIP failure.
+    auto hybrid_pick = [&](int& rc) -> int {
+        rt_ctx::Hybrid& h = ctx->hy;
+        const float cv[12] = {cam->pos.x,   cam->pos.y,   cam->pos.z,   cam->ul.x,    cam->ul.y,    cam->ul.z,
+                              cam->inc_x.x, cam->inc_x.y, cam->inc_x.z, cam->inc_y.x, cam->inc_y.y, cam->inc_y.z};
+        const bool same = h.scene == ctx->scene_gen && h.W == f->width && h.rows == f->n_rows && h.off == f->row_offset &&
+                          h.stride == f->row_stride && h.block == rb && h.bounces == f->bounces && h.spp == f->spp &&
+                          h.dealing == f->dealing && h.pct_req == f->hot_pct && std::memcmp(h.cam, cv, sizeof cv) == 0;
+        auto err = [&](hipError_t e, const char* what) { rc = fail(ctx, e, what); return -1; };
+        if (!h.ev) {
+            hipError_t e = hipEventCreateWithFlags(&h.ev, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&h.fork, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&h.join, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipStreamCreateWithFlags(&h.s2, hipStreamNonBlocking);
+            if (e != hipSuccess) return err(e, "rt_render: hybrid events / stream");
+        }
+        if (!same) {  // a new shape or camera: measure it
+            if (h.state == 1) {  // an earlier measurement's copy into h_tr must land first
+                const hipError_t e = hipEventSynchronize(h.ev);
+                if (e != hipSuccess) return err(e, "rt_render: hybrid measurement");
+            }
+            h.scene = ctx->scene_gen;
+            h.W = f->width;
+            h.rows = f->n_rows;
+            h.off = f->row_offset;
+            h.stride = f->row_stride;
+            h.block = rb;
+            h.bounces = f->bounces;
+            h.spp = f->spp;
+            h.dealing = f->dealing;
+            h.pct_req = f->hot_pct;
+            std::memcpy(h.cam, cv, sizeof cv);
+            h.n_tiles = (size_t)A.n_tiles;
+            if (h.tr_cap < h.n_tiles) {
+                if (h.d_tr) (void)hipFree(h.d_tr);
+                if (h.h_tr) (void)hipHostFree(h.h_tr);
+                h.d_tr = h.h_tr = nullptr;
+                h.tr_cap = 0;
+                hipError_t e = hipMalloc((void**)&h.d_tr, sizeof(unsigned long long) * 4 * h.n_tiles);
+                if (e == hipSuccess) e = hipHostMalloc((void**)&h.h_tr, sizeof(unsigned long long) * 4 * h.n_tiles,
+                                                       hipHostMallocDefault);
+                if (e != hipSuccess) return err(e, "rt_render: hybrid tile times");
+                h.tr_cap = h.n_tiles;
+            }
+            h.state = 0;
+        }
+        if (h.state == 0) return -2;
+        if (h.state == 1) {
+            const hipError_t q = hipEventQuery(h.ev);
+            if (q == hipErrorNotReady) {
+                (void)hipGetLastError();  // not an error: the measuring frame is still running
+                return -1;
+            }
+            if (q != hipSuccess) return err(q, "rt_render: hybrid measurement");
+            // the tile lists of every candidate threshold: [hot coop tiles][cold 8x8 tiles], one after another
+            const int tx = A.tiles_x, ty = A.n_tiles / A.tiles_x;
+            std::vector<long long> dur(h.n_tiles);
+            long long cmax = 1;
+            for (size_t t = 0; t < h.n_tiles; t++) {
+                dur[t] = (long long)(h.h_tr[4 * t + 1] - h.h_tr[4 * t]);
+                cmax = std::max(cmax, dur[t]);
+            }
+            std::vector<int> ord = centre_out(tx, ty);
+            if (!dealt_centre_out)
+                for (int t = 0; t < (int)ord.size(); t++) ord[t] = t;  // RT_DEAL_ROW_MAJOR
+            h.cold_regions = xcd_mode >= 1 && xcd_mode <= 3 && dealt_centre_out;
+            h.nc = 0;
+            if (f->hot_pct > 0) {
+                h.pct[0] = f->hot_pct;
+                h.lanes[0] = 4;
+                h.fan[0] = false;
+                h.nc = 1;
+            } else {
+                h.pct[0] = 0;  // k_persist
+                h.nc = 1;
+                for (const HotCand& hc : HYBRID_CANDS) {
+                    if (hc.lanes == 0 && !fan_ok) continue;
+                    h.pct[h.nc] = hc.pct;
+                    h.fan[h.nc] = hc.lanes == 0;
+                    h.lanes[h.nc++] = hc.lanes == 0 ? fan_r : hc.lanes;
+                }
+            }
+            std::vector<int> lists;
+            for (int c = 0; c < h.nc; c++) {
+                h.at[c] = lists.size();
+                h.n_hot[c] = h.n_cold[c] = 0;
+                if (h.pct[c] == 0) continue;
+                std::vector<int> hot8;
+                for (size_t t = 0; t < h.n_tiles; t++)
+                    if (dur[t] * 100 > (long long)h.pct[c] * cmax) hot8.push_back((int)t);
+                std::stable_sort(hot8.begin(), hot8.end(), [&](int a, int b) { return dur[a] > dur[b]; });
+                if (hot8.size() > h.n_tiles / 2) hot8.resize(h.n_tiles / 2);  // k_coop costs ~2x the wave time
+                std::vector<char> is_hot(h.n_tiles, 0);
+                // each 8x8 tile = (8 / TW) x (8 / TH) tiles of the hot kernel (rtd::GTile), hottest first
+                int tw, th;
+                hot_tile(h.lanes[c], tw, th);
+                const int ctw = (f->width + tw - 1) / tw, cth = (f->n_rows + th - 1) / th;
+                for (int t : hot8) {
+                    is_hot[t] = 1;
+                    for (int qy = 0; qy < 8 / th; qy++)
+                        for (int qx = 0; qx < 8 / tw; qx++) {
+                            const int cx = (t % tx) * (8 / tw) + qx, cy = (t / tx) * (8 / th) + qy;
+                            if (cx < ctw && cy < cth) lists.push_back(cy * ctw + cx);
+                        }
+                }
+                h.n_hot[c] = (int)(lists.size() - h.at[c]);
+                std::vector<int> cold;
+                for (int t : ord)
+                    if (!is_hot[t]) cold.push_back(t);
+                h.n_cold[c] = (int)cold.size();
+                if (h.cold_regions) cold = region_layout(cold, tx, ty, xcd_mode);
+                lists.insert(lists.end(), cold.begin(), cold.end());
+            }
+            if (h.lists_cap < lists.size()) {  // nothing in flight reads the lists: the measuring frame has finished
+                if (h.d_lists) (void)hipFree(h.d_lists);
+                h.d_lists = nullptr;
+                h.lists_cap = 0;
+                const hipError_t e = hipMalloc((void**)&h.d_lists, sizeof(int) * std::max<size_t>(1, lists.size()));
+                if (e != hipSuccess) return err(e, "rt_render: hybrid lists");
+                h.lists_cap = lists.size();
+            }
+            if (!lists.empty()) {
+                const hipError_t e = hipMemcpy(h.d_lists, lists.data(), sizeof(int) * lists.size(), hipMemcpyHostToDevice);
+                if (e != hipSuccess) return err(e, "rt_render: hybrid lists");
+            }
+            for (int c = 0; c < h.nc; c++) h.launch[c] = -1;  // (k_persist too: the measuring frame also copied)
+            h.choice = h.nc == 1 ? 0 : -1;
+            h.state = 2;
+        }
+        if (h.choice >= 0) return h.pct[h.choice] == 0 ? -1 : h.choice;
+        for (int c = 0; c < h.nc; c++)
+            if (h.launch[c] < 0 || ctx->launches - h.launch[c] >= rt_ctx::NEV) {  // untried (or its events reused)
+                h.launch[c] = ctx->launches;
+                return h.pct[c] == 0 ? -1 : c;
+            }
+        long long last = 0;
+        for (int c = 0; c < h.nc; c++) last = std::max(last, h.launch[c]);
+        const hipError_t q = hipEventQuery(ctx->ev1s[last % rt_ctx::NEV]);
+        if (q == hipErrorNotReady) {
+            (void)hipGetLastError();
+            return -1;  // the trials are still running
+        }
+        if (q != hipSuccess) return err(q, "rt_render: hybrid trials");
+        int best = 0;
+        for (int c = 0; c < h.nc; c++) {
+            const int sl = (int)(h.launch[c] % rt_ctx::NEV);
+            const hipError_t e = hipEventElapsedTime(&h.ms[c], ctx->ev0s[sl], ctx->ev1s[sl]);
+            if (e != hipSuccess) return err(e, "rt_render: hybrid trials");
+            if (h.ms[c] < h.ms[best]) best = c;
+        }
+        h.choice = best;
+        if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1) {
+            std::fprintf(stderr, "[prt hybrid] %dx%d b%d:", f->width, f->n_rows, f->bounces);
+            for (int c = 0; c < h.nc; c++)
+                std::fprintf(stderr, " %s%d/%s%d %.3f ms", h.pct[c] ? "hot>" : "persist", h.pct[c],
+                             h.fan[c] ? "fan" : "coop", h.lanes[c], h.ms[c]);
+            std::fprintf(stderr, " -> %d\n", best);
+        }
+        return h.pct[best] == 0 ? -1 : best;
+    };
     // one frame of configuration (variant, cap); d_work holds the persistent grids' work counters, and the
     // ray counters restart with every launch (rt_get_stats reports the frame, not the trial launches)
     auto dispatch = [&](int md, int cp) -> int {
@@ -1116,7 +1329,14 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             k<<<grid, rtd::BLOCK, 0, ctx->stream>>>(A);
             return RT_OK;
         }
-        if (md == RT_VARIANT_SPLIT) return f->bounces <= 4 ? launch_split<4>(ctx, A, count, cp) : launch_split<8>(ctx, A, count, cp);
+        if (md == RT_VARIANT_SPLIT) {
+            rtd::KArgs P = A;
+            if (region_off && n_frames > 1) {  // batches: k_persist's XCD-aware regions
+                P.region_off = region_off;
+                P.tile_order = region_order;
+            }
+            return f->bounces <= 4 ? launch_split<4>(ctx, P, count, cp) : launch_split<8>(ctx, P, count, cp);
+        }
         if (md == RT_VARIANT_FAN || (md >= RT_VARIANT_COOP2 && md <= RT_VARIANT_COOP8)) {
             rtd::KArgs B = A;
             const int gr = md == RT_VARIANT_FAN ? fan_r : md == RT_VARIANT_COOP2 ? 2 : md == RT_VARIANT_COOP4 ? 4 : 8;
@@ -1154,6 +1374,27 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         if (region_off) {
             P.region_off = region_off;
             P.tile_order = region_order;
+        }
+        if (md == RT_VARIANT_HYBRID) {
+            int rc = RT_OK;
+            const int pick = hybrid_pick(rc);
+            if (rc) return rc;
+            // the frame's HIP-event time starts here, after the host work of the pick (the trials compare them)
+            HIPC(hipEventRecord(ctx->ev0, ctx->stream));
+            if (pick >= 0) return f->bounces <= 4 ? launch_hybrid<4>(ctx, A, count, pick) : launch_hybrid<8>(ctx, A, count, pick);
+            rt_ctx::Hybrid& h = ctx->hy;
+            if (pick == -2) {  // measuring frame: k_persist with per-tile times, copied to the host behind it
+                P.tile_trace = h.d_tr;
+                if (f->bounces <= 4) launch_paths<4>(P, RT_VARIANT_PERSIST, count, ctx->device, ctx->stream, cp);
+                else launch_paths<8>(P, RT_VARIANT_PERSIST, count, ctx->device, ctx->stream, cp);
+                HIPC(hipGetLastError());
+                HIPC(hipMemcpyAsync(h.h_tr, h.d_tr, sizeof(unsigned long long) * 4 * h.n_tiles, hipMemcpyDeviceToHost,
+                                    ctx->stream));
+                HIPC(hipEventRecord(h.ev, ctx->stream));
+                h.state = 1;
+                return RT_OK;
+            }
+            md = RT_VARIANT_PERSIST;  // k_persist chosen, or the measurement / trials still on their way
         }
         if (f->bounces <= 4) launch_paths<4>(P, md, count, ctx->device, ctx->stream, cp);
         else launch_paths<8>(P, md, count, ctx->device, ctx->stream, cp);
@@ -1286,12 +1527,14 @@ namespace {
 template <int MAXB>
 int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count, int cap_a) {
     const int nl = A.s.n_lights;
-    A.nslots = (size_t)A.n_tiles * 64;
+    // a record slot per lane of every (frame, tile) item of the batch: item * 64 + lane (rt_split.hpp)
+    const size_t items = (size_t)A.n_tiles * (size_t)A.n_frames;
+    A.nslots = items * 64;
     int rc;
     if ((rc = grow(ctx, &ctx->d_srec, ctx->srec_cap, (size_t)A.bounces * A.nslots * 3)) ||
         (rc = grow(ctx, &ctx->d_spinfo, ctx->spinfo_cap, A.nslots)) ||
         (rc = grow(ctx, &ctx->d_svis, ctx->svis_cap, (size_t)A.bounces * std::max(nl, 1) * A.nslots)) ||
-        (rc = grow(ctx, &ctx->d_sbatch, ctx->sbatch_cap, (size_t)A.n_tiles * A.bounces * std::max(nl, 1))))
+        (rc = grow(ctx, &ctx->d_sbatch, ctx->sbatch_cap, items * A.bounces * std::max(nl, 1))))
         return rc;
     A.srec = ctx->d_srec;
     A.spinfo = ctx->d_spinfo;
@@ -1299,13 +1542,59 @@ int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count, int cap_a) {
     A.sbatch = ctx->d_sbatch;
     hipStream_t s = ctx->stream;
     auto ka = count ? rtd::k_split_closest<MAXB, true> : rtd::k_split_closest<MAXB, false>;
+    if (A.n_frames > 1) ka = count ? rtd::k_split_closest<MAXB, true, true> : rtd::k_split_closest<MAXB, false, true>;
     auto kb = count ? rtd::k_split_shadow<true> : rtd::k_split_shadow<false>;
     // persistent grids; a block is one wave per SIMD, so the cap is waves per SIMD
-    const int ga = std::max(1, std::min(resident(ka, ctx->device, cap_a), (A.n_tiles + 3) / 4));
+    const int ga = std::max(1, (int)std::min<size_t>((size_t)resident(ka, ctx->device, cap_a), (items + 3) / 4));
     const int gb = std::max(1, resident(kb, ctx->device, 8));
     ka<<<ga, rtd::BLOCK, 0, s>>>(A);
     kb<<<gb, rtd::BLOCK, 0, s>>>(A);
     rtd::k_split_resolve<MAXB><<<(int)((A.nslots + 255) / 256), 256, 0, s>>>(A);
+    return RT_OK;
+}
+}  // namespace
+
+namespace {
+// RT_VARIANT_HYBRID, one frame: the hot coop tiles (ctx->hy lists) through k_coop<4> on the context's second
+// stream while k_persist renders the cold 8x8 tiles on the context stream; both persistent grids together fill
+// the chip (the coop grid is sized to start every hot tile at once), and the context stream waits for both.
+template <int MAXB>
+int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c) {
+    rt_ctx::Hybrid& h = ctx->hy;
+    const int n_hot = h.n_hot[c], n_cold = h.n_cold[c];
+    int* lists = h.d_lists + h.at[c];
+    auto kp = count ? rtd::k_persist<MAXB, false, true> : rtd::k_persist<MAXB, false, false>;
+    const int g = h.lanes[c];
+    auto kc = count ? rtd::k_coop<MAXB, true, 4> : rtd::k_coop<MAXB, false, 4>;
+    if (g == 2) kc = count ? rtd::k_coop<MAXB, true, 2> : rtd::k_coop<MAXB, false, 2>;
+    if (h.fan[c]) {
+        kc = count ? rtd::k_fan<MAXB, true, 4> : rtd::k_fan<MAXB, false, 4>;
+        if (g == 2) kc = count ? rtd::k_fan<MAXB, true, 2> : rtd::k_fan<MAXB, false, 2>;
+        if (g == 8) kc = count ? rtd::k_fan<MAXB, true, 8> : rtd::k_fan<MAXB, false, 8>;
+    }
+    int tw, th;
+    hot_tile(g, tw, th);
+    rtd::KArgs B = A;  // the hot kernel's tiles, dealt hottest first from their own work counter
+    B.tiles_x = (A.W + tw - 1) / tw;
+    B.n_tiles = n_hot;
+    B.tile_order = lists;
+    B.region_off = nullptr;
+    B.work = A.work + 224;
+    rtd::KArgs P = A;
+    P.n_tiles = n_cold;
+    P.region_off = h.cold_regions ? lists + n_hot : nullptr;
+    P.tile_order = lists + n_hot + (h.cold_regions ? 9 : 0);
+    const int rp = resident(kp, ctx->device), rcp = resident(kc, ctx->device);
+    const int nc = std::max(1, std::min((n_hot + 3) / 4, rcp / 2));
+    const int np = std::max(1, std::min(rp - (int)((long long)nc * rp / rcp), (n_cold + 3) / 4));
+    HIPC(hipEventRecord(h.fork, ctx->stream));  // after the work / counter resets
+    HIPC(hipStreamWaitEvent(h.s2, h.fork, 0));
+    if (n_hot > 0) kc<<<nc, rtd::BLOCK, 0, h.s2>>>(B);
+    HIPC(hipGetLastError());
+    if (n_cold > 0) kp<<<np, rtd::BLOCK, 0, ctx->stream>>>(P);
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(h.join, h.s2));
+    HIPC(hipStreamWaitEvent(ctx->stream, h.join, 0));
     return RT_OK;
 }
 }  // namespace
@@ -1787,6 +2076,11 @@ extern "C" int rt_get_stats(rt_ctx* ctx, rt_stats* st) {
     st->stack_overflows = c[rtd::C_ERR];
     st->node_bytes = 8 * c[rtd::C_NB];
     st->wave_steps = c[rtd::C_WS];
+    st->shadow_wave_steps = c[rtd::C_WSH];
+    st->steps_lanes_16 = c[rtd::C_Q1];
+    st->steps_lanes_32 = c[rtd::C_Q2];
+    st->steps_lanes_48 = c[rtd::C_Q3];
+    st->steps_lanes_64 = c[rtd::C_Q4];
     if (c[rtd::C_ERR]) {
         ctx->err = "traversal stack overflow: BVH deeper than 32 levels";
         return RT_E_STATE;
@@ -1823,6 +2117,13 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
             if (t.e0[i]) (void)hipEventDestroy(t.e0[i]);
             if (t.e1[i]) (void)hipEventDestroy(t.e1[i]);
         }
+    if (ctx->hy.s2) (void)hipStreamSynchronize(ctx->hy.s2);
+    if (ctx->hy.d_tr) (void)hipFree(ctx->hy.d_tr);
+    if (ctx->hy.h_tr) (void)hipHostFree(ctx->hy.h_tr);
+    if (ctx->hy.d_lists) (void)hipFree(ctx->hy.d_lists);
+    for (hipEvent_t e : {ctx->hy.ev, ctx->hy.fork, ctx->hy.join})
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->hy.s2) (void)hipStreamDestroy(ctx->hy.s2);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

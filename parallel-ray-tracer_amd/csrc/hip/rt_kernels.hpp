@@ -35,11 +35,13 @@ enum {
     C_PRIM, C_REFL, C_SHAD, C_SKIP, C_HITS, C_CHI, C_CHL, C_CHT, C_SHI, C_SHL, C_SHT, C_PIX, C_ERR, C_FALLBACK,
     C_NB,  // node/leaf record bytes read, in 8-B units (RT_FLAG_COUNTERS)
     C_WS,  // wave-level wide-node steps (RT_FLAG_COUNTERS): lane visits / (64 x this) = SIMD efficiency
-    NCOUNT = 16
+    C_WSH,  // of which shadow walks' (k_persist's walks, RT_FLAG_COUNTERS)
+    C_Q1, C_Q2, C_Q3, C_Q4,  // wave steps with 1-16 / 17-32 / 33-48 / 49-64 active lanes (same)
+    NCOUNT = 21
 };
 
 struct Ctr {
-    unsigned prim, refl, shad, skip, hits, chi, chl, cht, shi, shl, sht, pix, err, fb, nb, ws;
+    unsigned prim, refl, shad, skip, hits, chi, chl, cht, shi, shl, sht, pix, err, fb, nb, ws, wsh, q1, q2, q3, q4;
 };
 
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
@@ -51,10 +53,10 @@ __device__ __forceinline__ unsigned wave_sum(unsigned v) {
 template <bool COUNT>
 __device__ __forceinline__ void flush(const Ctr& c, unsigned long long* g) {
     const bool l0 = (threadIdx.x & 63) == 0;
-    unsigned v[NCOUNT] = {c.prim, c.refl, c.shad, c.skip, c.hits, c.chi, c.chl, c.cht,
-                          c.shi, c.shl, c.sht, c.pix, c.err, c.fb, c.nb, c.ws};
+    unsigned v[NCOUNT] = {c.prim, c.refl, c.shad, c.skip, c.hits, c.chi, c.chl, c.cht, c.shi, c.shl, c.sht,
+                          c.pix,  c.err,  c.fb,   c.nb,   c.ws,   c.wsh, c.q1,  c.q2,  c.q3,  c.q4};
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
+    for (int i = 0; i < NCOUNT; i++) {
         if (!COUNT && ((i >= C_CHI && i <= C_SHT) || i >= C_NB)) continue;
         unsigned s = wave_sum(v[i]);
         if (l0 && s) atomicAdd(g + i, (unsigned long long)s);
@@ -283,6 +285,19 @@ __device__ __forceinline__ unsigned first_active_lane() {
     return (unsigned)((threadIdx.x & 63u) == (unsigned)__builtin_ctzll(ex));
 }
 
+// k_persist's walks (RT_FLAG_COUNTERS): one wave step, by walk kind and by the number of active lanes
+__device__ __forceinline__ void count_step(Ctr& c, bool shadow) {
+    const unsigned long long ex = __builtin_amdgcn_read_exec();
+    const unsigned f = (unsigned)((threadIdx.x & 63u) == (unsigned)__builtin_ctzll(ex));
+    const unsigned b = ((unsigned)__builtin_popcountll(ex) - 1u) >> 4;
+    c.ws += f;
+    if (shadow) c.wsh += f;
+    c.q1 += b == 0 ? f : 0u;
+    c.q2 += b == 1 ? f : 0u;
+    c.q3 += b == 2 ? f : 0u;
+    c.q4 += b == 3 ? f : 0u;
+}
+
 __device__ __forceinline__ float ubyte(unsigned w, int b) { return (float)((w >> (8 * b)) & 0xFFu); }
 
 // Tests the 8 children of wide node `node`: nh = hit interior slots as bits (s ^ oct), th = triangle
@@ -400,7 +415,7 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
             c.chi++;
             c.chl += nl;
             c.nb += 10;
-            c.ws += first_active_lane();
+            count_step(c, false);
         }
         const int next = wide_next(nh, cb, imask, oct, sp, stk, wcap);
         if (next >= 0) N = wload(W, next);
@@ -477,7 +492,7 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
             c.shi++;
             c.shl += nl;
             c.nb += 10;
-            c.ws += first_active_lane();
+            count_step(c, true);
         }
         const int next = wide_next(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
         if (next >= 0) N = wload(W, next);

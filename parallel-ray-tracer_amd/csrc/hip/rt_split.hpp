@@ -14,44 +14,50 @@
 //                     (raytracer.c:149-160, the same expressions as path_step), the fold, the clamp.
 // Every per-pixel operation is path_step's, only moved: results are k_persist's bit for bit. Kernel
 // boundaries order the hand-offs (no fences, no waiting inside a kernel). spp == 1, lights <= 32.
+// Frame batches (BATCH, rt_render_frames): the closest kernel deals (frame, tile) items like k_persist
+// (rtd::next_item: XCD-aware regions, every frame's central tiles first); a record slot is
+// item * 64 + lane with item = frame * n_tiles + tile, so the three kernels cover the whole batch.
 #pragma once
 #include "rt_kernels.hpp"
 
 namespace rtd {
 
 constexpr unsigned SPLIT_TAIL = 1u << 8, SPLIT_MISS = 1u << 9;  // path info: L | flags
-constexpr int SPLIT_BATCH_AT = 32, SPLIT_TAKE_AT = 64;          // KArgs::work slots (separate 128-B lines)
+// KArgs::work slots (separate 128-B lines, past next_item's 8 region counters at 16 r)
+constexpr int SPLIT_BATCH_AT = 160, SPLIT_TAKE_AT = 192;
 
 // per (level, slot) record: f4[0] = ip, light mask (bits); f4[1] = n, material (bits); f4[2] = d, 0
 __device__ __forceinline__ size_t srec_at(const KArgs& A, int it, size_t slot) {
     return ((size_t)it * A.nslots + slot) * 3;
 }
 
-template <int MAXB, bool COUNT>
+template <int MAXB, bool COUNT, bool BATCH = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(3))) void k_split_closest(KArgs A) {
     __shared__ int lds[STACK * BLOCK];
     int* stk = lds + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const DScene& s = A.s;
     Ctr c = {};
+    int reg = 0;
     for (;;) {
-        unsigned tile = 0;
-        if (lane == 0) tile = atomicAdd(A.work, 1u);
-        tile = __shfl(tile, 0, 64);
-        if (tile >= (unsigned)A.n_tiles) break;
-        if (A.tile_order) tile = (unsigned)A.tile_order[tile];
+        int frame;
+        unsigned tile;
+        if (!next_item(A, lane, reg, frame, tile)) break;
         const int x = (int)(tile % (unsigned)A.tiles_x) * 8 + (lane & 7);
         const int k = (int)(tile / (unsigned)A.tiles_x) * 8 + (lane >> 3);
-        const size_t slot = (size_t)tile * 64 + lane;
+        const unsigned item = (unsigned)frame * (unsigned)A.n_tiles + tile;
+        const size_t slot = (size_t)item * 64 + lane;
         unsigned info = 0;
         unsigned masks[MAXB];
 #pragma unroll
         for (int q = 0; q < MAXB; q++) masks[q] = 0;
-        if (x < A.W && k < A.n_rows && image_row(A, k) < A.H) {
+        const int y = image_row(A, k, frame);
+        if (x < A.W && k < A.n_rows && y < A.H) {
             c.pix++;
-            const size_t px = (size_t)k * A.W + x;
-            v3 o = mk(A.pos[0], A.pos[1], A.pos[2]);
-            v3 d = primary_dir(A, (float)x, (float)image_row(A, k));
+            const size_t px = (size_t)frame * A.frame_px + (size_t)k * A.W + x;
+            const Cam C = cam_of<BATCH>(A, frame);
+            v3 o = C.pos;
+            v3 d = primary_dir(C, (float)x, (float)y);
             if (A.bounce_hit)
                 for (int i = 0; i < A.bounces; i++) A.bounce_hit[px * A.bounces + i] = -2;
             for (int it = 0; it < A.bounces; ++it) {
@@ -114,7 +120,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                 const unsigned long long any = __ballot((mk_ >> j) & 1u);
                 if (any && lane == 0) {
                     const unsigned at = atomicAdd(A.work + SPLIT_BATCH_AT, 1u);
-                    A.sbatch[at] = (tile << 8) | ((unsigned)it << 5) | (unsigned)j;
+                    A.sbatch[at] = (item << 8) | ((unsigned)it << 5) | (unsigned)j;
                 }
             }
         }
@@ -135,8 +141,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK))) void k_split_s
         b = __shfl(b, 0, 64);
         if (b >= nb) break;
         const unsigned e = A.sbatch[b];
-        const unsigned tile = e >> 8, it = (e >> 5) & 7u, j = e & 31u;
-        const size_t slot = (size_t)tile * 64 + lane;
+        const unsigned item = e >> 8, it = (e >> 5) & 7u, j = e & 31u;
+        const size_t slot = (size_t)item * 64 + lane;
         const float4 f0 = A.srec[srec_at(A, (int)it, slot)];
         if ((__float_as_uint(f0.w) >> j) & 1u) {  // light_v past the back-face test, raytracer.c:72-74
             const v3 ip = xyz(f0), Lp = xyz(A.s.lights[2 * j]);
@@ -158,7 +164,8 @@ __global__ __launch_bounds__(256) void k_split_resolve(KArgs A) {
     const unsigned info = A.spinfo[slot];
     const int L = (int)(info & 0xFFu);
     if (!L) return;  // outside the frame
-    const unsigned tile = (unsigned)(slot >> 6), lane = (unsigned)(slot & 63);
+    const unsigned item = (unsigned)(slot >> 6), lane = (unsigned)(slot & 63);
+    const unsigned frame = item / (unsigned)A.n_tiles, tile = item % (unsigned)A.n_tiles;
     const int x = (int)(tile % (unsigned)A.tiles_x) * 8 + (int)(lane & 7u);
     const int k = (int)(tile / (unsigned)A.tiles_x) * 8 + (int)(lane >> 3);
     const DScene& s = A.s;
@@ -204,7 +211,7 @@ __global__ __launch_bounds__(256) void k_split_resolve(KArgs A) {
         seti<MAXB>(mats, it, m);
     }
     const v3 col = clamp01(fold_path<MAXB>(s, cols, mats, L, (info & SPLIT_TAIL) != 0));
-    store_px(A.rgb, A.bgra, (size_t)k * A.W + x, col);
+    store_px(A.rgb, A.bgra, (size_t)frame * A.frame_px + (size_t)k * A.W + x, col);
 }
 
 }  // namespace rtd

@@ -59,11 +59,13 @@ class Frame(ctypes.Structure):
                 ("row_stride", ctypes.c_int), ("n_rows", ctypes.c_int), ("bounces", ctypes.c_int),
                 ("spp", ctypes.c_int), ("kernel", ctypes.c_int), ("row_block", ctypes.c_int),
                 ("frame_shift", ctypes.c_int), ("variant", ctypes.c_int), ("tune", ctypes.c_int),
-                ("waves_cap", ctypes.c_int), ("dealing", ctypes.c_int), ("regroup", ctypes.c_int)]
+                ("waves_cap", ctypes.c_int), ("dealing", ctypes.c_int), ("regroup", ctypes.c_int),
+                ("hot_pct", ctypes.c_int)]
 
 
 STAT_FIELDS = ["primary", "reflection", "shadow", "shadow_skipped", "hits", "ch_inner", "ch_leaf",
-               "ch_tri", "sh_inner", "sh_leaf", "sh_tri", "pixels", "fallbacks", "stack_overflows", "node_bytes", "wave_steps"]
+               "ch_tri", "sh_inner", "sh_leaf", "sh_tri", "pixels", "fallbacks", "stack_overflows", "node_bytes", "wave_steps",
+               "shadow_wave_steps", "steps_lanes_16", "steps_lanes_32", "steps_lanes_48", "steps_lanes_64"]
 
 
 class WbvhInfo(ctypes.Structure):

@@ -16,7 +16,7 @@ KERNELS = {"auto": 0, "strict": 1, "fast": 2}
 # rt_frame.variant (launch configurations of the fast kernel, include/rt_hip.h); a variant name is also
 # accepted as `kernel` (kernel="coop4" == kernel="fast", variant="coop4")
 VARIANTS = {"default": 0, "persist": 1, "persist4": 2, "split": 3, "coop2": 4, "coop4": 5, "coop8": 6, "fan": 7,
-            "pool": 10}
+            "pool": 10, "hybrid": 11}
 DEALING = {"default": 0, "global": 1, "rows": 2, "columns": 3, "blocks": 4, "row_major": 5}
 ACCEL = {"auto": 0, "reference": 1, "gpu": 2, "host": 3}
 ACCEL_NAMES = {v: k for k, v in ACCEL.items()}
@@ -202,13 +202,13 @@ class Renderer:
         self.scene = scene
         return self
 
-    def _frame(self, width, height, rows, bounces, spp, kernel, variant, tune, waves_cap, dealing, regroup):
+    def _frame(self, width, height, rows, bounces, spp, kernel, variant, tune, waves_cap, dealing, regroup, hot_pct=0):
         ro, rs, nr, rb, sh = _rows(rows, height)
         if isinstance(kernel, str) and kernel in VARIANTS:
             kernel, variant = "fast", kernel
         v = VARIANTS.get(variant, variant) if variant is not None else 0
         return Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel), rb, sh, v,
-                     1 if tune else 0, waves_cap, DEALING.get(dealing, dealing), regroup), nr
+                     1 if tune else 0, waves_cap, DEALING.get(dealing, dealing), regroup, hot_pct), nr
 
     def _outputs(self, nf, nr, width, bounces, rgb, hit, t, bounce_hit, bgra):
         import torch
@@ -220,14 +220,16 @@ class Renderer:
                        _ptr(bgra, "bgra", n, (torch.int32, getattr(torch, "uint32", torch.int32)), self.device))
 
     def render(self, cam, width, height, rows=None, bounces=4, spp=1, kernel="auto", rgb=None, hit=None, t=None,
-               bounce_hit=None, bgra=None, variant=None, tune=False, waves_cap=0, dealing="default", regroup=0):
+               bounce_hit=None, bgra=None, variant=None, tune=False, waves_cap=0, dealing="default", regroup=0,
+               hot_pct=0):
         """render_frame(): asynchronous. rows = (offset, stride, n[, block[, frame_shift]]) (rt_frame; prt.dist)
         or None for the full frame.
         rgb / hit / t / bounce_hit ([n, W, bounces] int32) / bgra ([n, W] int32: the BMP-quantised pixel in
         top-down rows, rt_outputs.bgra): optional device tensors (torch: checked for size, dtype, device and
-        contiguity) or raw pointers. variant / tune / waves_cap / dealing / regroup: the fast kernel's launch
-        configuration (rt_frame; VARIANTS, DEALING)."""
-        f, nr = self._frame(width, height, rows, bounces, spp, kernel, variant, tune, waves_cap, dealing, regroup)
+        contiguity) or raw pointers. variant / tune / waves_cap / dealing / regroup / hot_pct: the fast kernel's
+        launch configuration (rt_frame; VARIANTS, DEALING)."""
+        f, nr = self._frame(width, height, rows, bounces, spp, kernel, variant, tune, waves_cap, dealing, regroup,
+                            hot_pct)
         out = self._outputs(1, nr, width, bounces, rgb, hit, t, bounce_hit, bgra)
         self._chk(_L.rt_render(self._ctx, ctypes.byref(cam), ctypes.byref(f), ctypes.byref(out)), "rt_render")
         self._last = (width, nr)

@@ -395,7 +395,7 @@ def test_cli_drop_in_writes_the_reference_bmp(tmp_path):
 
 @pytest.mark.parametrize("name", ["car_boxed", "sportscar", "dragon"])
 def test_split_pipeline_equals_persistent_kernel(dev, name):
-    """RT_VARIANT_SPLIT (closest/shadow/resolve, the default for >= 3 lights) against RT_VARIANT_PERSIST, on
+    """RT_VARIANT_SPLIT (closest/shadow/resolve; measured slower than k_persist in round 3) against RT_VARIANT_PERSIST, on
     1-, 4- and 2-light scenes: bit-exact to each other and to the fixtures, with identical ray counts"""
     s = host.Scene.named(name).build_bvh(3)
     outs = {}
@@ -410,6 +410,27 @@ def test_split_pipeline_equals_persistent_kernel(dev, name):
     if fx:
         ref = np.load(os.path.join(GOLD, fx))
         assert same_bits(b["rgb"], ref["rgb"])
+    # a frame batch (three cameras, XCD-aware dealing of (frame, tile) items) through the three kernels
+    import torch
+    W, H = 96, 54
+    cams = [host.camera(W, H), moved_camera(W, H, 0.25, 0.0), moved_camera(W, H, -0.4, 0.3)]
+    bat = {}
+    for v in ("persist4", "split"):
+        r = dev.Renderer(0, counters=True)
+        r.upload(s)
+        rgb = torch.full((3, H, W, 3), -1.0, dtype=torch.float32, device="cuda")
+        hit = torch.full((3, H, W), -7, dtype=torch.int32, device="cuda")
+        bg = torch.zeros((3, H, W), dtype=torch.int32, device="cuda")
+        r.render_frames(cams, W, H, kernel=v, rgb=rgb, hit=hit, bgra=bg)
+        r.sync()
+        bat[v] = (rgb.cpu().numpy(), hit.cpu().numpy(), bg.cpu().numpy(), r.stats())
+        r.close()
+    a, b = bat["persist4"], bat["split"]
+    assert same_bits(a[0], b[0]) and same_bits(b[0][0], outs["split"]["rgb"])
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[2], b[2])
+    for k in ("primary", "reflection", "shadow", "shadow_skipped", "hits", "pixels"):
+        assert a[3][k] == b[3][k], k
 
 
 @pytest.mark.parametrize("name,n_cand", [("sportscar", 7), ("car_boxed", 7), ("dragon", 7)])
@@ -449,7 +470,7 @@ def moved_camera(W, H, dx, dz):
     return c
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "strict"])
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "strict", "split"])
 @pytest.mark.parametrize("name", ["car_boxed", "dragon"])
 def test_frame_batch_equals_single_frames(dev, name, kernel):
     """rt_render_frames: a batch of frames (different cameras, one persistent launch on the fast paths)
@@ -651,3 +672,52 @@ def test_rotated_row_blocks_cover_every_frame(dev, kernel):
     with pytest.raises(dev.RtError):  # rotation is a fast-kernel feature
         r.render_frames(cams, W, H, rows=(0, N * B, n, B, B), kernel="strict")
     r.close()
+
+
+@pytest.mark.parametrize("name", ["dragon", "car_boxed"])
+def test_hybrid_frames_equal_persistent_frames(dev, name):
+    """RT_VARIANT_HYBRID (rt_hip.hip launch_hybrid): the measuring frame (k_persist with per-tile times), frames
+    while the measurement is in flight, and the frames after it (the costliest tiles through k_coop<4> on a second
+    stream, the rest through k_persist) all equal a forced k_persist frame bit for bit, with the same ray counts;
+    also for a row subset, a moved camera (measured again), and the thresholds that make every / no tile hot"""
+    import torch
+    s = host.Scene.named(name).build_bvh(3)
+    W, H = 200, 120
+    for rows, pct in ((None, 0), (None, 1), (None, 100), ((8, 24, 40, 8), 0), (None, 60)):
+        nr = rows[2] if rows else H
+        cams = [host.camera(W, H), moved_camera(W, H, 0.25, 0.0)]
+        for cam in cams:
+            ref = render_cam(dev, s, W, H, cam, "persist", rows=rows)
+            r = dev.Renderer(0, counters=True)
+            r.upload(s)
+            # frame 0 measures, frame 1 is issued while the measurement is in flight (the default launch, most
+            # likely), frames 2.. (each after a sync) try the candidate thresholds and k_persist, then the choice
+            for group in ((0, 1),) + tuple((i,) for i in range(2, 10)):
+                outs = []
+                for frame in group:
+                    hit = torch.full((nr, W), -7, dtype=torch.int32, device="cuda")
+                    rgb = torch.zeros((nr, W, 3), dtype=torch.float32, device="cuda")
+                    r.render(cam, W, H, rows=rows, kernel="hybrid", hot_pct=pct, rgb=rgb, hit=hit)
+                    outs.append((frame, hit, rgb))
+                r.sync()
+                for frame, hit, rgb in outs:
+                    np.testing.assert_array_equal(hit.cpu().numpy(), ref["hit"])
+                    assert same_bits(rgb.cpu().numpy(), ref["rgb"]), (rows, pct, frame)
+                st = r.stats()
+                for k in ("primary", "reflection", "shadow", "shadow_skipped", "hits", "pixels"):
+                    assert st[k] == ref["stats"][k], (rows, pct, group, k)
+            r.close()
+
+
+def render_cam(dev, scene, W, H, cam, kernel, rows=None):
+    import torch
+    r = dev.Renderer(0, counters=True)
+    r.upload(scene)
+    nr = rows[2] if rows else H
+    hit = torch.empty((nr, W), dtype=torch.int32, device="cuda")
+    rgb = torch.empty((nr, W, 3), dtype=torch.float32, device="cuda")
+    r.render(cam, W, H, rows=rows, kernel=kernel, rgb=rgb, hit=hit)
+    r.sync()
+    out = {"rgb": rgb.cpu().numpy(), "hit": hit.cpu().numpy(), "stats": r.stats()}
+    r.close()
+    return out

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Single-frame latency as the reference's loop sees it (cpu/src/main.c:171-185, gpu/src/main.cu:110-115: one
+render_frame() per iteration, each waited for): per launch configuration, `--iters` frames through rt_render,
+each followed by rt_sync; median HIP-event kernel ms and median host wall ms per frame over the second half, bit-exactness of the
+last frame against the first configuration.
+usage: python tools/latency.py [--scene dragon] [--iters 20] persist hybrid hybrid:hot_pct=50 ..."""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "parallel-ray-tracer_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="dragon")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("variants", nargs="+")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    from prt import device, host
+    s = host.Scene.named(a.scene).build_bvh(3)
+    W, H = a.width, a.height
+    cam = host.camera(W, H)
+    ref = None
+    for spec in a.variants:
+        name, _, opts = spec.partition(":")
+        kw = {k: (int(v) if v.lstrip("-").isdigit() else v) for k, v in (o.split("=") for o in opts.split(",") if o)}
+        r = device.Renderer(0)
+        r.upload(s)
+        rgb = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        ks, ws = [], []
+        for _ in range(a.iters):
+            t0 = time.perf_counter()
+            r.render(cam, W, H, kernel=name, rgb=rgb, **kw)
+            ks.append(r.sync())
+            ws.append((time.perf_counter() - t0) * 1e3)
+        got = rgb.cpu().numpy()
+        r.close()
+        if ref is None:
+            ref = got
+        same = np.array_equal(got.view(np.int32), ref.view(np.int32))
+        h = a.iters // 2  # the second half: after any measuring / trial frames
+        print(f"{a.scene:10s} {spec:22s} bit-exact {same!s:5s} kernel ms median {statistics.median(ks[h:]):.3f} "
+              f"min {min(ks[h:]):.3f} first {ks[0]:.3f}  wall ms median {statistics.median(ws[h:]):.3f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
