@@ -76,6 +76,10 @@ typedef struct rt_scene_info {
     int accel_built;            /* RT_ACCEL_* of the fast walk's BVH as built (RT_ACCEL_HOST = host binned SAH, RT_ACCEL_GPU = PLOC on the device) */
     float build_ms;             /* host wall time of the acceleration build (binary tree + wide collapse) */
     float gpu_build_ms;         /* of which the GPU tree build (RT_ACCEL_GPU; incl. transfers) */
+    int unit_triangles;         /* triangles a unit-length ray can hit (|e1 x e2| >= EPSILON: hit_triangle's det cull,
+                                   cpu/src/raytracer.c:41-45), indexed by the view reflection and shadow rays walk;
+                                   0: that view is the full one */
+    int unit_nodes, unit_depth; /* its 8-wide BVH */
 } rt_scene_info;
 
 /* rt_frame.kernel */

@@ -108,7 +108,7 @@ __device__ __forceinline__ void wide_node_g(const WNode& nd, const RayPre& p, un
         const float tfy = __builtin_fmaf((float)((fyw >> sh) & 0xFFu), ky, ay);
         const float tnz = __builtin_fmaf((float)((nzw >> sh) & 0xFFu), kz, az);
         const float tfz = __builtin_fmaf((float)((fzw >> sh) & 0xFFu), kz, az);
-        const float lo = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f));
+        const float lo = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, BOX_TMIN));
         const float hi = fminf(fminf(tfx, tfy), fminf(tfz, lim));
         hit |= lo <= hi ? (1u << s) : 0u;
     }
@@ -254,14 +254,15 @@ __device__ __forceinline__ bool visible_wide_g(const DWide& W, v3 o, v3 d, float
 
 template <int G, bool COUNT>
 __device__ __forceinline__ int closest_g(const DScene& s, v3 o, v3 d, float& best, int& nd, int* __restrict__ stk,
-                                         Ctr& c, unsigned q) {
+                                         Ctr& c, unsigned q, bool unit) {
     int hp = -1;
     bool tie = false;
     best = FMAX;
     nd = 0;
     if (!degenerate(d)) {
-        closest_wide_g<G, COUNT>(s.wide, o, d, best, hp, nd, tie, stk, c, q);
-        if (!tie) return hp >= 0 ? s.wide.tri_orig[hp] : -1;
+        const DWide& W = wide_for(s, unit);
+        closest_wide_g<G, COUNT>(W, o, d, best, hp, nd, tie, stk, c, q);
+        if (!tie) return hp >= 0 ? W.tri_orig[hp] : -1;
         hp = -1;
         best = FMAX;
         nd = 0;
@@ -274,7 +275,7 @@ __device__ __forceinline__ int closest_g(const DScene& s, v3 o, v3 d, float& bes
 template <int G, bool COUNT>
 __device__ __forceinline__ bool visible_g(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c,
                                           unsigned q) {
-    if (!degenerate(d)) return visible_wide_g<G, COUNT>(s.wide, o, d, ld2, stk, c, q);
+    if (!degenerate(d)) return visible_wide_g<G, COUNT>(wide_for(s, true), o, d, ld2, stk, c, q);  // |d| = 1
     c.fb++;
     return visible_walk<true, COUNT, true>(s.ref, o, d, ld2, stk, c);
 }

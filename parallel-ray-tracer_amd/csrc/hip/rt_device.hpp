@@ -59,6 +59,10 @@ struct DScene {
     const float4* __restrict__ lights;
     int n_lights;
     float amb_x, amb_y, amb_z;
+    // the fast walk's view for unit-length directions (reflection and shadow rays): `wide` without the triangles
+    // no such ray can hit — hit_triangle culls |det| < EPS and |det| <= |n| |d| (rt_hip.hip unit_view); nodes ==
+    // nullptr: `wide` serves every ray
+    DWide unit;
 };
 
 struct KArgs {
@@ -106,7 +110,7 @@ struct KArgs {
 // agree on every offset (an LDS pointer, 32-bit on gfx950 but 64-bit on the host, once shifted every
 // later field and hung a kernel). Pinned sizes catch such drift at compile time in whichever pass
 // disagrees; never put address-space-qualified pointers in these structs.
-static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 144 && sizeof(KArgs) == 408,
+static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 168 && sizeof(KArgs) == 432,
               "kernel-argument layout changed: update the pinned sizes only after checking both passes agree");
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

@@ -65,6 +65,10 @@ struct rt_ctx {
     float4 *wide_nodes = nullptr, *wide_tris = nullptr;
     int* wide_orig = nullptr;
     int wide_n = 0, wide_depth = 0;
+    // the unit-direction view (rtd::DScene::unit): the wide BVH over the triangles a unit-length ray can hit
+    float4 *unit_nodes = nullptr, *unit_tris = nullptr;
+    int* unit_orig = nullptr;
+    int unit_n = 0, unit_depth = 0, unit_tris_n = 0;
     float4* d_shade = nullptr;
     float4* d_mats = nullptr;
     float4* d_lights = nullptr;
@@ -203,6 +207,11 @@ void free_scene(rt_ctx* ctx) {
     ctx->wide_nodes = ctx->wide_tris = nullptr;
     ctx->wide_orig = nullptr;
     ctx->wide_n = ctx->wide_depth = 0;
+    for (void* p : {(void*)ctx->unit_nodes, (void*)ctx->unit_tris, (void*)ctx->unit_orig})
+        if (p) (void)hipFree(p);
+    ctx->unit_nodes = ctx->unit_tris = nullptr;
+    ctx->unit_orig = nullptr;
+    ctx->unit_n = ctx->unit_depth = ctx->unit_tris_n = 0;
     for (void* p : {(void*)ctx->d_shade, (void*)ctx->d_mats, (void*)ctx->d_lights})
         if (p) (void)hipFree(p);
     ctx->d_shade = nullptr;
@@ -505,6 +514,66 @@ int gpu_ploc(rt_ctx* ctx, const rt_triangle* T, int n, int R, std::vector<rt_bvh
 }
 }  // namespace
 
+namespace {
+// Reflection and shadow rays have unit-length directions (raytracer.c:153,166), and hit_triangle culls
+// |det| < EPSILON with det = -d . n (raytracer.c:41-45): in float, |det| <= |n| |d| (1 + 7 u) with |d| <= 1 + 3 u,
+// so a triangle whose (precomputed, tri_records) |n| is below EPS (1 - 1e-5) can never be hit by such a ray. On the
+// BASELINE scenes that is 22 % (dragon stand-in), 23 % (car_boxed), 28 % (two_cars), 81 % (sportscar stand-in) and
+// 99.7 % (dragon871k) of the triangles: the wide view built without them serves the unit-direction walks, the
+// full one the primary rays (whose directions are not normalised, main.c:229-233).
+constexpr double UNIT_KEEP = 1.0 - 1e-5;  // x EPSILON (1e-3f, raytracer.c:19)
+bool unit_hittable(const rt_triangle& t) {
+    const rt_vec3 &a = t.coords[0], &b = t.coords[1], &c = t.coords[2];  // n as tri_records forms it
+    const float e1x = b.x - a.x, e1y = b.y - a.y, e1z = b.z - a.z;
+    const float e2x = c.x - a.x, e2y = c.y - a.y, e2z = c.z - a.z;
+    const float nx = e1y * e2z - e1z * e2y, ny = e1z * e2x - e1x * e2z, nz = e1x * e2y - e1y * e2x;
+    return std::sqrt((double)nx * nx + (double)ny * ny + (double)nz * nz) >= UNIT_KEEP * (double)rtd::EPS;
+}
+
+// The 8-wide quantised view of a triangle set, built as the full view was (`method`: RT_ACCEL_GPU = PLOC on the
+// device, else the host binned SAH), same inflation and node price. RT_E_STATE: none (too deep for the wide walk).
+int wide_view(rt_ctx* ctx, const rt_triangle* T, int n, int method, int R, float inflate, float cnode,
+              std::vector<float4>& wn, std::vector<float4>& wt, std::vector<int>& wo, int& depth) {
+    rt_bvh_node* nodes = nullptr;
+    int nlen = 0;
+    int* idx = nullptr;
+    std::vector<rt_bvh_node> gnodes;
+    std::vector<int> gidx;
+    bool gpu = false;
+    if (method == RT_ACCEL_GPU) {
+        int gdepth = 0;
+        const int rc = gpu_ploc(ctx, T, n, R, gnodes, gidx, gdepth);
+        if (rc == RT_E_HIP) return rc;
+        gpu = rc == RT_OK;
+    }
+    if (gpu) {
+        nodes = gnodes.data();
+        nlen = (int)gnodes.size();
+        idx = gidx.data();
+    } else if (rth_bvh_build(T, (size_t)n, RTH_BVH_BINNED_SAH, nullptr, &nodes, &nlen, &idx, nullptr) != RT_OK) {
+        return RT_E_STATE;
+    }
+    uint32_t* words = nullptr;
+    int* order = nullptr;
+    rth_wbvh_info wi{};
+    int rc = RT_E_STATE;
+    if (rth_wbvh_build_cost(nodes, nlen, idx, T, n, inflate, cnode, &words, &order, &wi) == RT_OK && wi.depth <= rtd::WSTACK) {
+        wn.resize(5 * (size_t)wi.n_nodes);
+        std::memcpy(wn.data(), words, sizeof(uint32_t) * 20 * (size_t)wi.n_nodes);
+        tri_records(T, order, n, wt, wo);
+        depth = wi.depth;
+        rc = RT_OK;
+    }
+    rth_free(words);
+    rth_free(order);
+    if (!gpu) {
+        rth_free(nodes);
+        rth_free(idx);
+    }
+    return rc;
+}
+}  // namespace
+
 extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     if (!ctx) return RT_E_ARG;
     if (!sc || !sc->triangles || !sc->bvh || !sc->tri_idx || sc->n_triangles <= 0 || sc->n_nodes <= 0)
@@ -597,6 +666,39 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
         }
         own_acc = built != RT_ACCEL_GPU;  // (no binary acceleration view for a GPU-built tree)
     }
+    // the unit-direction view (reflection and shadow rays): the same build over the triangles such a ray can hit
+    std::vector<float4> unit_nodes, unit_tris;
+    std::vector<int> unit_orig;
+    int unit_depth = 0, unit_tris_n = 0;
+    if (!wide_nodes.empty()) {
+        std::vector<rt_triangle> sub;
+        std::vector<int> sub_id;
+        for (int i = 0; i < n; i++)
+            if (unit_hittable(sc->triangles[i])) {
+                sub.push_back(sc->triangles[i]);
+                sub_id.push_back(i);
+            }
+        if (!sub.empty() && (int)sub.size() < n) {
+            float mx = 16.0f;  // the full view's inflation (all triangles' coordinate magnitude)
+            for (int i = 0; i < n; i++)
+                for (const rt_vec3& c : sc->triangles[i].coords)
+                    mx = std::max(mx, std::max(std::fabs(c.x), std::max(std::fabs(c.y), std::fabs(c.z))));
+            const int R = sc->ploc_radius > 0 ? std::min(sc->ploc_radius, rtb::PLOC_R_MAX) : rtb::PLOC_R;
+            rc = wide_view(ctx, sub.data(), (int)sub.size(), built, R, std::ldexp(mx, -16), sc->collapse_node_cost,
+                           unit_nodes, unit_tris, unit_orig, unit_depth);
+            if (rc == RT_E_HIP) return rc;
+            if (rc == RT_OK) {
+                for (int& o : unit_orig) o = sub_id[o];  // subset position -> original triangle index
+                unit_tris_n = (int)sub.size();
+            } else {  // no usable view: the full one serves every ray
+                unit_nodes.clear();
+                unit_tris.clear();
+                unit_orig.clear();
+                unit_depth = 0;
+            }
+            rc = RT_OK;
+        }
+    }
     const float build_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_build).count();
     // materials: distinct (ks, kd, kr) triples of triangle_t (the reference stores them per triangle)
     std::unordered_map<std::string, int> mat_id;
@@ -631,12 +733,18 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
         (rc = upload(ctx, &ctx->d_lights, lights)) ||
         (!wide_nodes.empty() && ((rc = upload(ctx, &ctx->wide_nodes, wide_nodes)) ||
                                  (rc = upload(ctx, &ctx->wide_tris, wide_tris)) ||
-                                 (rc = upload(ctx, &ctx->wide_orig, wide_orig))))) {
+                                 (rc = upload(ctx, &ctx->wide_orig, wide_orig)))) ||
+        (!unit_nodes.empty() && ((rc = upload(ctx, &ctx->unit_nodes, unit_nodes)) ||
+                                 (rc = upload(ctx, &ctx->unit_tris, unit_tris)) ||
+                                 (rc = upload(ctx, &ctx->unit_orig, unit_orig))))) {
         free_scene(ctx);
         return rc;
     }
     ctx->wide_n = (int)(wide_nodes.size() / 5);
     ctx->wide_depth = wide_depth;
+    ctx->unit_n = (int)(unit_nodes.size() / 5);
+    ctx->unit_depth = unit_depth;
+    ctx->unit_tris_n = unit_nodes.empty() ? 0 : unit_tris_n;
     ctx->n_lights = sc->n_lights;
     ctx->n_tris = n;
     ctx->amb[0] = sc->amb.x;
@@ -649,6 +757,9 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     ctx->info.n_lights = sc->n_lights;
     ctx->info.wide_nodes = ctx->wide_n;
     ctx->info.wide_depth = wide_depth;
+    ctx->info.unit_triangles = ctx->unit_tris_n;
+    ctx->info.unit_nodes = ctx->unit_n;
+    ctx->info.unit_depth = unit_depth;
     ctx->info.accel_built = built;
     ctx->info.build_ms = build_ms;
     ctx->info.gpu_build_ms = gpu_ms;
@@ -879,6 +990,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     A.s.ref = dview(ctx->ref);
     A.s.acc = ctx->acc.nodes ? dview(ctx->acc) : A.s.ref;
     A.s.wide = rtd::DWide{ctx->wide_nodes, ctx->wide_tris, ctx->wide_orig};
+    A.s.unit = rtd::DWide{ctx->unit_nodes, ctx->unit_tris, ctx->unit_orig};
     A.s.shade = ctx->d_shade;
     A.s.mats = ctx->d_mats;
     A.s.lights = ctx->d_lights;
@@ -943,7 +1055,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     }
     A.pathbuf = ctx->d_pathbuf;
     A.gstack = ctx->d_gstack;
-    A.wcap = ctx->wide_n > 0 ? std::max(1, ctx->wide_depth) : 0;
+    A.wcap = ctx->wide_n > 0 ? std::max(1, std::max(ctx->wide_depth, ctx->unit_depth)) : 0;
     if (n_frames > 1) {  // the batch's cameras, uploaded when they change (pinned staging, stream-ordered)
         const size_t nf = 12 * (size_t)n_frames;
         static_assert(sizeof(rt_camera) == 48, "rt_camera = 4 x rt_vec3");

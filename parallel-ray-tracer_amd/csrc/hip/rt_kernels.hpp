@@ -272,6 +272,12 @@ __device__ __forceinline__ bool visible_walk(const DBvh& B, v3 o, v3 d, float ld
 // Same result semantics as closest_walk<false>: min t over all triangles, boxes pruned at
 // best * PRUNE_SLACK so that exact ties are always met and reported.
 constexpr int WSTACK = 16;  // node-group entries (2 ints) in the STACK-int LDS column; builder depth <= 16
+// A child box left before t = EPS holds no hit: hit_triangle accepts t > EPS only (raytracer.c:56), and the
+// computed far plane lies beyond the true box by the inflation (>= 20x the triangle test's rounding of t), so
+// every triangle point inside has t below the computed exit. Testing the interval from EPS instead of 0 prunes
+// such boxes for free — above all the flat boxes of the surface a shadow or reflection ray starts on (a wall's
+// whole subtree is a stack of flat boxes around the ray's origin).
+constexpr float BOX_TMIN = EPS;
 // Shadow walks visit a node's hit children FAR first (visiting order k ^ (octant ^ 7): from the light's side
 // toward the ray origin; the closest walks stay near-first). An any-hit walk's result does not depend on the
 // order; far-first meets an occluder sooner on average — a shadow ray leaves a surface whose own neighbourhood
@@ -346,8 +352,8 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
         const float tfz = __builtin_fmaf(ubyte(bz ? lz[h] : hz[h], b), kz, az);
         // Inflation (2^-16 max|coord|) puts every computed near plane strictly before and every far plane
         // strictly after the child's true box, per axis, so the interval below contains the true one; the
-        // folded test max(tmin, 0) <= min(tmax, lim) only adds visits (e.g. tmax == 0): conservative.
-        const float lo = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f));
+        // folded test max(tmin, BOX_TMIN) <= min(tmax, lim) only adds visits: conservative (BOX_TMIN below).
+        const float lo = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, BOX_TMIN));
         const float hi = fminf(fminf(tfx, tfy), fminf(tfz, lim));
         hit8 |= lo <= hi ? (1u << s) : 0u;
     }
@@ -547,11 +553,18 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
     return true;
 }
 
+// The fast walk's wide view for a ray: the unit-direction view (a superset of every triangle such a ray can hit)
+// for reflection and shadow rays, the full one for primary rays (unnormalised directions, main.c:229-233)
+__device__ __forceinline__ const DWide& wide_for(const DScene& s, bool unit) {
+    return unit && s.unit.nodes ? s.unit : s.wide;
+}
+
 // Closest hit with the kernel's policy; returns the ORIGINAL triangle index (-1 = miss).
 // sstk (nullable): the binary walks' stack when the wide walk's `stk` holds only wcap entries (DYN kernels)
+// unit: d has unit length (a reflection ray): the unit-direction view serves the fast walk
 template <bool STRICT, bool COUNT, bool REG = true, bool PIPE = false>
 __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best, int& nd, int* __restrict__ stk,
-                                       Ctr& c, int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
+                                       Ctr& c, int* __restrict__ sstk = nullptr, int wcap = WSTACK, bool unit = false) {
     int* __restrict__ bstk = sstk ? sstk : stk;
     int hp = -1;
     bool tie = false;
@@ -559,8 +572,9 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
     nd = 0;
     if (!STRICT && !degenerate(d)) {
         if (s.wide.nodes) {
-            closest_wide<COUNT, PIPE>(s.wide, o, d, best, hp, nd, tie, stk, c, wcap);
-            if (!tie) return hp >= 0 ? s.wide.tri_orig[hp] : -1;
+            const DWide& W = wide_for(s, unit);
+            closest_wide<COUNT, PIPE>(W, o, d, best, hp, nd, tie, stk, c, wcap);
+            if (!tie) return hp >= 0 ? W.tri_orig[hp] : -1;
         } else {
             closest_walk<false, COUNT, REG>(s.acc, o, d, best, hp, nd, tie, bstk, c);
             if (!tie) return hp >= 0 ? s.acc.tri_orig[hp] : -1;
@@ -581,7 +595,7 @@ __device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, 
                                         int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
     int* __restrict__ bstk = sstk ? sstk : stk;
     if (!STRICT && !degenerate(d)) {
-        if (s.wide.nodes) return visible_wide<COUNT, PIPE>(s.wide, o, d, ld2, stk, c, wcap);
+        if (s.wide.nodes) return visible_wide<COUNT, PIPE>(wide_for(s, true), o, d, ld2, stk, c, wcap);  // |d| = 1
         return visible_walk<false, COUNT, REG>(s.acc, o, d, ld2, bstk, c);
     }
     if (!STRICT) c.fb++;
@@ -591,7 +605,7 @@ __device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, 
 // group-cooperative walks (rt_coop.hpp): G lanes per ray
 template <int G, bool COUNT>
 __device__ __forceinline__ int closest_g(const DScene& s, v3 o, v3 d, float& best, int& nd, int* __restrict__ stk,
-                                         Ctr& c, unsigned q);
+                                         Ctr& c, unsigned q, bool unit);
 template <int G, bool COUNT>
 __device__ __forceinline__ bool visible_g(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c,
                                           unsigned q);
@@ -644,8 +658,8 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
     if (it == 0) c.prim++;
     else c.refl++;
     int orig;
-    if constexpr (G > 1) orig = closest_g<G, COUNT>(s, o, d, best, nd, stk, c, q);
-    else orig = closest<STRICT, COUNT, REG>(s, o, d, best, nd, stk, c, sstk, wcap);
+    if constexpr (G > 1) orig = closest_g<G, COUNT>(s, o, d, best, nd, stk, c, q, it > 0);
+    else orig = closest<STRICT, COUNT, REG>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0);  // it > 0: |d| = 1
     if (it == 0) {
         hit0 = orig;
         t0 = best;

@@ -65,7 +65,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
                 int nd;
                 if (it == 0) c.prim++;
                 else c.refl++;
-                const int orig = closest<false, COUNT, true, true>(s, o, d, best, nd, stk, c);
+                const int orig = closest<false, COUNT, true, true>(s, o, d, best, nd, stk, c, nullptr, WSTACK, it > 0);
                 if (it == 0) {
                     if (A.hit) A.hit[px] = orig;
                     if (A.t) A.t[px] = best;

@@ -90,3 +90,35 @@ def test_gpu_build_random_mode_and_fallback():
         ref = np.load(os.path.join(GOLD, fx + ".npz"))
         np.testing.assert_array_equal(out["hit"], ref["hit"])
         assert same_bits(out["rgb"], ref["rgb"])
+
+
+def unit_hittable_count(scene):
+    """triangles a unit-length ray can hit: |e1 x e2| (float, tri_records' roundings) >= EPSILON (1 - 1e-5)
+    (hit_triangle's |det| < EPSILON cull, cpu/src/raytracer.c:41-45)"""
+    co = np.array(np.asarray(scene.triangles)["coords"].tolist(), dtype=np.float32)
+    e1, e2 = co[:, 1] - co[:, 0], co[:, 2] - co[:, 0]
+    n = np.stack([e1[:, 1] * e2[:, 2] - e1[:, 2] * e2[:, 1], e1[:, 2] * e2[:, 0] - e1[:, 0] * e2[:, 2],
+                  e1[:, 0] * e2[:, 1] - e1[:, 1] * e2[:, 0]], axis=1).astype(np.float64)
+    return int((np.sqrt((n * n).sum(1)) >= (1.0 - 1e-5) * float(np.float32(1e-3))).sum())
+
+
+@pytest.mark.parametrize("name,W,H,fixture", [("car_boxed", 160, 90, "car_boxed_160x90_strict"),
+                                              ("dragon", 96, 54, "dragon_96x54_strict"),
+                                              ("sportscar", 96, 54, "sportscar_96x54_strict")])
+def test_unit_direction_view_renders_the_reference_fixture(name, W, H, fixture):
+    """the unit-direction view (reflection and shadow rays walk a wide BVH without the triangles hit_triangle's
+    |det| < EPSILON cull hides from every unit-length ray, rt_hip.hip unit_hittable): built over exactly the
+    triangles the criterion keeps, and every kernel still renders the reference fixture's bits with the
+    reference's ray counts"""
+    s = host.Scene.named(name).build_bvh(3)
+    want = unit_hittable_count(s)
+    n = s.n_triangles
+    ref = np.load(os.path.join(GOLD, fixture + ".npz"))
+    for kernel in ("fast", "persist4", "coop4", "split"):
+        out = render(s, W, H, kernel, counters=True)
+        info = out["info"]
+        assert 0 < want < n and info["unit_triangles"] == want, (info, want, n)
+        assert info["unit_nodes"] > 0 and info["unit_depth"] <= 16
+        np.testing.assert_array_equal(out["hit"], ref["hit"])
+        assert same_bits(out["t"], ref["t"]) and same_bits(out["rgb"], ref["rgb"]), kernel
+
