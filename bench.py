@@ -487,7 +487,7 @@ def main():
     # the drop-in seam as the reference drives it (gpu/src/main.cu:110-115: one render_frame per iteration, each
     # waited for), with the default launch rule (RT_VARIANT_HYBRID: its measuring and trial frames first)
     hyb = []
-    for _ in range(16):
+    for _ in range(26):  # the measuring frame, 2 x 8 trials, then the choice
         rl.render(cam, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp, kernel=args.kernel,
                   **out(fg.target(0)[0] if F > 1 else fg.target(0)))
         hyb.append(rl.sync())
@@ -552,7 +552,7 @@ def main():
             "frame_latency_detail": {"tuned_ms": lat_tuned, "default_rule_ms": lat_default,
                                      "rule": "min of the autotuned launch (tune=1, min of 2 frames) and the default "
                                              "rule's steady state (RT_VARIANT_HYBRID, render + sync per frame, median "
-                                             "of the last 6 of 16 frames)"},
+                                             "of the last 6 of 26 frames)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": k_avg_ms, "alg_bytes_per_launch": bytes_launch, "frames_per_launch": F,

@@ -80,6 +80,10 @@ typedef struct rt_scene_info {
                                    cpu/src/raytracer.c:41-45), indexed by the view reflection and shadow rays walk;
                                    0: that view is the full one */
     int unit_nodes, unit_depth; /* its 8-wide BVH */
+    int primary_triangles;      /* triangles a direction of length <= 3 can hit, indexed by the view primary rays walk
+                                   when every primary direction of a launch is that short (the reference camera's are
+                                   1.87-2.77); 0: no such view (it would leave out < 2 % of the triangles) */
+    int primary_nodes;
 } rt_scene_info;
 
 /* rt_frame.kernel */

@@ -63,6 +63,9 @@ struct DScene {
     // no such ray can hit — hit_triangle culls |det| < EPS and |det| <= |n| |d| (rt_hip.hip unit_view); nodes ==
     // nullptr: `wide` serves every ray
     DWide unit;
+    // the view for this launch's primary rays: `wide` without the triangles no direction of length <= PRIMARY_D can
+    // hit (the host sets it only when every primary direction of the frame is that short); nullptr: `wide`
+    DWide prim;
 };
 
 struct KArgs {
@@ -110,7 +113,7 @@ struct KArgs {
 // agree on every offset (an LDS pointer, 32-bit on gfx950 but 64-bit on the host, once shifted every
 // later field and hung a kernel). Pinned sizes catch such drift at compile time in whichever pass
 // disagrees; never put address-space-qualified pointers in these structs.
-static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 168 && sizeof(KArgs) == 432,
+static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 192 && sizeof(KArgs) == 456,
               "kernel-argument layout changed: update the pinned sizes only after checking both passes agree");
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

@@ -69,6 +69,10 @@ struct rt_ctx {
     float4 *unit_nodes = nullptr, *unit_tris = nullptr;
     int* unit_orig = nullptr;
     int unit_n = 0, unit_depth = 0, unit_tris_n = 0;
+    // the primary view (rtd::DScene::prim): the wide BVH over the triangles a direction of length <= PRIMARY_D can hit
+    float4 *prim_nodes = nullptr, *prim_tris = nullptr;
+    int* prim_orig = nullptr;
+    int prim_n = 0, prim_depth = 0, prim_tris_n = 0;
     float4* d_shade = nullptr;
     float4* d_mats = nullptr;
     float4* d_lights = nullptr;
@@ -150,7 +154,8 @@ struct rt_ctx {
         int pct[NCAND] = {}, lanes[NCAND] = {}, n_hot[NCAND] = {}, n_cold[NCAND] = {};
         bool fan[NCAND] = {};  // the hot tiles through k_fan<lanes> instead of k_coop<lanes>
         size_t at[NCAND] = {};
-        long long launch[NCAND] = {};
+        static constexpr int ROUNDS = 2;  // trials per candidate (the minimum counts: single frames are noisy)
+        long long launch[NCAND][ROUNDS] = {};
         float ms[NCAND] = {};
         unsigned long long* d_tr = nullptr;  // [tiles][4], rtd::k_persist's TRACE records
         unsigned long long* h_tr = nullptr;  // pinned
@@ -212,6 +217,11 @@ void free_scene(rt_ctx* ctx) {
     ctx->unit_nodes = ctx->unit_tris = nullptr;
     ctx->unit_orig = nullptr;
     ctx->unit_n = ctx->unit_depth = ctx->unit_tris_n = 0;
+    for (void* p : {(void*)ctx->prim_nodes, (void*)ctx->prim_tris, (void*)ctx->prim_orig})
+        if (p) (void)hipFree(p);
+    ctx->prim_nodes = ctx->prim_tris = nullptr;
+    ctx->prim_orig = nullptr;
+    ctx->prim_n = ctx->prim_depth = ctx->prim_tris_n = 0;
     for (void* p : {(void*)ctx->d_shade, (void*)ctx->d_mats, (void*)ctx->d_lights})
         if (p) (void)hipFree(p);
     ctx->d_shade = nullptr;
@@ -521,13 +531,39 @@ namespace {
 // BASELINE scenes that is 22 % (dragon stand-in), 23 % (car_boxed), 28 % (two_cars), 81 % (sportscar stand-in) and
 // 99.7 % (dragon871k) of the triangles: the wide view built without them serves the unit-direction walks, the
 // full one the primary rays (whose directions are not normalised, main.c:229-233).
+// Primary rays are not normalised (main.c:229-233): a launch whose primary directions are all at most PRIMARY_D
+// long (the reference camera's are 1.87-2.77) walks a view without the triangles no such direction can hit.
 constexpr double UNIT_KEEP = 1.0 - 1e-5;  // x EPSILON (1e-3f, raytracer.c:19)
-bool unit_hittable(const rt_triangle& t) {
+constexpr double PRIMARY_D = 3.0;
+// can a direction of length <= dmax hit the triangle (|n| >= EPSILON (1 - 1e-5) / dmax)?
+bool hittable(const rt_triangle& t, double dmax) {
     const rt_vec3 &a = t.coords[0], &b = t.coords[1], &c = t.coords[2];  // n as tri_records forms it
     const float e1x = b.x - a.x, e1y = b.y - a.y, e1z = b.z - a.z;
     const float e2x = c.x - a.x, e2y = c.y - a.y, e2z = c.z - a.z;
     const float nx = e1y * e2z - e1z * e2y, ny = e1z * e2x - e1x * e2z, nz = e1x * e2y - e1y * e2x;
-    return std::sqrt((double)nx * nx + (double)ny * ny + (double)nz * nz) >= UNIT_KEEP * (double)rtd::EPS;
+    return std::sqrt((double)nx * nx + (double)ny * ny + (double)nz * nz) >= UNIT_KEEP * (double)rtd::EPS / dmax;
+}
+
+// Upper bound on |d| of every primary ray of a frame, d = ((ul - pos) + inc_x * fx) + inc_y * fy for
+// fx in [0, W], fy in [0, H] (main.c:229-233; spp samples stay inside their pixel): |d| is convex in (fx, fy), so
+// its maximum is at a corner; the float evaluation adds at most a few ulp of the terms' magnitudes (1e-5 of them
+// here, ~80x that).
+double primary_dmax(const rt_camera* c, int W, int H) {
+    const double bx = (double)c->ul.x - c->pos.x, by = (double)c->ul.y - c->pos.y, bz = (double)c->ul.z - c->pos.z;
+    double m = 0.0;
+    for (int cx = 0; cx < 2; cx++)
+        for (int cy = 0; cy < 2; cy++) {
+            const double x = cx ? W : 0, y = cy ? H : 0;
+            const double dx = bx + c->inc_x.x * x + c->inc_y.x * y, dy = by + c->inc_x.y * x + c->inc_y.y * y,
+                         dz = bz + c->inc_x.z * x + c->inc_y.z * y;
+            m = std::max(m, std::sqrt(dx * dx + dy * dy + dz * dz));
+        }
+    const double terms = std::sqrt(bx * bx + by * by + bz * bz) +
+                         W * std::sqrt((double)c->inc_x.x * c->inc_x.x + (double)c->inc_x.y * c->inc_x.y +
+                                       (double)c->inc_x.z * c->inc_x.z) +
+                         H * std::sqrt((double)c->inc_y.x * c->inc_y.x + (double)c->inc_y.y * c->inc_y.y +
+                                       (double)c->inc_y.z * c->inc_y.z);
+    return m * (1.0 + 1e-5) + 1e-5 * terms;
 }
 
 // The 8-wide quantised view of a triangle set, built as the full view was (`method`: RT_ACCEL_GPU = PLOC on the
@@ -674,7 +710,7 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
         std::vector<rt_triangle> sub;
         std::vector<int> sub_id;
         for (int i = 0; i < n; i++)
-            if (unit_hittable(sc->triangles[i])) {
+            if (hittable(sc->triangles[i], 1.0)) {
                 sub.push_back(sc->triangles[i]);
                 sub_id.push_back(i);
             }
@@ -695,6 +731,40 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
                 unit_tris.clear();
                 unit_orig.clear();
                 unit_depth = 0;
+            }
+            rc = RT_OK;
+        }
+    }
+    // the primary view: the same build over the triangles a direction of length <= PRIMARY_D can hit (only when
+    // that leaves out at least 2 % of them)
+    std::vector<float4> prim_nodes, prim_tris;
+    std::vector<int> prim_orig;
+    int prim_depth = 0, prim_tris_n = 0;
+    if (!wide_nodes.empty()) {
+        std::vector<rt_triangle> sub;
+        std::vector<int> sub_id;
+        for (int i = 0; i < n; i++)
+            if (hittable(sc->triangles[i], PRIMARY_D)) {
+                sub.push_back(sc->triangles[i]);
+                sub_id.push_back(i);
+            }
+        if (!sub.empty() && sub.size() < (size_t)n - (size_t)n / 50) {
+            float mx = 16.0f;
+            for (int i = 0; i < n; i++)
+                for (const rt_vec3& c : sc->triangles[i].coords)
+                    mx = std::max(mx, std::max(std::fabs(c.x), std::max(std::fabs(c.y), std::fabs(c.z))));
+            const int R = sc->ploc_radius > 0 ? std::min(sc->ploc_radius, rtb::PLOC_R_MAX) : rtb::PLOC_R;
+            rc = wide_view(ctx, sub.data(), (int)sub.size(), built, R, std::ldexp(mx, -16), sc->collapse_node_cost,
+                           prim_nodes, prim_tris, prim_orig, prim_depth);
+            if (rc == RT_E_HIP) return rc;
+            if (rc == RT_OK) {
+                for (int& o : prim_orig) o = sub_id[o];
+                prim_tris_n = (int)sub.size();
+            } else {
+                prim_nodes.clear();
+                prim_tris.clear();
+                prim_orig.clear();
+                prim_depth = 0;
             }
             rc = RT_OK;
         }
@@ -736,7 +806,10 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
                                  (rc = upload(ctx, &ctx->wide_orig, wide_orig)))) ||
         (!unit_nodes.empty() && ((rc = upload(ctx, &ctx->unit_nodes, unit_nodes)) ||
                                  (rc = upload(ctx, &ctx->unit_tris, unit_tris)) ||
-                                 (rc = upload(ctx, &ctx->unit_orig, unit_orig))))) {
+                                 (rc = upload(ctx, &ctx->unit_orig, unit_orig)))) ||
+        (!prim_nodes.empty() && ((rc = upload(ctx, &ctx->prim_nodes, prim_nodes)) ||
+                                 (rc = upload(ctx, &ctx->prim_tris, prim_tris)) ||
+                                 (rc = upload(ctx, &ctx->prim_orig, prim_orig))))) {
         free_scene(ctx);
         return rc;
     }
@@ -745,6 +818,9 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     ctx->unit_n = (int)(unit_nodes.size() / 5);
     ctx->unit_depth = unit_depth;
     ctx->unit_tris_n = unit_nodes.empty() ? 0 : unit_tris_n;
+    ctx->prim_n = (int)(prim_nodes.size() / 5);
+    ctx->prim_depth = prim_depth;
+    ctx->prim_tris_n = prim_nodes.empty() ? 0 : prim_tris_n;
     ctx->n_lights = sc->n_lights;
     ctx->n_tris = n;
     ctx->amb[0] = sc->amb.x;
@@ -760,6 +836,8 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     ctx->info.unit_triangles = ctx->unit_tris_n;
     ctx->info.unit_nodes = ctx->unit_n;
     ctx->info.unit_depth = unit_depth;
+    ctx->info.primary_triangles = ctx->prim_tris_n;
+    ctx->info.primary_nodes = ctx->prim_n;
     ctx->info.accel_built = built;
     ctx->info.build_ms = build_ms;
     ctx->info.gpu_build_ms = gpu_ms;
@@ -991,6 +1069,10 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     A.s.acc = ctx->acc.nodes ? dview(ctx->acc) : A.s.ref;
     A.s.wide = rtd::DWide{ctx->wide_nodes, ctx->wide_tris, ctx->wide_orig};
     A.s.unit = rtd::DWide{ctx->unit_nodes, ctx->unit_tris, ctx->unit_orig};
+    // the primary view when every primary direction of every frame of the launch is short enough for it
+    bool prim_ok = ctx->prim_nodes != nullptr;
+    for (int i = 0; i < n_frames && prim_ok; i++) prim_ok = primary_dmax(cams + i, f->width, f->height) <= PRIMARY_D;
+    if (prim_ok) A.s.prim = rtd::DWide{ctx->prim_nodes, ctx->prim_tris, ctx->prim_orig};
     A.s.shade = ctx->d_shade;
     A.s.mats = ctx->d_mats;
     A.s.lights = ctx->d_lights;
@@ -1055,7 +1137,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     }
     A.pathbuf = ctx->d_pathbuf;
     A.gstack = ctx->d_gstack;
-    A.wcap = ctx->wide_n > 0 ? std::max(1, std::max(ctx->wide_depth, ctx->unit_depth)) : 0;
+    A.wcap = ctx->wide_n > 0 ? std::max(1, std::max(ctx->wide_depth, std::max(ctx->unit_depth, ctx->prim_depth))) : 0;
     if (n_frames > 1) {  // the batch's cameras, uploaded when they change (pinned staging, stream-ordered)
         const size_t nf = 12 * (size_t)n_frames;
         static_assert(sizeof(rt_camera) == 48, "rt_camera = 4 x rt_vec3");
@@ -1265,8 +1347,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     }
     // RT_VARIANT_HYBRID: which launch this frame of the shape and camera gets. The first frame measures (k_persist
     // with per-tile times, copied to the host behind it); once they have arrived, the tile lists of every candidate
-    // threshold are built at once, and the next frames try the candidates one each — k_persist itself and the
-    // hybrid launch for each of HYBRID_CANDS — reading their HIP-event times without
+    // threshold are built at once, and the next frames try the candidates, twice each — k_persist itself and the
+    // hybrid launch for each of HYBRID_CANDS — reading their HIP-event times (the minimum of the two) without
     // blocking once the last has finished, and keep the fastest (PRT_TUNE_LOG=1 prints them). rt_frame.hot_pct > 0
     // fixes the threshold instead (no trials). Returns -2: measure; -1: a k_persist frame; c >= 0: candidate c's
     // hybrid launch (lists at ctx->hy). rc: a HIP failure.
@@ -1394,18 +1476,21 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 const hipError_t e = hipMemcpy(h.d_lists, lists.data(), sizeof(int) * lists.size(), hipMemcpyHostToDevice);
                 if (e != hipSuccess) return err(e, "rt_render: hybrid lists");
             }
-            for (int c = 0; c < h.nc; c++) h.launch[c] = -1;  // (k_persist too: the measuring frame also copied)
+            for (int c = 0; c < h.nc; c++)  // (k_persist too: the measuring frame also copied)
+                for (int r = 0; r < rt_ctx::Hybrid::ROUNDS; r++) h.launch[c][r] = -1;
             h.choice = h.nc == 1 ? 0 : -1;
             h.state = 2;
         }
         if (h.choice >= 0) return h.pct[h.choice] == 0 ? -1 : h.choice;
-        for (int c = 0; c < h.nc; c++)
-            if (h.launch[c] < 0 || ctx->launches - h.launch[c] >= rt_ctx::NEV) {  // untried (or its events reused)
-                h.launch[c] = ctx->launches;
-                return h.pct[c] == 0 ? -1 : c;
-            }
+        for (int r = 0; r < rt_ctx::Hybrid::ROUNDS; r++)
+            for (int c = 0; c < h.nc; c++)
+                if (h.launch[c][r] < 0 || ctx->launches - h.launch[c][r] >= rt_ctx::NEV) {  // untried (or events reused)
+                    h.launch[c][r] = ctx->launches;
+                    return h.pct[c] == 0 ? -1 : c;
+                }
         long long last = 0;
-        for (int c = 0; c < h.nc; c++) last = std::max(last, h.launch[c]);
+        for (int c = 0; c < h.nc; c++)
+            for (int r = 0; r < rt_ctx::Hybrid::ROUNDS; r++) last = std::max(last, h.launch[c][r]);
         const hipError_t q = hipEventQuery(ctx->ev1s[last % rt_ctx::NEV]);
         if (q == hipErrorNotReady) {
             (void)hipGetLastError();
@@ -1414,9 +1499,14 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         if (q != hipSuccess) return err(q, "rt_render: hybrid trials");
         int best = 0;
         for (int c = 0; c < h.nc; c++) {
-            const int sl = (int)(h.launch[c] % rt_ctx::NEV);
-            const hipError_t e = hipEventElapsedTime(&h.ms[c], ctx->ev0s[sl], ctx->ev1s[sl]);
-            if (e != hipSuccess) return err(e, "rt_render: hybrid trials");
+            h.ms[c] = 1e30f;
+            for (int r = 0; r < rt_ctx::Hybrid::ROUNDS; r++) {
+                const int sl = (int)(h.launch[c][r] % rt_ctx::NEV);
+                float ms = 0.0f;
+                const hipError_t e = hipEventElapsedTime(&ms, ctx->ev0s[sl], ctx->ev1s[sl]);
+                if (e != hipSuccess) return err(e, "rt_render: hybrid trials");
+                h.ms[c] = std::min(h.ms[c], ms);
+            }
             if (h.ms[c] < h.ms[best]) best = c;
         }
         h.choice = best;

@@ -554,9 +554,11 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
 }
 
 // The fast walk's wide view for a ray: the unit-direction view (a superset of every triangle such a ray can hit)
-// for reflection and shadow rays, the full one for primary rays (unnormalised directions, main.c:229-233)
+// for reflection and shadow rays; for primary rays (unnormalised directions, main.c:229-233) the primary view when
+// the host found this launch's directions short enough for it, else the full one
 __device__ __forceinline__ const DWide& wide_for(const DScene& s, bool unit) {
-    return unit && s.unit.nodes ? s.unit : s.wide;
+    if (unit) return s.unit.nodes ? s.unit : s.wide;
+    return s.prim.nodes ? s.prim : s.wide;
 }
 
 // Closest hit with the kernel's policy; returns the ORIGINAL triangle index (-1 = miss).

@@ -81,7 +81,7 @@ class SceneInfo(ctypes.Structure):  # rt_scene_info
     _fields_ = [("n_triangles", ctypes.c_int), ("n_lights", ctypes.c_int), ("wide_nodes", ctypes.c_int),
                 ("wide_depth", ctypes.c_int), ("accel_built", ctypes.c_int), ("build_ms", ctypes.c_float),
                 ("gpu_build_ms", ctypes.c_float), ("unit_triangles", ctypes.c_int), ("unit_nodes", ctypes.c_int),
-                ("unit_depth", ctypes.c_int)]
+                ("unit_depth", ctypes.c_int), ("primary_triangles", ctypes.c_int), ("primary_nodes", ctypes.c_int)]
 
 
 _host = None

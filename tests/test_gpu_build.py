@@ -92,14 +92,14 @@ def test_gpu_build_random_mode_and_fallback():
         assert same_bits(out["rgb"], ref["rgb"])
 
 
-def unit_hittable_count(scene):
-    """triangles a unit-length ray can hit: |e1 x e2| (float, tri_records' roundings) >= EPSILON (1 - 1e-5)
-    (hit_triangle's |det| < EPSILON cull, cpu/src/raytracer.c:41-45)"""
+def unit_hittable_count(scene, dmax=1.0):
+    """triangles a direction of length <= dmax can hit: |e1 x e2| (float, tri_records' roundings) >=
+    EPSILON (1 - 1e-5) / dmax (hit_triangle's |det| < EPSILON cull, cpu/src/raytracer.c:41-45)"""
     co = np.array(np.asarray(scene.triangles)["coords"].tolist(), dtype=np.float32)
     e1, e2 = co[:, 1] - co[:, 0], co[:, 2] - co[:, 0]
     n = np.stack([e1[:, 1] * e2[:, 2] - e1[:, 2] * e2[:, 1], e1[:, 2] * e2[:, 0] - e1[:, 0] * e2[:, 2],
                   e1[:, 0] * e2[:, 1] - e1[:, 1] * e2[:, 0]], axis=1).astype(np.float64)
-    return int((np.sqrt((n * n).sum(1)) >= (1.0 - 1e-5) * float(np.float32(1e-3))).sum())
+    return int((np.sqrt((n * n).sum(1)) >= (1.0 - 1e-5) * float(np.float32(1e-3)) / dmax).sum())
 
 
 @pytest.mark.parametrize("name,W,H,fixture", [("car_boxed", 160, 90, "car_boxed_160x90_strict"),
@@ -121,4 +121,36 @@ def test_unit_direction_view_renders_the_reference_fixture(name, W, H, fixture):
         assert info["unit_nodes"] > 0 and info["unit_depth"] <= 16
         np.testing.assert_array_equal(out["hit"], ref["hit"])
         assert same_bits(out["t"], ref["t"]) and same_bits(out["rgb"], ref["rgb"]), kernel
+
+
+@pytest.mark.parametrize("name", ["sportscar", "car_boxed"])
+def test_primary_view_and_long_primary_directions(name):
+    """the primary view (primary rays of a launch whose directions are all <= 3 long walk a wide BVH without the
+    triangles no such direction can hit): built over exactly the triangles the criterion keeps; a camera whose
+    directions are longer (the reference camera with ul - pos and the pixel steps doubled: |d| up to 5.5) walks
+    the full view and still equals the strict kernel (the reference's walk) bit for bit"""
+    import torch
+    from prt import device
+    s = host.Scene.named(name).build_bvh(3)
+    W, H = 96, 54
+    r = device.Renderer(0, counters=True)
+    r.upload(s)
+    info = r.scene_info()
+    assert info["primary_triangles"] == unit_hittable_count(s, 3.0) < s.n_triangles, info
+    c = host.camera(W, H)
+    for a, b in ((c.ul, c.pos),):
+        a.x, a.y, a.z = b.x + 2 * (a.x - b.x), b.y + 2 * (a.y - b.y), b.z + 2 * (a.z - b.z)
+    for v in (c.inc_x, c.inc_y):
+        v.x, v.y, v.z = 2 * v.x, 2 * v.y, 2 * v.z
+    outs = {}
+    for kernel in ("strict", "fast", "persist4"):
+        hit = torch.empty((H, W), dtype=torch.int32, device="cuda")
+        rgb = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        r.render(c, W, H, kernel=kernel, rgb=rgb, hit=hit)
+        r.sync()
+        outs[kernel] = (hit.cpu().numpy(), rgb.cpu().numpy(), r.stats()["rays"])
+    r.close()
+    for kernel in ("fast", "persist4"):
+        np.testing.assert_array_equal(outs[kernel][0], outs["strict"][0])
+        assert same_bits(outs[kernel][1], outs["strict"][1]) and outs[kernel][2] == outs["strict"][2], kernel
 
