@@ -1,11 +1,11 @@
 #!/bin/bash
-# BASELINE.json's configurations on one GPU: one bench line each (16-frame batches, no CPU baseline),
+# BASELINE.json's configurations on one GPU: one bench line each (the driver's 20 steps: one 20-frame launch; no CPU baseline),
 # with the autotuner's decision logged (PRT_TUNE_LOG). Output: gpurun_out/cfg_<name>.log
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 run() {  # name args...
     local n=$1; shift
-    PRT_TUNE_LOG=1 timeout -k 10 300 python bench.py --no-cpu-baseline --frames 16 "$@" > gpurun_out/cfg_$n.log 2>&1
+    PRT_TUNE_LOG=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 20 --warmup 5 "$@" > gpurun_out/cfg_$n.log 2>&1
     local rc=$?
     echo "$n rc=$rc"
     [ $rc -eq 0 ] || exit $rc
