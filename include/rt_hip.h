@@ -111,10 +111,22 @@ enum {
                                 through k_coop (2 or 4 lanes per ray) on a second stream while k_persist renders the rest.
                                 The first frame of a shape / camera measures (k_persist with per-tile times), the next
                                 ones try hot thresholds and k_persist itself, and the fastest renders from then on
-                                (rt_frame.hot_pct > 0: that threshold, 4 lanes per ray, no trials) */
-    RT_VARIANT_POOL = 10     /* k_pool: 16x16-pixel tile per workgroup, each bounce level's closest-hit and shadow rays
+                                (rt_frame.hot_pct > 0: that threshold and rt_frame.hot_kernel, no trials) */
+    RT_VARIANT_POOL = 10,    /* k_pool: 16x16-pixel tile per workgroup, each bounce level's closest-hit and shadow rays
                                 compacted into tile-local LDS queues and traced with dynamic fetch (rt_frame.regroup =
                                 idle lanes per refill), 4 waves per SIMD */
+    RT_VARIANT_RELAY = 12    /* k_relay (single 1-spp frames, 1..7 lights): one workgroup of 1 + lights waves per 8x8 tile,
+                                wave 0 walks the closest-hit chains and wave j level i's shadow rays toward light j - 1 while
+                                wave 0 walks level i + 1 (LDS hand-off); the hybrid launch's relay candidates use it for
+                                the costliest tiles only */
+};
+
+/* rt_frame.hot_kernel: the kernel RT_VARIANT_HYBRID sends the hot tiles to when rt_frame.hot_pct > 0 */
+enum {
+    RT_HOT_COOP4 = 0, /* k_coop, 4 lanes per ray */
+    RT_HOT_COOP2 = 1, /* k_coop, 2 lanes per ray */
+    RT_HOT_FAN = 2,   /* k_fan, 1 + lights lanes per pixel */
+    RT_HOT_RELAY = 3  /* k_relay, 1 + lights waves per 8x8 tile */
 };
 
 /* rt_frame.dealing: order in which persistent waves take their tiles (k_persist 8x8, k_pool 16x16) */
@@ -152,7 +164,8 @@ typedef struct rt_frame {
     int dealing;   /* RT_DEAL_* */
     int regroup;   /* k_pool: idle lanes of a wave that trigger a refill from the tile's queue; 0 = 16 */
     int hot_pct;   /* RT_VARIANT_HYBRID: tiles whose measured time exceeds hot_pct % of the costliest tile's go to the
-                      cooperative kernel; 0 = try several thresholds and keep the fastest */
+                      kernel hot_kernel names; 0 = try several thresholds and hot kernels and keep the fastest */
+    int hot_kernel; /* RT_HOT_* (with hot_pct > 0) */
 } rt_frame;
 
 /* Device output pointers (all nullable). rgb: [n_rows][width][3] f32 in [0,1] = vec_t pixels

@@ -22,6 +22,7 @@
 #include "rt_kernels.hpp"
 #include "rt_coop.hpp"
 #include "rt_fan.hpp"
+#include "rt_relay.hpp"
 #include "rt_output.hpp"
 #include "rt_split.hpp"
 #include "rt_pool.hpp"
@@ -145,14 +146,15 @@ struct rt_ctx {
     // and the tile lists they give (the coop tiles of the costliest 8x8 tiles; the rest for k_persist)
     struct Hybrid {
         long long scene = -1;
-        int W = 0, rows = 0, off = 0, stride = 0, block = 0, bounces = 0, spp = 0, dealing = 0, pct_req = 0;
+        int W = 0, rows = 0, off = 0, stride = 0, block = 0, bounces = 0, spp = 0, dealing = 0, pct_req = 0, hk_req = 0;
         float cam[12] = {};
         int state = 0;  // 0: measure next; 1: a measuring frame's tile times are on their way to h_tr; 2: lists ready
         // candidates: hot threshold (0 = k_persist), their lists at d_lists + at[c], trial launch, time, choice
-        static constexpr int NCAND = 8;
+        static constexpr int NCAND = 12;
         int nc = 0, choice = -1;
         int pct[NCAND] = {}, lanes[NCAND] = {}, n_hot[NCAND] = {}, n_cold[NCAND] = {};
-        bool fan[NCAND] = {};  // the hot tiles through k_fan<lanes> instead of k_coop<lanes>
+        bool fan[NCAND] = {};    // the hot tiles through k_fan<lanes> instead of k_coop<lanes>
+        bool relay[NCAND] = {};  // the hot tiles through k_relay (8x8 tiles, 1 + lights waves each)
         size_t at[NCAND] = {};
         static constexpr int ROUNDS = 2;  // trials per candidate (the minimum counts: single frames are noisy)
         long long launch[NCAND][ROUNDS] = {};
@@ -172,15 +174,16 @@ namespace {
 
 // RT_VARIANT_HYBRID candidates: tiles slower than pct % of the slowest tile of the measuring frame go to k_coop
 // with `lanes` lanes per ray (each candidate is tried once against k_persist; hybrid_pick)
-// (lanes: k_coop's lanes per ray; 0: k_fan, 1 + lights lanes per pixel)
+// (lanes: k_coop's lanes per ray; 0: k_fan, 1 + lights lanes per pixel; -1: k_relay, 1 + lights waves per tile)
 struct HotCand {
     int pct, lanes;
 };
-constexpr HotCand HYBRID_CANDS[7] = {{45, 4}, {60, 4}, {75, 4}, {60, 2}, {75, 2}, {60, 0}, {75, 0}};
-// pixel tile of the hot kernel (rtd::GTile): k_coop<2> 8x4, k_coop<4> / k_fan<4> 4x4, k_fan<2> 8x4, k_fan<8> 4x2
-inline void hot_tile(int g, int& tw, int& th) {
-    tw = g == 2 ? 8 : 4;
-    th = g == 8 ? 2 : 4;
+constexpr HotCand HYBRID_CANDS[10] = {{45, 4}, {60, 4}, {75, 4}, {60, 2}, {75, 2}, {60, 0}, {75, 0}, {30, -1}, {50, -1}, {70, -1}};
+// pixel tile of the hot kernel (rtd::GTile): k_coop<2> 8x4, k_coop<4> / k_fan<4> 4x4, k_fan<2> 8x4, k_fan<8> 4x2;
+// k_relay (relay) 8x8
+inline void hot_tile(int g, bool relay, int& tw, int& th) {
+    tw = relay ? 8 : g == 2 ? 8 : 4;
+    th = relay ? 8 : g == 8 ? 2 : 4;
 }
 
 int fail(rt_ctx* c, hipError_t e, const char* what) {
@@ -858,10 +861,10 @@ namespace {
 
 // resident workgroups per CU of a persistent kernel (occupancy API, capped at 8)
 template <class K>
-int resident(K kernel, int device, int cap = 8, size_t dyn_lds = 0) {
+int resident(K kernel, int device, int cap = 8, size_t dyn_lds = 0, int block = rtd::BLOCK) {
     if (cap <= 0) cap = 8;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, rtd::BLOCK, dyn_lds) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, dyn_lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -973,6 +976,32 @@ int launch_coop(const rtd::KArgs& A, int G, bool count, int device, hipStream_t 
     return RT_OK;
 }
 
+// k_relay (rt_relay.hpp): one workgroup of 1 + lights waves per 8x8 tile (A.tile_order / A.n_tiles), at most
+// `max_blocks` workgroups (0: every resident one) and never more than 4 per CU (the gstack slots of the strict
+// re-walks: 2 per workgroup, 8 per CU allocated)
+template <int MAXB>
+auto relay_kernel(bool count) {
+    return count ? rtd::k_relay<MAXB, true> : rtd::k_relay<MAXB, false>;
+}
+template <int MAXB>
+int relay_resident(const rtd::KArgs& A, bool count, int device) {
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    const int threads = 64 * (1 + A.s.n_lights);
+    return std::min(resident(relay_kernel<MAXB>(count), device, 4, rtd::relay_lds_bytes(MAXB, A.s.n_lights, A.wcap), threads),
+                    4 * cus);
+}
+template <int MAXB>
+int launch_relay(const rtd::KArgs& A, bool count, int device, hipStream_t s, int max_blocks) {
+    const int threads = 64 * (1 + A.s.n_lights);
+    int blocks = std::min(relay_resident<MAXB>(A, count, device), A.n_tiles);
+    if (max_blocks > 0) blocks = std::min(blocks, max_blocks);
+    auto k = relay_kernel<MAXB>(count);
+    if (A.tile_trace) k = count ? rtd::k_relay<MAXB, true, true> : rtd::k_relay<MAXB, false, true>;  // diagnostics
+    k<<<std::max(1, blocks), threads, rtd::relay_lds_bytes(MAXB, A.s.n_lights, A.wcap), s>>>(A);
+    return RT_OK;
+}
+
 template <int MAXB>
 int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count, int cap_a);  // below
 }  // namespace
@@ -1042,8 +1071,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     while (g * g < f->spp) g++;
     if (f->spp < 1 || g * g != f->spp || g > 16) return arg_err(ctx, "rt_render: spp must be a square 1..256");
     if (f->kernel < RT_KERNEL_AUTO || f->kernel > RT_KERNEL_FAST) return arg_err(ctx, "rt_render: bad kernel");
-    if (f->variant < RT_VARIANT_DEFAULT || f->variant > RT_VARIANT_HYBRID || f->variant == 8 || f->variant == 9 ||
-        f->hot_pct < 0 || f->hot_pct > 100 ||
+    if (f->variant < RT_VARIANT_DEFAULT || f->variant > RT_VARIANT_RELAY || f->variant == 8 || f->variant == 9 ||
+        f->hot_pct < 0 || f->hot_pct > 100 || f->hot_kernel < RT_HOT_COOP4 || f->hot_kernel > RT_HOT_RELAY ||
         f->tune < 0 || f->tune > 1 ||
         f->waves_cap < 0 || f->waves_cap > 8 || f->dealing < RT_DEAL_DEFAULT || f->dealing > RT_DEAL_ROW_MAJOR ||
         f->regroup < 0 || f->regroup > 64)
@@ -1252,7 +1281,13 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     const bool wide_ok = kernel == RT_KERNEL_FAST && ctx->wide_n > 0;
     const bool fan_ok = wide_ok && ctx->n_lights >= 1 && ctx->n_lights <= 7;
     const int fan_r = ctx->n_lights <= 1 ? 2 : ctx->n_lights <= 3 ? 4 : 8;  // lanes per pixel: 1 + lights
+    // k_relay: single 1-spp frames of 1..7 lights (1 + lights waves per workgroup), dynamic-LDS wide stacks
+    const bool relay_ok = wide_ok && ctx->n_lights >= 1 && ctx->n_lights <= rtd::RELAY_MAXL && f->spp == 1 &&
+                          n_frames == 1 && fs == 0 && A.gstack && A.wcap > 0 && !A.tile_trace;
     auto usable = [&](int v) {
+        if (v == RT_VARIANT_RELAY) return relay_ok || (A.tile_trace && wide_ok && ctx->n_lights >= 1 &&
+                                                       ctx->n_lights <= rtd::RELAY_MAXL && f->spp == 1 && fs == 0 &&
+                                                       A.gstack && A.wcap > 0);  // (diagnostics: its tile trace)
         if (v == RT_VARIANT_SPLIT) return split_ok;
         if (v == RT_VARIANT_FAN) return fan_ok;
         if (v >= RT_VARIANT_COOP2 && v <= RT_VARIANT_COOP8) return wide_ok;
@@ -1358,7 +1393,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                               cam->inc_x.x, cam->inc_x.y, cam->inc_x.z, cam->inc_y.x, cam->inc_y.y, cam->inc_y.z};
         const bool same = h.scene == ctx->scene_gen && h.W == f->width && h.rows == f->n_rows && h.off == f->row_offset &&
                           h.stride == f->row_stride && h.block == rb && h.bounces == f->bounces && h.spp == f->spp &&
-                          h.dealing == f->dealing && h.pct_req == f->hot_pct && std::memcmp(h.cam, cv, sizeof cv) == 0;
+                          h.dealing == f->dealing && h.pct_req == f->hot_pct && h.hk_req == f->hot_kernel &&
+                          std::memcmp(h.cam, cv, sizeof cv) == 0;
         auto err = [&](hipError_t e, const char* what) { rc = fail(ctx, e, what); return -1; };
         if (!h.ev) {
             hipError_t e = hipEventCreateWithFlags(&h.ev, hipEventDisableTiming);
@@ -1382,6 +1418,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             h.spp = f->spp;
             h.dealing = f->dealing;
             h.pct_req = f->hot_pct;
+            h.hk_req = f->hot_kernel;
             std::memcpy(h.cam, cv, sizeof cv);
             h.n_tiles = (size_t)A.n_tiles;
             if (h.tr_cap < h.n_tiles) {
@@ -1419,18 +1456,24 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             h.cold_regions = xcd_mode >= 1 && xcd_mode <= 3 && dealt_centre_out;
             h.nc = 0;
             if (f->hot_pct > 0) {
+                const int hk = (f->hot_kernel == RT_HOT_FAN && !fan_ok) || (f->hot_kernel == RT_HOT_RELAY && !relay_ok)
+                                   ? RT_HOT_COOP4
+                                   : f->hot_kernel;
                 h.pct[0] = f->hot_pct;
-                h.lanes[0] = 4;
-                h.fan[0] = false;
+                h.lanes[0] = hk == RT_HOT_COOP2 ? 2 : hk == RT_HOT_FAN ? fan_r : hk == RT_HOT_RELAY ? 1 : 4;
+                h.fan[0] = hk == RT_HOT_FAN;
+                h.relay[0] = hk == RT_HOT_RELAY;
                 h.nc = 1;
             } else {
                 h.pct[0] = 0;  // k_persist
+                h.fan[0] = h.relay[0] = false;
                 h.nc = 1;
                 for (const HotCand& hc : HYBRID_CANDS) {
-                    if (hc.lanes == 0 && !fan_ok) continue;
+                    if ((hc.lanes == 0 && !fan_ok) || (hc.lanes < 0 && !relay_ok)) continue;
                     h.pct[h.nc] = hc.pct;
                     h.fan[h.nc] = hc.lanes == 0;
-                    h.lanes[h.nc++] = hc.lanes == 0 ? fan_r : hc.lanes;
+                    h.relay[h.nc] = hc.lanes < 0;
+                    h.lanes[h.nc++] = hc.lanes == 0 ? fan_r : hc.lanes < 0 ? 1 : hc.lanes;
                 }
             }
             std::vector<int> lists;
@@ -1443,10 +1486,11 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                     if (dur[t] * 100 > (long long)h.pct[c] * cmax) hot8.push_back((int)t);
                 std::stable_sort(hot8.begin(), hot8.end(), [&](int a, int b) { return dur[a] > dur[b]; });
                 if (hot8.size() > h.n_tiles / 2) hot8.resize(h.n_tiles / 2);  // k_coop costs ~2x the wave time
+                if (h.relay[c] && hot8.size() > 1024) hot8.resize(1024);  // k_relay: at most one round of workgroups
                 std::vector<char> is_hot(h.n_tiles, 0);
                 // each 8x8 tile = (8 / TW) x (8 / TH) tiles of the hot kernel (rtd::GTile), hottest first
                 int tw, th;
-                hot_tile(h.lanes[c], tw, th);
+                hot_tile(h.lanes[c], h.relay[c], tw, th);
                 const int ctw = (f->width + tw - 1) / tw, cth = (f->n_rows + th - 1) / th;
                 for (int t : hot8) {
                     is_hot[t] = 1;
@@ -1514,7 +1558,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             std::fprintf(stderr, "[prt hybrid] %dx%d b%d:", f->width, f->n_rows, f->bounces);
             for (int c = 0; c < h.nc; c++)
                 std::fprintf(stderr, " %s%d/%s%d %.3f ms", h.pct[c] ? "hot>" : "persist", h.pct[c],
-                             h.fan[c] ? "fan" : "coop", h.lanes[c], h.ms[c]);
+                             h.relay[c] ? "relay" : h.fan[c] ? "fan" : "coop", h.lanes[c], h.ms[c]);
             std::fprintf(stderr, " -> %d\n", best);
         }
         return h.pct[best] == 0 ? -1 : best;
@@ -1553,6 +1597,10 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                                        : launch_fan<8>(B, gr, count, ctx->device, ctx->stream, cp);
             return f->bounces <= 4 ? launch_coop<4>(B, gr, count, ctx->device, ctx->stream, cp)
                                    : launch_coop<8>(B, gr, count, ctx->device, ctx->stream, cp);
+        }
+        if (md == RT_VARIANT_RELAY) {  // k_relay (rt_relay.hpp): every 8x8 tile, centre-out
+            return f->bounces <= 4 ? launch_relay<4>(A, count, ctx->device, ctx->stream, 0)
+                                   : launch_relay<8>(A, count, ctx->device, ctx->stream, 0);
         }
         if (md == RT_VARIANT_POOL) {  // k_pool (rt_pool.hpp): 16 x 16 pixel tiles per workgroup
             rtd::KArgs B = A;
@@ -1775,7 +1823,7 @@ int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c) {
         if (g == 8) kc = count ? rtd::k_fan<MAXB, true, 8> : rtd::k_fan<MAXB, false, 8>;
     }
     int tw, th;
-    hot_tile(g, tw, th);
+    hot_tile(g, h.relay[c], tw, th);
     rtd::KArgs B = A;  // the hot kernel's tiles, dealt hottest first from their own work counter
     B.tiles_x = (A.W + tw - 1) / tw;
     B.n_tiles = n_hot;
@@ -1786,12 +1834,17 @@ int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c) {
     P.n_tiles = n_cold;
     P.region_off = h.cold_regions ? lists + n_hot : nullptr;
     P.tile_order = lists + n_hot + (h.cold_regions ? 9 : 0);
-    const int rp = resident(kp, ctx->device), rcp = resident(kc, ctx->device);
-    const int nc = std::max(1, std::min((n_hot + 3) / 4, rcp / 2));
+    const int rp = resident(kp, ctx->device);
+    const int rcp = h.relay[c] ? relay_resident<MAXB>(B, count, ctx->device) : resident(kc, ctx->device);
+    // the hot grid starts every hot tile at once (k_relay: one workgroup per tile), at most half the chip
+    const int nc = std::max(1, std::min(h.relay[c] ? n_hot : (n_hot + 3) / 4, rcp / 2));
     const int np = std::max(1, std::min(rp - (int)((long long)nc * rp / rcp), (n_cold + 3) / 4));
     HIPC(hipEventRecord(h.fork, ctx->stream));  // after the work / counter resets
     HIPC(hipStreamWaitEvent(h.s2, h.fork, 0));
-    if (n_hot > 0) kc<<<nc, rtd::BLOCK, 0, h.s2>>>(B);
+    if (n_hot > 0) {
+        if (h.relay[c]) launch_relay<MAXB>(B, count, ctx->device, h.s2, nc);
+        else kc<<<nc, rtd::BLOCK, 0, h.s2>>>(B);
+    }
     HIPC(hipGetLastError());
     if (n_cold > 0) kp<<<np, rtd::BLOCK, 0, ctx->stream>>>(P);
     HIPC(hipGetLastError());

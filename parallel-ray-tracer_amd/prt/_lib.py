@@ -60,7 +60,7 @@ class Frame(ctypes.Structure):
                 ("spp", ctypes.c_int), ("kernel", ctypes.c_int), ("row_block", ctypes.c_int),
                 ("frame_shift", ctypes.c_int), ("variant", ctypes.c_int), ("tune", ctypes.c_int),
                 ("waves_cap", ctypes.c_int), ("dealing", ctypes.c_int), ("regroup", ctypes.c_int),
-                ("hot_pct", ctypes.c_int)]
+                ("hot_pct", ctypes.c_int), ("hot_kernel", ctypes.c_int)]
 
 
 STAT_FIELDS = ["primary", "reflection", "shadow", "shadow_skipped", "hits", "ch_inner", "ch_leaf",

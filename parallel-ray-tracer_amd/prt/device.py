@@ -16,7 +16,8 @@ KERNELS = {"auto": 0, "strict": 1, "fast": 2}
 # rt_frame.variant (launch configurations of the fast kernel, include/rt_hip.h); a variant name is also
 # accepted as `kernel` (kernel="coop4" == kernel="fast", variant="coop4")
 VARIANTS = {"default": 0, "persist": 1, "persist4": 2, "split": 3, "coop2": 4, "coop4": 5, "coop8": 6, "fan": 7,
-            "pool": 10, "hybrid": 11}
+            "pool": 10, "hybrid": 11, "relay": 12}
+HOT_KERNELS = {"coop4": 0, "coop2": 1, "fan": 2, "relay": 3}  # rt_frame.hot_kernel (RT_HOT_*)
 DEALING = {"default": 0, "global": 1, "rows": 2, "columns": 3, "blocks": 4, "row_major": 5}
 ACCEL = {"auto": 0, "reference": 1, "gpu": 2, "host": 3}
 ACCEL_NAMES = {v: k for k, v in ACCEL.items()}
@@ -202,13 +203,15 @@ class Renderer:
         self.scene = scene
         return self
 
-    def _frame(self, width, height, rows, bounces, spp, kernel, variant, tune, waves_cap, dealing, regroup, hot_pct=0):
+    def _frame(self, width, height, rows, bounces, spp, kernel, variant, tune, waves_cap, dealing, regroup, hot_pct=0,
+               hot_kernel="coop4"):
         ro, rs, nr, rb, sh = _rows(rows, height)
         if isinstance(kernel, str) and kernel in VARIANTS:
             kernel, variant = "fast", kernel
         v = VARIANTS.get(variant, variant) if variant is not None else 0
         return Frame(width, height, ro, rs, nr, bounces, spp, KERNELS.get(kernel, kernel), rb, sh, v,
-                     1 if tune else 0, waves_cap, DEALING.get(dealing, dealing), regroup, hot_pct), nr
+                     1 if tune else 0, waves_cap, DEALING.get(dealing, dealing), regroup, hot_pct,
+                     HOT_KERNELS.get(hot_kernel, hot_kernel)), nr
 
     def _outputs(self, nf, nr, width, bounces, rgb, hit, t, bounce_hit, bgra):
         import torch
@@ -221,15 +224,15 @@ class Renderer:
 
     def render(self, cam, width, height, rows=None, bounces=4, spp=1, kernel="auto", rgb=None, hit=None, t=None,
                bounce_hit=None, bgra=None, variant=None, tune=False, waves_cap=0, dealing="default", regroup=0,
-               hot_pct=0):
+               hot_pct=0, hot_kernel="coop4"):
         """render_frame(): asynchronous. rows = (offset, stride, n[, block[, frame_shift]]) (rt_frame; prt.dist)
         or None for the full frame.
         rgb / hit / t / bounce_hit ([n, W, bounces] int32) / bgra ([n, W] int32: the BMP-quantised pixel in
         top-down rows, rt_outputs.bgra): optional device tensors (torch: checked for size, dtype, device and
-        contiguity) or raw pointers. variant / tune / waves_cap / dealing / regroup / hot_pct: the fast kernel's
-        launch configuration (rt_frame; VARIANTS, DEALING)."""
+        contiguity) or raw pointers. variant / tune / waves_cap / dealing / regroup / hot_pct / hot_kernel: the fast
+        kernel's launch configuration (rt_frame; VARIANTS, DEALING, HOT_KERNELS)."""
         f, nr = self._frame(width, height, rows, bounces, spp, kernel, variant, tune, waves_cap, dealing, regroup,
-                            hot_pct)
+                            hot_pct, hot_kernel)
         out = self._outputs(1, nr, width, bounces, rgb, hit, t, bounce_hit, bgra)
         self._chk(_L.rt_render(self._ctx, ctypes.byref(cam), ctypes.byref(f), ctypes.byref(out)), "rt_render")
         self._last = (width, nr)

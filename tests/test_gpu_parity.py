@@ -692,7 +692,7 @@ def test_hybrid_frames_equal_persistent_frames(dev, name):
             r.upload(s)
             # frame 0 measures, frame 1 is issued while the measurement is in flight (the default launch, most
             # likely), frames 2.. (each after a sync) try the candidate thresholds and k_persist, then the choice
-            for group in ((0, 1),) + tuple((i,) for i in range(2, 19)):
+            for group in ((0, 1),) + tuple((i,) for i in range(2, 27)):
                 outs = []
                 for frame in group:
                     hit = torch.full((nr, W), -7, dtype=torch.int32, device="cuda")

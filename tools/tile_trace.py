@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--counters", action="store_true", help="COUNT kernel: per-tile wave steps and node visits")
     ap.add_argument("--world", type=int, default=1, help="render rank --rank's cyclic rows of a --world split")
     ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--variant", default="auto", help="persist (default rule under a trace) or relay (k_relay's trace: "
+                    "per tile the path wave's steps and the light waves' steps in place of node visits)")
     a = ap.parse_args()
     import torch
     from prt import device, host
@@ -32,12 +34,12 @@ def main():
     rows = cyclic_rows(a.H, a.rank, a.world)
     rgb = torch.empty((rows[2], a.W, 3), dtype=torch.float32, device="cuda")
     for _ in range(5):
-        r.render(cam, a.W, a.H, rows=rows, rgb=rgb)
+        r.render(cam, a.W, a.H, rows=rows, rgb=rgb, kernel=a.variant)
     r.sync()
     a.out = a.out or os.path.join(ROOT, "gpurun_out", f"tile_trace_{a.scene}.bin")
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     os.environ["PRT_TILE_TRACE"] = a.out
-    r.render(cam, a.W, a.H, rows=rows, rgb=rgb)
+    r.render(cam, a.W, a.H, rows=rows, rgb=rgb, kernel=a.variant)
     r.sync()
     del os.environ["PRT_TILE_TRACE"]
     ms = r.kernel_times(1)[0]
