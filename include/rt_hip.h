@@ -115,10 +115,13 @@ enum {
     RT_VARIANT_POOL = 10,    /* k_pool: 16x16-pixel tile per workgroup, each bounce level's closest-hit and shadow rays
                                 compacted into tile-local LDS queues and traced with dynamic fetch (rt_frame.regroup =
                                 idle lanes per refill), 4 waves per SIMD */
-    RT_VARIANT_RELAY = 12    /* k_relay (single 1-spp frames, 1..7 lights): one workgroup of 1 + lights waves per 8x8 tile,
+    RT_VARIANT_RELAY = 12,   /* k_relay (single 1-spp frames, 1..7 lights): one workgroup of 1 + lights waves per 8x8 tile,
                                 wave 0 walks the closest-hit chains and wave j level i's shadow rays toward light j - 1 while
                                 wave 0 walks level i + 1 (LDS hand-off); the hybrid launch's relay candidates use it for
                                 the costliest tiles only */
+    RT_VARIANT_SHPOOL = 13   /* k_persist at 4 waves per SIMD with each bounce level's shadow rays (every pixel's, every
+                                light's) walked as ONE per-wave pool: a lane whose walk ends takes the next unassigned ray,
+                                lanes of ended paths included (rt_frame.regroup = idle lanes per refill; 1..32 lights) */
 };
 
 /* rt_frame.hot_kernel: the kernel RT_VARIANT_HYBRID sends the hot tiles to when rt_frame.hot_pct > 0 */

@@ -164,7 +164,7 @@ __device__ __forceinline__ void closest_wide_g(const DWide& W, v3 o, v3 d, float
             c.ws += first_active_lane();
         }
         const int next = wide_next(nh, cb, imask, oct, sp, stk);
-        if (next >= 0) N = wload(W, next);
+        N = wload(W, next >= 0 ? next : 0);  // unconditional (rt_kernels.hpp closest_wide)
         if (th) {  // uniform in the group
             float lb = best;
             int lhp = hp, lnd = nd;
@@ -222,7 +222,7 @@ __device__ __forceinline__ bool visible_wide_g(const DWide& W, v3 o, v3 d, float
             c.ws += first_active_lane();
         }
         const int next = wide_next(nh, cb, imask, oct, sp, stk);
-        if (next >= 0) N = wload(W, next);
+        N = wload(W, next >= 0 ? next : 0);  // unconditional (rt_kernels.hpp closest_wide)
         if (th) {
             float lb = best;
             unsigned occ = 0;

@@ -54,7 +54,7 @@ __device__ __forceinline__ void walk_unified(const DWide& W, v3 o, v3 d, bool sh
             c.ws += first_active_lane();
         }
         const int next = wide_next(nh, cb, imask, oct, sp, stk);
-        if (next >= 0) N = wload(W, next);
+        N = wload(W, next >= 0 ? next : 0);  // unconditional (rt_kernels.hpp closest_wide)
         while (th) {
             const int i = tb + __builtin_ctz(th);
             th &= th - 1u;

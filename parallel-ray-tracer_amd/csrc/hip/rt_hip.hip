@@ -20,6 +20,7 @@
 #include "rt_hip.h"
 #include "rt_host.h"
 #include "rt_kernels.hpp"
+#include "rt_shpool.hpp"
 #include "rt_coop.hpp"
 #include "rt_fan.hpp"
 #include "rt_relay.hpp"
@@ -877,6 +878,35 @@ int resident(K kernel, int device, int cap = 8, size_t dyn_lds = 0, int block = 
 //                        the wide stack sized to the scene's wide depth when 4 workgroups of that fit a CU (LDS
 //                        measured 1.2 % faster than the global slab on dragon, 2.3 % on car_boxed), else global;
 // `cap`: workgroups per CU at most (0: the occupancy limit); the grid never exceeds the tiles / 4.
+// the 4-wave k_persist instantiation of a launch: path buffer in LDS (pbl) or global memory, frame batch, spp = 1
+// build, counters; SHP: the per-wave shadow pool (rt_shpool.hpp)
+template <int MAXB, bool SHP>
+void (*persist4(bool pbl, bool batch, bool spp1, bool count))(rtd::KArgs) {
+    using rtd::k_persist;
+    if (pbl) {
+        if (batch && spp1) return count ? k_persist<MAXB, false, true, true, 4, false, true, 2, true, true, SHP>
+                                        : k_persist<MAXB, false, false, true, 4, false, true, 2, true, true, SHP>;
+        if (batch) return count ? k_persist<MAXB, false, true, true, 4, false, true, 2, true, false, SHP>
+                                : k_persist<MAXB, false, false, true, 4, false, true, 2, true, false, SHP>;
+        return count ? k_persist<MAXB, false, true, true, 4, false, false, 2, true, false, SHP>
+                     : k_persist<MAXB, false, false, true, 4, false, false, 2, true, false, SHP>;
+    }
+    // (deep trees: the LDS holds no path buffer next to the stack)
+    if (batch && spp1) return count ? k_persist<MAXB, false, true, true, 4, false, true, 1, false, true, SHP>
+                                    : k_persist<MAXB, false, false, true, 4, false, true, 1, false, true, SHP>;
+    if (batch) return count ? k_persist<MAXB, false, true, true, 4, false, true, 1, false, false, SHP>
+                            : k_persist<MAXB, false, false, true, 4, false, true, 1, false, false, SHP>;
+    return count ? k_persist<MAXB, false, true, true, 4, false, false, 1, false, false, SHP>
+                 : k_persist<MAXB, false, false, true, 4, false, false, 1, false, false, SHP>;
+}
+
+// k_persist (the persistent one-lane-per-path kernel) in configuration `variant`:
+//   RT_VARIANT_PERSIST   k_persist, <= 168 VGPRs (3 waves per SIMD), path levels in registers;
+//   RT_VARIANT_PERSIST4  k_persist, <= 128 VGPRs (4 waves per SIMD), path levels in a path buffer: in LDS after
+//                        the wide stack sized to the scene's wide depth when 4 workgroups of that fit a CU (LDS
+//                        measured 1.2 % faster than the global slab on dragon, 2.3 % on car_boxed), else global;
+//   RT_VARIANT_SHPOOL    PERSIST4 with each bounce level's shadow rays walked as a per-wave pool (rt_shpool.hpp);
+// `cap`: workgroups per CU at most (0: the occupancy limit); the grid never exceeds the tiles / 4.
 template <int MAXB>
 void launch_paths(const rtd::KArgs& A, int variant, bool count, int device, hipStream_t s, int cap) {
     const bool batch = A.n_frames > 1;
@@ -891,32 +921,18 @@ void launch_paths(const rtd::KArgs& A, int variant, bool count, int device, hipS
     auto k = count ? rtd::k_persist<MAXB, false, true> : rtd::k_persist<MAXB, false, false>;
     if (batch) k = count ? rtd::k_persist<MAXB, false, true, true, 3, false, true> : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
     size_t dyn = 0;
-    if (variant == RT_VARIANT_PERSIST4) {
+    if (variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL) {
+        const bool shp = variant == RT_VARIANT_SHPOOL;
         bool pbl = A.gstack && A.wcap > 0;
         if (pbl) {
             int per_cu = 0;
-            auto kp = rtd::k_persist<MAXB, false, false, true, 4, false, true, 2, true>;
+            auto kp = shp ? persist4<MAXB, true>(true, true, true, false) : persist4<MAXB, false>(true, true, true, false);
             pbl = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, rtd::BLOCK, lds_wide + lds_pb) == hipSuccess &&
                   per_cu >= 4;
         }
-        if (pbl) {
-            dyn = lds_wide + lds_pb;
-            k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, false, 2, true>
-                      : rtd::k_persist<MAXB, false, false, true, 4, false, false, 2, true>;
-            if (batch) k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, 2, true>
-                                 : rtd::k_persist<MAXB, false, false, true, 4, false, true, 2, true>;
-            if (batch && A.spp <= 1)  // the bench's kernel: spp = 1 build
-                k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, 2, true, true>
-                          : rtd::k_persist<MAXB, false, false, true, 4, false, true, 2, true, true>;
-        } else {
-            k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, false, true>
-                      : rtd::k_persist<MAXB, false, false, true, 4, false, false, true>;
-            if (batch) k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, true>
-                                 : rtd::k_persist<MAXB, false, false, true, 4, false, true, true>;
-            if (batch && A.spp <= 1)  // spp = 1 build (deep trees: the LDS holds no path buffer next to the stack)
-                k = count ? rtd::k_persist<MAXB, false, true, true, 4, false, true, 1, false, true>
-                          : rtd::k_persist<MAXB, false, false, true, 4, false, true, 1, false, true>;
-        }
+        if (pbl) dyn = lds_wide + lds_pb;
+        // (the 4-wave kernels without the LDS path buffer: a global slab; the bench's batches: the spp = 1 build)
+        k = shp ? persist4<MAXB, true>(pbl, batch, A.spp <= 1, count) : persist4<MAXB, false>(pbl, batch, A.spp <= 1, count);
     }
     const int blocks = std::max(1, std::min(resident(k, device, cu_cap, dyn), (A.n_tiles + 3) / 4));
     k<<<blocks, rtd::BLOCK, dyn, s>>>(A);
@@ -1071,7 +1087,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     while (g * g < f->spp) g++;
     if (f->spp < 1 || g * g != f->spp || g > 16) return arg_err(ctx, "rt_render: spp must be a square 1..256");
     if (f->kernel < RT_KERNEL_AUTO || f->kernel > RT_KERNEL_FAST) return arg_err(ctx, "rt_render: bad kernel");
-    if (f->variant < RT_VARIANT_DEFAULT || f->variant > RT_VARIANT_RELAY || f->variant == 8 || f->variant == 9 ||
+    if (f->variant < RT_VARIANT_DEFAULT || f->variant > RT_VARIANT_SHPOOL || f->variant == 8 || f->variant == 9 ||
         f->hot_pct < 0 || f->hot_pct > 100 || f->hot_kernel < RT_HOT_COOP4 || f->hot_kernel > RT_HOT_RELAY ||
         f->tune < 0 || f->tune > 1 ||
         f->waves_cap < 0 || f->waves_cap > 8 || f->dealing < RT_DEAL_DEFAULT || f->dealing > RT_DEAL_ROW_MAJOR ||
@@ -1293,6 +1309,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         if (v >= RT_VARIANT_COOP2 && v <= RT_VARIANT_COOP8) return wide_ok;
         if (v == 8 || v == 9) return false;  // (k_chain, removed in round 2)
         if (v == RT_VARIANT_POOL) return wide_ok && !A.tile_trace && A.wcap > 0;
+        if (v == RT_VARIANT_SHPOOL) return wide_ok && ctx->n_lights <= 32;  // (a 32-bit visibility mask per pixel)
         if (v == RT_VARIANT_HYBRID) return wide_ok && !A.tile_trace && n_frames == 1 && fs == 0;
         return true;
     };

@@ -424,7 +424,10 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
             count_step(c, false);
         }
         const int next = wide_next(nh, cb, imask, oct, sp, stk, wcap);
-        if (next >= 0) N = wload(W, next);
+        // the next node's loads go out before this node's triangle tests, unconditionally (a walk that has ended
+        // reloads the root): a load under a branch is copied into the merged register right after it, and that
+        // copy waits for the load (dragon 0.712 -> 0.689 ms per frame, sportscar 0.931 -> 0.901, car_boxed 0.870 -> 0.858)
+        N = wload(W, next >= 0 ? next : 0);
         if (!PIPE) {
             while (th) {
                 const int i = tb + __builtin_ctz(th);
@@ -441,7 +444,8 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
                     tie = true;
                 }
             }
-        } else if (th) {  // the next triangle's loads go out before this one's test
+        }
+        if (PIPE && th) {  // the next triangle's loads go out before this one's test
             int i = tb + __builtin_ctz(th);
             th &= th - 1u;
             float4 ta = W.tris[3 * i], tb4 = W.tris[3 * i + 1], tc = W.tris[3 * i + 2];
@@ -501,7 +505,7 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
             count_step(c, true);
         }
         const int next = wide_next(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
-        if (next >= 0) N = wload(W, next);
+        N = wload(W, next >= 0 ? next : 0);  // unconditional (closest_wide)
         if (!PIPE) {
             while (th) {
                 const int i = tb + __builtin_ctz(th);
@@ -516,7 +520,8 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
                     if (ld2 > dot(oi, oi)) return false;
                 }
             }
-        } else if (th) {  // software-pipelined as in closest_wide
+        }
+        if (PIPE && th) {  // software-pipelined as in closest_wide
             int i = tb + __builtin_ctz(th);
             th &= th - 1u;
             float4 ta = W.tris[3 * i], tb4 = W.tris[3 * i + 1], tc = W.tris[3 * i + 2];
@@ -859,9 +864,16 @@ __device__ __forceinline__ v3 primary_dir(const KArgs& A, float fx, float fy) {
     return primary_dir(cam_of(A, 0), fx, fy);
 }
 
+// trace_path with each level's shadow rays walked as a wave-level pool (rt_shpool.hpp, RT_VARIANT_SHPOOL)
+template <int MAXB, bool COUNT, int PB>
+__device__ v3 trace_path_shp(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0,
+                             int bh_pix, int* __restrict__ sstk, int wcap);
+
 // Pixel (x, compact row k) of frame `frame` of the launch (outputs at frame * frame_px).
 // SPP1: a build for spp = 1 only (the stratified-sample loop compiled out, fewer live values around the path)
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0, bool SPP1 = false>
+// SHP: the paths' shadow rays through the per-wave shadow pool (trace_path_shp; PB kernels)
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0, bool SPP1 = false,
+          bool SHP = false>
 __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int frame, int x, int k,
                                              int* __restrict__ stk, Ctr& c, unsigned q = 0,
                                              int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
@@ -874,8 +886,12 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
     if (A.bounce_hit)
         for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
     if (SPP1 || A.spp <= 1) {
-        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB>(A, C.pos, primary_dir(C, (float)x, (float)y), stk,
-                                                                  c, hit0, t0, (int)o, q, sstk, wcap));
+        if constexpr (SHP)
+            col = clamp01(trace_path_shp<MAXB, COUNT, PB>(A, C.pos, primary_dir(C, (float)x, (float)y), stk, c, hit0,
+                                                          t0, (int)o, sstk, wcap));
+        else
+            col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB>(A, C.pos, primary_dir(C, (float)x, (float)y),
+                                                                      stk, c, hit0, t0, (int)o, q, sstk, wcap));
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples
         const int g = A.spp_grid;
         v3 acc = mk(0.0f, 0.0f, 0.0f);
@@ -885,8 +901,13 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
                 const float fy = (float)y + ((float)sj + 0.5f) / (float)g;
                 int h;
                 float tt;
-                const v3 cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB>(
-                    A, C.pos, primary_dir(C, fx, fy), stk, c, h, tt, si == 0 && sj == 0 ? (int)o : -1, q, sstk, wcap));
+                v3 cs;
+                if constexpr (SHP)
+                    cs = clamp01(trace_path_shp<MAXB, COUNT, PB>(A, C.pos, primary_dir(C, fx, fy), stk, c, h, tt,
+                                                                 si == 0 && sj == 0 ? (int)o : -1, sstk, wcap));
+                else
+                    cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB>(
+                        A, C.pos, primary_dir(C, fx, fy), stk, c, h, tt, si == 0 && sj == 0 ? (int)o : -1, q, sstk, wcap));
                 acc = add(acc, cs);
                 if (si == 0 && sj == 0) {
                     hit0 = h;
@@ -960,7 +981,7 @@ __device__ __forceinline__ bool next_item(const KArgs& A, int lane, int& reg, in
 // of STACK = 34) and the binary walks' (rare strict fallbacks) in global memory, so that more workgroups
 // fit a CU's LDS: the kernels with OCC > 4 waves per SIMD.
 template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int OCC = 3, bool TRACE = false, bool BATCH = false,
-          int PB = 0, bool DYN = false, bool SPP1 = false>
+          int PB = 0, bool DYN = false, bool SPP1 = false, bool SHP = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(OCC > 0 ? OCC : 1)))
 void k_persist(KArgs A) {
     static_assert(PB != 2 || DYN, "an LDS path buffer lives in the DYN kernels' dynamic LDS");
@@ -990,7 +1011,7 @@ void k_persist(KArgs A) {
         unsigned long long t0 = 0;
         const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
         if (TRACE) t0 = __builtin_amdgcn_s_memrealtime();
-        if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT, REG, 1, PB, SPP1>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, 0u,
+        if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT, REG, 1, PB, SPP1, SHP>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, 0u,
                                                                               sstk, wcap);
         if (TRACE) {  // {begin, end, wave | fallbacks << 32, wave steps | lane node visits << 32} (COUNT)
             const unsigned fb = wave_sum(c.fb - fb0), ws = wave_sum(c.ws - ws0), nv = wave_sum(c.chi + c.shi - nd0);

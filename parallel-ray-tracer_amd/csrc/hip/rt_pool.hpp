@@ -173,7 +173,7 @@ __device__ __forceinline__ void pool_closest(const DScene& s, const PoolLds& L, 
                 c.ws += first_active_lane();
             }
             const int next = wide_next(nh, cb, imask, oct, sp, L.stk + threadIdx.x, wcap);
-            if (next >= 0) N = wload(W, next);
+            N = wload(W, next >= 0 ? next : 0);  // unconditional (rt_kernels.hpp closest_wide)
             while (th) {
                 const int i = tb + __builtin_ctz(th);
                 th &= th - 1u;
@@ -275,7 +275,7 @@ __device__ __forceinline__ void pool_shadow(const DScene& s, const PoolLds& L, i
                 c.ws += first_active_lane();
             }
             const int next = wide_next(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, L.stk + threadIdx.x, wcap);
-            if (next >= 0) N = wload(W, next);
+            N = wload(W, next >= 0 ? next : 0);  // unconditional (rt_kernels.hpp closest_wide)
             bool occl = false;
             while (th) {
                 const int i = tb + __builtin_ctz(th);

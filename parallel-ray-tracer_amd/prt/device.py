@@ -16,7 +16,7 @@ KERNELS = {"auto": 0, "strict": 1, "fast": 2}
 # rt_frame.variant (launch configurations of the fast kernel, include/rt_hip.h); a variant name is also
 # accepted as `kernel` (kernel="coop4" == kernel="fast", variant="coop4")
 VARIANTS = {"default": 0, "persist": 1, "persist4": 2, "split": 3, "coop2": 4, "coop4": 5, "coop8": 6, "fan": 7,
-            "pool": 10, "hybrid": 11, "relay": 12}
+            "pool": 10, "hybrid": 11, "relay": 12, "shpool": 13}
 HOT_KERNELS = {"coop4": 0, "coop2": 1, "fan": 2, "relay": 3}  # rt_frame.hot_kernel (RT_HOT_*)
 DEALING = {"default": 0, "global": 1, "rows": 2, "columns": 3, "blocks": 4, "row_major": 5}
 ACCEL = {"auto": 0, "reference": 1, "gpu": 2, "host": 3}

@@ -20,8 +20,9 @@ RGB_TOL = 1e-5
 # with its default rule ("fast"), and each variant forced: k_persist at 4 waves/SIMD ("persist4"), k_coop
 # ("coopG": G lanes per ray), k_fan ("fan":
 # 1 + lights lanes per pixel). k_pool ("pool": tile-local ray queues with dynamic fetch; measured slower, never
-# a default) and the split pipeline have their own tests.
-KERNELS = ["strict", "fast", "persist4", "coop2", "coop4", "coop8", "fan"]
+# a default) and the split pipeline have their own tests. "shpool": k_persist with each level's shadow rays walked
+# as a per-wave pool (rt_shpool.hpp).
+KERNELS = ["strict", "fast", "persist4", "coop2", "coop4", "coop8", "fan", "shpool"]
 
 
 def select(kernel):
@@ -208,7 +209,7 @@ def test_spp_matches_oracle(dev, scenes, spp, kernel):
 _SPP64 = {}
 
 
-@pytest.mark.parametrize("kernel", ["fast", "persist4", "coop4", "fan"])
+@pytest.mark.parametrize("kernel", ["fast", "persist4", "coop4", "fan", "shpool"])
 def test_car_boxed_64spp_matches_oracle(dev, scenes, kernel):
     """BASELINE config 5 (car_boxed 3840x2160, 64 spp, multi-bounce): the reference has one corner ray per
     pixel (cpu/src/main.c:228-239); SURVEY §8d defines spp = s x s stratified sub-pixel samples, mean of the
@@ -470,7 +471,7 @@ def moved_camera(W, H, dx, dz):
     return c
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "strict", "split"])
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "strict", "split", "shpool"])
 @pytest.mark.parametrize("name", ["car_boxed", "dragon"])
 def test_frame_batch_equals_single_frames(dev, name, kernel):
     """rt_render_frames: a batch of frames (different cameras, one persistent launch on the fast paths)
@@ -623,7 +624,7 @@ def test_path_level_placements_render_the_same_frames(dev, name):
         assert a0["stats"]["rays"] == a1["stats"]["rays"], v
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan"])
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "shpool"])
 def test_rotated_row_blocks_cover_every_frame(dev, kernel):
     """rt_frame.frame_shift: frame f of rank q renders block residue (q + f) % N (prt.dist rotate), rows
     past the image skipped — over the N ranks every frame of the batch is rendered exactly once, bit for

@@ -14,7 +14,7 @@ def main():
     for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                k = r["Kernel_Name"].split("(")[0][:60]
+                k = r["Kernel_Name"].split("(")[0][:110]
                 vals.setdefault(k, {}).setdefault(r["Counter_Name"], {}).setdefault(r["Dispatch_Id"], 0.0)
                 vals[k][r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
     for k, cs in sorted(vals.items()):
