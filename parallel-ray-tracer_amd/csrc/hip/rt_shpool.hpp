@@ -68,12 +68,21 @@ __device__ __forceinline__ unsigned shadow_pool(const DScene& s, bool has, v3 ip
     float ld2 = 0.0f, reach = 0.0f, best = FMAX;
     int sp = 0;
     WNode N = {};
+    bool done = false, res = false;  // this lane's finished ray and its result, handed over at the next refill
     for (;;) {
+        // hand the finished rays' results to their owners (bit light of the owner's vis)
+        unsigned long long fin = uni64(__ballot(done && res));
+        while (fin) {
+            const int f = uni(__builtin_ctzll(fin));
+            fin = uni64(fin & (fin - 1ull));
+            const int w = __builtin_amdgcn_readlane(wo, f);
+            vis |= lane == (unsigned)(w & 63) ? 1u << ((w >> 8) & 31) : 0u;
+        }
+        done = res = false;
         PRT_POOL_ADVANCE();
         const unsigned long long idle = uni64(__ballot(!busy));
         if (idle == all && cm == 0) break;
-        bool done = false, res = false;
-        if (cm != 0 && (idle == all || __builtin_popcountll(idle) >= regroup)) {
+        if (cm != 0) {  // refill every idle lane while there is work
             unsigned long long req = idle, got = 0;
             while (req) {
                 if (cm == 0) {
@@ -116,49 +125,48 @@ __device__ __forceinline__ unsigned shadow_pool(const DScene& s, bool has, v3 ip
                 }
             }
         }
-        if (busy) {  // one step of visible_wide
-            unsigned nh, th, imask, nlf;
-            int cb, tb;
-            wide_node<COUNT>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nlf, SHADOW_ORDER_XOR);
-            if (COUNT) {
-                c.shi++;
-                c.shl += nlf;
-                c.nb += 10;
-                count_step(c, true);
-            }
-            const int next = wide_next(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
-            N = wload(W, next >= 0 ? next : 0);  // unconditional (closest_wide)
-            bool occ = false;
-            while (th) {
-                const int i = tb + __builtin_ctz(th);
-                th &= th - 1u;
-                int k;
-                const float tt = hit_triangle(o, d, W.tris + 3 * i, k);
-                if (COUNT) c.sht++;
-                if (tt < best) {
-                    best = tt;
-                    const v3 q = add(o, mul(d, best));
-                    const v3 oi = sub(o, q);
-                    if (ld2 > dot(oi, oi)) {
-                        occ = true;
-                        break;
+        // walk until the wave is idle, or enough of it to refill while work is left: visible_wide's loop, one
+        // ballot per step
+        const bool more = cm != 0 || cj + 1 < nl;
+        for (;;) {
+            if (busy) {  // one step of visible_wide
+                unsigned nh, th, imask, nlf;
+                int cb, tb;
+                wide_node<COUNT>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nlf, SHADOW_ORDER_XOR);
+                if (COUNT) {
+                    c.shi++;
+                    c.shl += nlf;
+                    c.nb += 10;
+                    count_step(c, true);
+                }
+                const int next = wide_next(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
+                N = wload(W, next >= 0 ? next : 0);  // unconditional (closest_wide)
+                bool occ = false;
+                while (th) {
+                    const int i = tb + __builtin_ctz(th);
+                    th &= th - 1u;
+                    int k;
+                    const float tt = hit_triangle(o, d, W.tris + 3 * i, k);
+                    if (COUNT) c.sht++;
+                    if (tt < best) {
+                        best = tt;
+                        const v3 q = add(o, mul(d, best));
+                        const v3 oi = sub(o, q);
+                        if (ld2 > dot(oi, oi)) {
+                            occ = true;
+                            break;
+                        }
                     }
                 }
+                if (occ || next < 0) {
+                    if (!occ && next == -2) c.err++;
+                    done = true;
+                    res = !occ;
+                    busy = false;
+                }
             }
-            if (occ || next < 0) {
-                if (!occ && next == -2) c.err++;
-                done = true;
-                res = !occ;
-                busy = false;
-            }
-        }
-        // hand the finished rays' results to their owners (bit light of the owner's vis)
-        unsigned long long fin = uni64(__ballot(done && res));
-        while (fin) {
-            const int f = uni(__builtin_ctzll(fin));
-            fin = uni64(fin & (fin - 1ull));
-            const int w = __builtin_amdgcn_readlane(wo, f);
-            vis |= lane == (unsigned)(w & 63) ? 1u << ((w >> 8) & 31) : 0u;
+            const unsigned long long id2 = uni64(__ballot(!busy));
+            if (id2 == all || (more && __builtin_popcountll(id2) >= regroup)) break;
         }
     }
     return vis;
