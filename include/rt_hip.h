@@ -96,7 +96,8 @@ enum {
 
 /* rt_frame.variant: launch configuration of RT_KERNEL_FAST */
 enum {
-    RT_VARIANT_DEFAULT = 0,  /* the library's rule: RT_VARIANT_PERSIST4 for frame batches and spp > 1, RT_VARIANT_HYBRID
+    RT_VARIANT_DEFAULT = 0,  /* the library's rule: RT_VARIANT_PERSIST4 for frame batches and spp > 1 (RT_VARIANT_SHPOOL
+                                with 2..3 lights), RT_VARIANT_HYBRID
                                 for single 1-spp frames (RT_VARIANT_PERSIST where it cannot run); with rt_frame.tune = 1
                                 the measured fastest candidate instead */
     RT_VARIANT_PERSIST = 1,  /* k_persist: one lane per pixel path, walks in lockstep, 3 waves per SIMD */

@@ -924,13 +924,15 @@ void launch_paths(const rtd::KArgs& A, int variant, bool count, int device, hipS
     if (variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL) {
         const bool shp = variant == RT_VARIANT_SHPOOL;
         bool pbl = A.gstack && A.wcap > 0;
+        const size_t lds_vis = shp ? sizeof(unsigned) * rtd::BLOCK : 0;  // the shadow pool's visibility words
         if (pbl) {
             int per_cu = 0;
             auto kp = shp ? persist4<MAXB, true>(true, true, true, false) : persist4<MAXB, false>(true, true, true, false);
-            pbl = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, rtd::BLOCK, lds_wide + lds_pb) == hipSuccess &&
+            pbl = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, rtd::BLOCK, lds_wide + lds_pb + lds_vis) ==
+                      hipSuccess &&
                   per_cu >= 4;
         }
-        if (pbl) dyn = lds_wide + lds_pb;
+        if (pbl) dyn = lds_wide + lds_pb + lds_vis;
         // (the 4-wave kernels without the LDS path buffer: a global slab; the bench's batches: the spp = 1 build)
         k = shp ? persist4<MAXB, true>(pbl, batch, A.spp <= 1, count) : persist4<MAXB, false>(pbl, batch, A.spp <= 1, count);
     }
@@ -1318,7 +1320,12 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         // (a multi-sample frame fills the chip like a batch: car_boxed 4K 64 spp 195 ms at 4 waves vs 219 at 3)
         // (single 1-spp frames: the hybrid launch, which measures and keeps k_persist where that is faster; the split
         // pipeline lost to it on every BASELINE scene in round 3, sportscar 3.76 vs 3.04 ms)
-        mode = (n_frames > 1 || f->spp > 1) ? RT_VARIANT_PERSIST4 : RT_VARIANT_HYBRID;
+        // (batches of 2..3-light scenes: the per-wave shadow pool, DESIGN.md §3g — dragon 0.708 -> 0.666 ms per frame;
+        // it loses on 1 light (car_boxed 0.868 vs 0.902: nothing to pool) and on the 4-light sportscar, 0.922 vs 0.953)
+        mode = (n_frames > 1 || f->spp > 1)
+                   ? (ctx->n_lights >= 2 && ctx->n_lights <= 3 && usable(RT_VARIANT_SHPOOL) ? RT_VARIANT_SHPOOL
+                                                                                          : RT_VARIANT_PERSIST4)
+                   : RT_VARIANT_HYBRID;
     if (!usable(mode)) mode = RT_VARIANT_PERSIST;  // (no wide view, or a diagnostics trace)
     int cap = f->waves_cap > 0 ? f->waves_cap : (mode == RT_VARIANT_SPLIT ? 2 : 0);
     const bool tunable = kernel == RT_KERNEL_FAST && f->tune == 1 && f->variant == RT_VARIANT_DEFAULT && !A.tile_trace;

@@ -26,6 +26,35 @@ __device__ __forceinline__ unsigned long long uni64(unsigned long long v) {
 }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// position of the k-th (0-based) set bit of m (k < popcount(m)): a binary search over popcounts, on scalar registers
+// for a wave-uniform (m, k), per lane otherwise
+__device__ __forceinline__ int kth_bit(unsigned long long m, unsigned k) {
+    int pos = 0;
+    unsigned c = (unsigned)__builtin_popcount((unsigned)m);
+    if (k >= c) {
+        k -= c;
+        m >>= 32;
+        pos = 32;
+    }
+    unsigned w = (unsigned)m;
+#pragma unroll
+    for (int b = 16; b >= 2; b >>= 1) {
+        c = (unsigned)__builtin_popcount(w & ((1u << b) - 1u));
+        if (k >= c) {
+            k -= c;
+            w >>= b;
+            pos += b;
+        }
+    }
+    return pos + (k >= (w & 1u) ? 1 : 0);
+}
+// m without its lowest n set bits (n <= popcount(m))
+__device__ __forceinline__ unsigned long long drop_low(unsigned long long m, unsigned n) {
+    if (n == 0) return m;
+    const int p = kth_bit(m, n - 1u);
+    return p >= 63 ? 0ull : m & ~((2ull << p) - 1ull);
+}
+
 // the pool's cursor past exhausted lights: the next light with owners past the back-face test (wave-uniform; one
 // ballot per light, the skip / shadow counts per owner as path_step keeps them)
 __device__ __forceinline__ void pool_advance(const DScene& s, bool has, v3 ip, v3 n, int nl, int& cj,
@@ -49,12 +78,13 @@ __device__ __forceinline__ void pool_advance(const DScene& s, bool has, v3 ip, v
 // (all lanes idle always do). Must be called by every lane of the wave that runs the path loop (uniform flow).
 template <bool COUNT>
 __device__ __forceinline__ unsigned shadow_pool(const DScene& s, bool has, v3 ip, v3 n, int* __restrict__ stk,
-                                                int* __restrict__ sstk, int wcap, int regroup, Ctr& c) {
+                                                int* __restrict__ sstk, int wcap, int regroup, unsigned* visw,
+                                                Ctr& c) {
     const unsigned lane = threadIdx.x & 63u;
     const unsigned long long all = uni64(__ballot(1));
     const int nl = s.n_lights;
     const DWide& W = wide_for(s, true);  // |d| = 1: the unit-direction view
-    unsigned vis = 0;
+    visw[lane] = 0u;  // the wave's 64 visibility words (LDS): bit j of word p = light j visible from lane p's hit
     // the cursor (wave-uniform): light cj, and the owner lanes whose ray toward cj is still unassigned
     int cj = -1;
     unsigned long long cm = 0;
@@ -68,38 +98,36 @@ __device__ __forceinline__ unsigned shadow_pool(const DScene& s, bool has, v3 ip
     float ld2 = 0.0f, reach = 0.0f, best = FMAX;
     int sp = 0;
     WNode N = {};
-    bool done = false, res = false;  // this lane's finished ray and its result, handed over at the next refill
     for (;;) {
-        // hand the finished rays' results to their owners (bit light of the owner's vis)
-        unsigned long long fin = uni64(__ballot(done && res));
-        while (fin) {
-            const int f = uni(__builtin_ctzll(fin));
-            fin = uni64(fin & (fin - 1ull));
-            const int w = __builtin_amdgcn_readlane(wo, f);
-            vis |= lane == (unsigned)(w & 63) ? 1u << ((w >> 8) & 31) : 0u;
-        }
-        done = res = false;
         PRT_POOL_ADVANCE();
         const unsigned long long idle = uni64(__ballot(!busy));
         if (idle == all && cm == 0) break;
         if (cm != 0) {  // refill every idle lane while there is work
-            unsigned long long req = idle, got = 0;
-            while (req) {
-                if (cm == 0) {
-                    PRT_POOL_ADVANCE();
-                    if (cm == 0) break;
+            // every idle lane at once: the k-th requester takes the k-th unassigned owner of light cj, the rest
+            // move on to the next light (one round per light, no per-ray scalar loop)
+            unsigned long long req = idle;
+            bool got = false;
+            while (req != 0ull && cm != 0ull) {
+                const unsigned nreq = (unsigned)__builtin_popcountll(req), nav = (unsigned)__builtin_popcountll(cm);
+                const unsigned k = __builtin_amdgcn_mbcnt_hi((unsigned)(req >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((unsigned)req, 0u));
+                if (((req >> lane) & 1ull) && k < nav) {
+                    wo = kth_bit(cm, k) | (cj << 8);
+                    got = true;
                 }
-                const int r = uni(__builtin_ctzll(req));
-                req = uni64(req & (req - 1ull));
-                const int ow = uni(__builtin_ctzll(cm));
-                cm = uni64(cm & (cm - 1ull));
-                wo = lane == (unsigned)r ? (ow | (cj << 8)) : wo;
-                got = uni64(got | (1ull << r));
+                if (nreq >= nav) {
+                    req = uni64(drop_low(req, nav));
+                    cm = 0ull;
+                    PRT_POOL_ADVANCE();
+                } else {
+                    cm = uni64(drop_low(cm, nreq));
+                    req = 0ull;
+                }
             }
             // the owner's hit point (every lane reads: a cross-lane read needs its source lane active)
             const int src = wo & 63;
             const float px = __shfl(ip.x, src, 64), py = __shfl(ip.y, src, 64), pz = __shfl(ip.z, src, 64);
-            if ((got >> lane) & 1ull) {
+            if (got) {
                 // the reference's shadow ray, light_v (raytracer.c:62-99) as path_step forms it
                 const v3 ipo = mk(px, py, pz);
                 const v3 Lp = xyz(s.lights[2 * (wo >> 8)]);
@@ -112,8 +140,8 @@ __device__ __forceinline__ unsigned shadow_pool(const DScene& s, bool has, v3 ip
                 d = l;
                 if (degenerate(d)) {  // zero direction component: the reference's NaN slabs, walked strictly
                     c.fb++;
-                    res = visible_walk<true, COUNT, true>(s.ref, o, d, ld2, sstk ? sstk : stk, c);
-                    done = true;
+                    if (visible_walk<true, COUNT, true>(s.ref, o, d, ld2, sstk ? sstk : stk, c))
+                        atomicOr(visw + (wo & 63), 1u << ((wo >> 8) & 31));
                 } else {
                     p = ray_pre(o, d);
                     oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
@@ -160,8 +188,7 @@ __device__ __forceinline__ unsigned shadow_pool(const DScene& s, bool has, v3 ip
                 }
                 if (occ || next < 0) {
                     if (!occ && next == -2) c.err++;
-                    done = true;
-                    res = !occ;
+                    if (!occ) atomicOr(visw + (wo & 63), 1u << ((wo >> 8) & 31));  // the owner's visibility bit
                     busy = false;
                 }
             }
@@ -169,7 +196,8 @@ __device__ __forceinline__ unsigned shadow_pool(const DScene& s, bool has, v3 ip
             if (id2 == all || (more && __builtin_popcountll(id2) >= regroup)) break;
         }
     }
-    return vis;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    return visw[lane];
 }
 #undef PRT_POOL_ADVANCE
 
@@ -186,6 +214,14 @@ __device__ v3 trace_path_shp(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, 
         pb = (float4*)(lds_dyn + 2 * wcap * BLOCK) + (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
     } else {
         pb = A.pathbuf + ((size_t)(blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6)) * MAXB) * 64 + (threadIdx.x & 63);
+    }
+    unsigned* visw;  // the shadow pool's visibility words: after the path buffer (PB = 2, launch_paths adds them)
+    if constexpr (PB == 2) {
+        extern __shared__ int lds_dyn[];
+        visw = (unsigned*)((float4*)(lds_dyn + 2 * wcap * BLOCK) + (size_t)BLOCK * MAXB) + (threadIdx.x & ~63u);
+    } else {
+        __shared__ unsigned visw_s[BLOCK];
+        visw = visw_s + (threadIdx.x & ~63u);
     }
     const DScene& s = A.s;
     const v3 amb = mk(s.amb_x, s.amb_y, s.amb_z);
@@ -221,7 +257,7 @@ __device__ v3 trace_path_shp(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, 
                 has = true;
             }
         }
-        const unsigned vis = shadow_pool<COUNT>(s, has, ip, n, stk, sstk, wcap, A.regroup, c);
+        const unsigned vis = shadow_pool<COUNT>(s, has, ip, n, stk, sstk, wcap, A.regroup, visw, c);
         if (has) {  // raytracer.c:144-172 as path_step, the lights' visibility from the pool
             const v3 kd0 = xyz(s.mats[3 * m + 1]);
             v3 col = mk(0.0f + kd0.x * amb.x, 0.0f + kd0.y * amb.y, 0.0f + kd0.z * amb.z);
