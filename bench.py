@@ -50,9 +50,13 @@ def alg_bytes(st, pixels, n_lights, px_bytes=12):
     return nodes + 48 * tri + (84 + 32 * n_lights) * st["hits"] + px_bytes * pixels
 
 
-def pmc_key(scene, W, H, spp, kernel, bvh, output, frames, world):
-    """profiles/pmc_traffic.json key of one bench configuration (tools/pmc_traffic.py writes the same)"""
-    return f"{scene}_{W}x{H}_spp{spp}_{kernel}_{bvh}_{output}_f{frames}_n{world}"
+def pmc_key(args, frames, world):
+    """profiles/pmc_traffic.json key of one bench configuration (tools/pmc_traffic.py takes it from the bench line):
+    every argument that changes what the profiled launches run"""
+    a = args
+    return (f"{a.scene}_{a.width}x{a.height}_spp{a.spp}_b{a.bounces}_{a.kernel}_{a.variant}{'_tune' if a.tune else ''}_"
+            f"{a.bvh}_{a.accel}_r{a.ploc_radius}_{a.output}_o{a.orbit:g}_rb{a.row_block}_s{a.streams}"
+            f"{'_norot' if a.no_rotate else ''}_f{frames}_n{world}")
 
 
 def data_note(name, n_tris, is_standin):
@@ -477,24 +481,39 @@ def main():
     survey_launch = survey_bytes(stc, F * W * n_r, len(scene.lights), 4 if bgra else 12)
     simd_eff = (stc["ch_inner"] + stc["sh_inner"]) / max(1, 64 * stc["wave_steps"])
     k_avg_ms = sum(kfull) / len(kfull)
-    # single-frame latency of this rank's rows (one launch, one frame; autotuned: its trial launch first)
-    rl = device.Renderer(local, stream=stream)
-    rl.upload(scene, accel=args.accel, ploc_radius=args.ploc_radius)
-    for _ in range(3):
-        rl.render(cam, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp, kernel=args.kernel, tune=True,
-                  **out(fg.target(0)[0] if F > 1 else fg.target(0)))
-    lat_tuned = sorted(rl.kernel_times(2))[0]
-    # the drop-in seam as the reference drives it (gpu/src/main.cu:110-115: one render_frame per iteration, each
-    # waited for), with the default launch rule (RT_VARIANT_HYBRID: its measuring and trial frames first)
-    hyb = []
-    for _ in range(26):  # the measuring frame, 2 x 8 trials, then the choice
-        rl.render(cam, W, H, rows=my_rows, bounces=args.bounces, spp=args.spp, kernel=args.kernel,
-                  **out(fg.target(0)[0] if F > 1 else fg.target(0)))
-        hyb.append(rl.sync())
-    lat_default = sorted(hyb[-6:])[len(hyb[-6:]) // 2]
-    lat_ms = min(lat_tuned, lat_default)
-    rl.close()
-    lat = torch.tensor([lat_ms], dtype=torch.float64, device="cuda")
+    # Single-frame latency of this rank's rows: the drop-in seam as the reference drives it (cpu/src/main.c:171-185,
+    # gpu/src/main.cu:110-115: one render_frame per iteration, each waited for) with the library's default rule.
+    # RT_VARIANT_HYBRID measures and tries its candidates on the first frames of a shape (rt_get_launch_info: trial /
+    # settled); the latency is the median HIP-event time of 9 frames after the rule has settled. Measured for the
+    # reference's fixed camera (frame_latency_ms) and for a walkthrough (every frame's camera moved: the rule is keyed
+    # by the frame's shape, so a moving camera settles the same way).
+    px_out = out(fg.target(0)[0] if F > 1 else fg.target(0))
+
+    def seam(cam_of, tune=False, n_after=9, limit=80):
+        rl = device.Renderer(local, stream=stream)
+        rl.upload(scene, accel=args.accel, ploc_radius=args.ploc_radius)
+        ts, n, info = [], 0, {}
+        while n < limit and len(ts) < n_after:
+            rl.render(cam_of(n), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp, kernel=args.kernel,
+                      tune=tune, **px_out)
+            ms = rl.sync()
+            n += 1
+            info = rl.launch_info()
+            if info["settled"]:
+                ts.append(ms)
+        rl.close()
+        ts.sort()
+        return (ts[len(ts) // 2] if ts else float("nan")), n - len(ts), info
+
+    def walk(i):
+        c = host.camera(W, H)
+        c.pos.x += i * args.orbit
+        c.ul.x += i * args.orbit
+        return c
+    lat_default, settle_frames, seam_info = seam(lambda i: cam)
+    lat_walk, settle_walk, _ = seam(walk)
+    lat_tuned, _, _ = seam(lambda i: cam, tune=True)
+    lat = torch.tensor([lat_default], dtype=torch.float64, device="cuda")
     if dist:
         dist.all_reduce(lat, op=dist.ReduceOp.MAX)
 
@@ -502,7 +521,7 @@ def main():
         # PMC counters of THIS configuration, measured by tools/profile.sh on launches of THIS many frames with
         # THIS library build (pmc_key / lib_md5); anything else is reported under pmc_stale, never as measured
         pmc, pmc_stale = {}, None
-        key = pmc_key(args.scene, W, H, args.spp, args.kernel, args.bvh, args.output, F, world)
+        key = pmc_key(args, F, world)
         if os.path.exists(args.traffic_json):
             try:
                 ent = json.load(open(args.traffic_json)).get(key)
@@ -549,10 +568,15 @@ def main():
                        "accel_built": info["accel_built"], "accel_build_ms": info["build_ms"],
                        "wide_depth": info["wide_depth"]},
             "frame_latency_ms": lat.item(),
-            "frame_latency_detail": {"tuned_ms": lat_tuned, "default_rule_ms": lat_default,
-                                     "rule": "min of the autotuned launch (tune=1, min of 2 frames) and the default "
-                                             "rule's steady state (RT_VARIANT_HYBRID, render + sync per frame, median "
-                                             "of the last 6 of 26 frames)"},
+            "frame_latency_detail": {"default_rule_ms": lat_default, "walkthrough_ms": lat_walk, "tuned_ms": lat_tuned,
+                                     "settle_frames": settle_frames, "settle_frames_walkthrough": settle_walk,
+                                     "choice": seam_info,
+                                     "rule": "frame_latency_ms = the default rule (rt_render with rt_frame's launch fields "
+                                             "zeroed, render + sync per frame as the reference's loop): median HIP-event "
+                                             "time of 9 frames after rt_get_launch_info reports the rule settled (its "
+                                             "measuring and trial frames excluded), fixed reference camera; "
+                                             "walkthrough_ms: the same with the camera moved every frame; tuned_ms: "
+                                             "rt_frame.tune = 1, the same way"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": k_avg_ms, "alg_bytes_per_launch": bytes_launch, "frames_per_launch": F,
@@ -563,6 +587,9 @@ def main():
                          "survey_achieved": survey_launch / (k_avg_ms / 1e3) / 1e9,
                          "survey_frac": survey_launch / (k_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                          "simd_efficiency": simd_eff,
+                         # VALU instructions per walk step (PMC SQ_INSTS_VALU of the launch / its wave-level node steps)
+                         "valu_per_wave_step": (pmc["sq_insts_valu_per_launch"] / max(1, stc["wave_steps"])
+                                                if pmc.get("sq_insts_valu_per_launch") else None),
                          # the launch's work per ray (RT_FLAG_COUNTERS): wide-node visits, leaf slots and
                          # triangle tests of the closest (primary + reflection) and the shadow walks
                          "per_ray": {"closest_nodes": stc["ch_inner"] / max(1, stc["primary"] + stc["reflection"]),

@@ -96,41 +96,39 @@ enum {
 
 /* rt_frame.variant: launch configuration of RT_KERNEL_FAST */
 enum {
-    RT_VARIANT_DEFAULT = 0,  /* the library's rule: RT_VARIANT_PERSIST4 for frame batches and spp > 1 (RT_VARIANT_SHPOOL
-                                with 2..3 lights), RT_VARIANT_HYBRID
-                                for single 1-spp frames (RT_VARIANT_PERSIST where it cannot run); with rt_frame.tune = 1
-                                the measured fastest candidate instead */
+    RT_VARIANT_DEFAULT = 0,  /* the library's rule: frame batches and spp > 1 run RT_VARIANT_SHPOOL when the scene has 2+
+                                lights and the shadow pool's LDS path buffer fits, else RT_VARIANT_PERSIST4; single 1-spp
+                                frames run RT_VARIANT_HYBRID (RT_VARIANT_PERSIST where it cannot run); with rt_frame.tune
+                                = 1 the measured fastest candidate instead */
     RT_VARIANT_PERSIST = 1,  /* k_persist: one lane per pixel path, walks in lockstep, 3 waves per SIMD */
     RT_VARIANT_PERSIST4 = 2, /* k_persist at 4 waves per SIMD (path levels in LDS) */
-    RT_VARIANT_SPLIT = 3,    /* closest chains / shadow batches / resolve: three launches (1 spp; a frame batch in the same three) */
+    /* 3: the split pipeline (closest chains / shadow batches / resolve), measured slower, removed in round 4: refused */
     RT_VARIANT_COOP2 = 4,    /* k_coop: 2 lanes per ray (shorter chains for small row sets) */
     RT_VARIANT_COOP4 = 5,    /* k_coop: 4 lanes per ray */
-    RT_VARIANT_COOP8 = 6,    /* k_coop: 8 lanes per ray */
+    /* 6: k_coop with 8 lanes per ray, 3x slower, removed in round 4: refused */
     RT_VARIANT_FAN = 7,      /* k_fan: 1 + lights lanes per pixel (shadow fan-out; 1..7 lights) */
     /* 8, 9: k_chain (each lane's walks back to back), measured slower and removed in round 2: refused */
-    RT_VARIANT_HYBRID = 11,  /* single frames: the tiles an earlier frame of the same shape and camera measured costliest
-                                through k_coop (2 or 4 lanes per ray) on a second stream while k_persist renders the rest.
-                                The first frame of a shape / camera measures (k_persist with per-tile times), the next
-                                ones try hot thresholds and k_persist itself, and the fastest renders from then on
+    /* 10: k_pool (tile-local LDS ray queues behind workgroup barriers), measured slower, removed in round 4: refused */
+    RT_VARIANT_HYBRID = 11,  /* single 1-spp frames: the tiles a measuring frame of the same SHAPE found costliest through
+                                k_coop (2 or 4 lanes per ray) on a second stream while k_persist or the shadow pool renders
+                                the rest. The first frame of a shape measures (k_persist with per-tile times), the next
+                                ones try the candidates -- including the whole-frame kernels -- twice each, and the fastest
+                                renders from then on; every 64 frames a measuring frame renews the tile lists for a moving
+                                camera. Nothing waits on the host: measurements and trials are read by event queries
                                 (rt_frame.hot_pct > 0: that threshold and rt_frame.hot_kernel, no trials) */
-    RT_VARIANT_POOL = 10,    /* k_pool: 16x16-pixel tile per workgroup, each bounce level's closest-hit and shadow rays
-                                compacted into tile-local LDS queues and traced with dynamic fetch (rt_frame.regroup =
-                                idle lanes per refill), 4 waves per SIMD */
-    RT_VARIANT_RELAY = 12,   /* k_relay (single 1-spp frames, 1..7 lights): one workgroup of 1 + lights waves per 8x8 tile,
-                                wave 0 walks the closest-hit chains and wave j level i's shadow rays toward light j - 1 while
-                                wave 0 walks level i + 1 (LDS hand-off); the hybrid launch's relay candidates use it for
-                                the costliest tiles only */
+    /* 12: k_relay (1 + lights waves per tile, LDS hand-off), measured slower, removed in round 4: refused */
     RT_VARIANT_SHPOOL = 13   /* k_persist at 4 waves per SIMD with each bounce level's shadow rays (every pixel's, every
                                 light's) walked as ONE per-wave pool: a lane whose walk ends takes the next unassigned ray,
-                                lanes of ended paths included (rt_frame.regroup = idle lanes per refill; 1..32 lights) */
+                                lanes of ended paths included (rt_frame.regroup = idle lanes per refill; 1..32 lights; the
+                                LDS path buffer must fit 4 workgroups per CU, else RT_VARIANT_PERSIST4 runs) */
 };
 
 /* rt_frame.hot_kernel: the kernel RT_VARIANT_HYBRID sends the hot tiles to when rt_frame.hot_pct > 0 */
 enum {
     RT_HOT_COOP4 = 0, /* k_coop, 4 lanes per ray */
     RT_HOT_COOP2 = 1, /* k_coop, 2 lanes per ray */
-    RT_HOT_FAN = 2,   /* k_fan, 1 + lights lanes per pixel */
-    RT_HOT_RELAY = 3  /* k_relay, 1 + lights waves per 8x8 tile */
+    RT_HOT_FAN = 2    /* k_fan, 1 + lights lanes per pixel */
+    /* 3: k_relay, removed in round 4: refused */
 };
 
 /* rt_frame.dealing: order in which persistent waves take their tiles (k_persist 8x8, k_pool 16x16) */
@@ -166,7 +164,7 @@ typedef struct rt_frame {
                       HIP-event times and the fastest renders from then on; 0: the default rule, no trial launches */
     int waves_cap; /* persistent grids: at most this many workgroups (4 waves each) per CU; 0 = occupancy limit */
     int dealing;   /* RT_DEAL_* */
-    int regroup;   /* k_pool: idle lanes of a wave that trigger a refill from the tile's queue; 0 = 16 */
+    int regroup;   /* RT_VARIANT_SHPOOL: idle lanes of a wave that trigger a refill from the pool; 0 = 16 */
     int hot_pct;   /* RT_VARIANT_HYBRID: tiles whose measured time exceeds hot_pct % of the costliest tile's go to the
                       kernel hot_kernel names; 0 = try several thresholds and hot kernels and keep the fastest */
     int hot_kernel; /* RT_HOT_* (with hot_pct > 0) */
@@ -227,6 +225,18 @@ int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* frame, const rt
  * stats of the call are the batch's sums. rt_gather / rt_download_bmp need a single-frame render. */
 int rt_render_frames(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_frame* frame,
                      const rt_outputs* out);
+/* What the last rt_render / rt_render_frames ran (no synchronisation): the default rule and rt_frame.tune resolve
+ * RT_VARIANT_DEFAULT per shape, trying candidates on the first frames of a shape. A caller timing the drop-in seam
+ * skips frames until `settled` (the reference's own loop needs no such thing: every frame is bit-exact either way). */
+typedef struct rt_launch_info {
+    int variant;      /* RT_VARIANT_* the last render ran (0 for RT_KERNEL_STRICT) */
+    int hot_pct;      /* RT_VARIANT_HYBRID with hot tiles: the threshold, else 0 */
+    int hot_lanes;    /* its lanes per ray (k_coop) or per pixel (k_fan) */
+    int cold_variant; /* its kernel of the cold tiles (RT_VARIANT_PERSIST or RT_VARIANT_SHPOOL) */
+    int trial;        /* 1: a measuring or trial frame of the default rule (or rt_frame.tune) */
+    int settled;      /* 1: the configuration of this shape is decided; no trial frames follow */
+} rt_launch_info;
+int rt_get_launch_info(rt_ctx* ctx, rt_launch_info* info);
 /* load_from_gpu(): copies the last frame's compact rows to host (synchronous); nullable args */
 int rt_download(rt_ctx* ctx, float* h_rgb, int* h_hit);
 /* waits for the stream; kernel_ms (nullable) = the last render's kernel time from HIP events */

@@ -79,15 +79,9 @@ struct KArgs {
     unsigned long long* counters;  // RT_NCOUNT slots (rt_stats order)
     unsigned int* work;            // persistent-kernel tile / pixel counter
     int n_tiles, tiles_x;
-    int regroup;                   // k_pool: idle lanes of a wave that trigger a refill (rt_frame.regroup)
+    int regroup;                   // shadow pool: idle lanes of a wave that trigger a refill (rt_frame.regroup)
     unsigned long long* tile_trace;  // diagnostics (PRT_TILE_TRACE): per-tile timeline (rt_kernels.hpp)
     const int* tile_order;           // nullable: k-th dealt tile = tile_order[k] (default: row-major)
-    // split pipeline (rt_split.hpp): per (level, tile slot) records, path info, visibility bytes, batches
-    float4* srec;
-    unsigned* spinfo;
-    unsigned char* svis;
-    unsigned* sbatch;
-    size_t nslots;
     // frame batches (rt_render_frames): n_frames frames of the same shape, frame f's camera at
     // cams[12 f .. 12 f + 11] (pos, ul, inc_x, inc_y; nullable when n_frames == 1: the fields above),
     // its outputs at pixel offset f * frame_px (frame_px = n_rows * W)
@@ -113,7 +107,7 @@ struct KArgs {
 // agree on every offset (an LDS pointer, 32-bit on gfx950 but 64-bit on the host, once shifted every
 // later field and hung a kernel). Pinned sizes catch such drift at compile time in whichever pass
 // disagrees; never put address-space-qualified pointers in these structs.
-static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 192 && sizeof(KArgs) == 456,
+static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 192 && sizeof(KArgs) == 416,
               "kernel-argument layout changed: update the pinned sizes only after checking both passes agree");
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

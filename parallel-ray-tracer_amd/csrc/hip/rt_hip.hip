@@ -23,10 +23,7 @@
 #include "rt_shpool.hpp"
 #include "rt_coop.hpp"
 #include "rt_fan.hpp"
-#include "rt_relay.hpp"
 #include "rt_output.hpp"
-#include "rt_split.hpp"
-#include "rt_pool.hpp"
 #include "rt_build.hpp"
 
 #include <chrono>
@@ -93,12 +90,19 @@ struct rt_ctx {
     int last_shift = 0;
     int last_frames = 1;     // frames of the last render (rt_render_frames)
     bool batch_sum = false;  // set while rt_render_frames launches frames one by one (counters add up)
-    // frame batches: the cameras on the device (d_cams) and the host copy they were uploaded from
+    // frame batches: the cameras on the device (d_cams, read by the kernels in stream order) and a ring of pinned host
+    // slots they are copied from (upload_cams): a slot is rewritten only once its earlier copy has run, so a changed
+    // camera set never waits for the renders in flight
+    static constexpr int CAM_SLOTS = 8;
     float* d_cams = nullptr;
+    hipEvent_t cam_ev[CAM_SLOTS] = {};
+    int cam_slot = 0;
+    std::vector<float> cams_last;  // the set d_cams holds (after its copy)
+    rt_launch_info last_launch{};  // rt_get_launch_info
     float4* d_pathbuf = nullptr;  // PB kernels: per-wave path levels (rtd::KArgs::pathbuf)
     int* d_gstack = nullptr;      // DYN kernels: the binary walks' stacks (rtd::KArgs::gstack)
-    float* h_cams = nullptr;  // pinned
-    int cams_cap = 0, cams_n = 0;
+    float* h_cams = nullptr;  // pinned: CAM_SLOTS x cams_cap cameras
+    int cams_cap = 0;
     // output stage (rt_gather, rt_download_bmp)
     float* d_full = nullptr;
     int* d_full_hit = nullptr;
@@ -109,12 +113,6 @@ struct rt_ctx {
     size_t bmp_cap = 0;
     unsigned* d_full_bgra = nullptr;  // gathered BGRA8 frames (rt_gather / rt_comm_gather of bgra renders)
     size_t full_bgra_cap = 0;
-    // split pipeline buffers (rt_split.hpp)
-    float4* d_srec = nullptr;
-    unsigned* d_spinfo = nullptr;
-    unsigned char* d_svis = nullptr;
-    unsigned* d_sbatch = nullptr;
-    size_t srec_cap = 0, spinfo_cap = 0, svis_cap = 0, sbatch_cap = 0;
     unsigned long long* d_counters = nullptr;  // rtd::NCOUNT
     std::unordered_map<long long, int*> orders;  // tile dealing orders (rt_frame.dealing), per tx x ty tile grid
     unsigned int* d_work = nullptr;
@@ -143,28 +141,31 @@ struct rt_ctx {
     // bounces, spp, frames, dealing, waves cap): a context that alternates frame shapes keeps every decision
     std::vector<Tune> tunes;
     long long scene_gen = 0;  // bumped by every upload
-    // RT_VARIANT_HYBRID (single frames): the per-tile times of a k_persist frame of the current shape and camera,
-    // and the tile lists they give (the coop tiles of the costliest 8x8 tiles; the rest for k_persist)
+    // RT_VARIANT_HYBRID (single 1-spp frames), keyed by the frame's SHAPE: the per-tile times of a measuring k_persist
+    // frame, the candidates' tile lists they give (the hot kernel's tiles of the costliest 8x8 tiles; the rest for the
+    // cold kernel), the trials and the choice
     struct Hybrid {
         long long scene = -1;
-        int W = 0, rows = 0, off = 0, stride = 0, block = 0, bounces = 0, spp = 0, dealing = 0, pct_req = 0, hk_req = 0;
-        float cam[12] = {};
+        int W = 0, rows = 0, off = 0, stride = 0, block = 0, bounces = 0, dealing = 0, pct_req = 0, hk_req = 0;
         int state = 0;  // 0: measure next; 1: a measuring frame's tile times are on their way to h_tr; 2: lists ready
-        // candidates: hot threshold (0 = k_persist), their lists at d_lists + at[c], trial launch, time, choice
+        long long frames = 0;  // frames since the choice or the last list refresh
         static constexpr int NCAND = 12;
+        static constexpr int ROUNDS = 2;    // trials per candidate (the minimum counts: single frames are noisy)
+        static constexpr int REFRESH = 64;  // frames of a shape between measuring frames once it is decided
+        // candidates: hot threshold (0 = the cold kernel over the whole frame), lanes per ray, k_fan or k_coop for
+        // the hot tiles, the cold tiles' kernel (RT_VARIANT_PERSIST / SHPOOL); their lists at d_lists + at[c]
         int nc = 0, choice = -1;
-        int pct[NCAND] = {}, lanes[NCAND] = {}, n_hot[NCAND] = {}, n_cold[NCAND] = {};
-        bool fan[NCAND] = {};    // the hot tiles through k_fan<lanes> instead of k_coop<lanes>
-        bool relay[NCAND] = {};  // the hot tiles through k_relay (8x8 tiles, 1 + lights waves each)
+        int pct[NCAND] = {}, lanes[NCAND] = {}, cold[NCAND] = {}, n_hot[NCAND] = {}, n_cold[NCAND] = {};
+        bool fan[NCAND] = {};
         size_t at[NCAND] = {};
-        static constexpr int ROUNDS = 2;  // trials per candidate (the minimum counts: single frames are noisy)
         long long launch[NCAND][ROUNDS] = {};
         float ms[NCAND] = {};
         unsigned long long* d_tr = nullptr;  // [tiles][4], rtd::k_persist's TRACE records
         unsigned long long* h_tr = nullptr;  // pinned
         size_t tr_cap = 0, n_tiles = 0;
-        int* d_lists = nullptr;  // per candidate: [hot coop tiles][cold 8x8 tiles: XCD region layout or order]
-        size_t lists_cap = 0;
+        int* d_lists = nullptr;  // per candidate: [hot tiles][cold 8x8 tiles: XCD region layout or order]
+        int* h_lists = nullptr;  // pinned staging of d_lists (stream-ordered copies)
+        size_t lists_cap = 0, hl_cap = 0;
         bool cold_regions = false;
         hipEvent_t ev = nullptr, fork = nullptr, join = nullptr;
         hipStream_t s2 = nullptr;
@@ -173,18 +174,33 @@ struct rt_ctx {
 
 namespace {
 
-// RT_VARIANT_HYBRID candidates: tiles slower than pct % of the slowest tile of the measuring frame go to k_coop
-// with `lanes` lanes per ray (each candidate is tried once against k_persist; hybrid_pick)
-// (lanes: k_coop's lanes per ray; 0: k_fan, 1 + lights lanes per pixel; -1: k_relay, 1 + lights waves per tile)
+// RT_VARIANT_HYBRID candidates: pct = 0: the cold kernel over the whole frame; else the 8x8 tiles slower than pct % of the
+// slowest tile of the measuring frame go to k_coop with `lanes` lanes per ray while the cold kernel renders the rest
+// (each candidate is tried ROUNDS times; hybrid_pick). Measured: car_boxed hot > 45 % k_coop<4>,
+// sportscar hot > 60 % k_coop<2> / <4>, dragon the whole-frame kernels; k_fan and k_relay hot tiles never won.
 struct HotCand {
-    int pct, lanes;
+    int pct, lanes, cold;
 };
-constexpr HotCand HYBRID_CANDS[10] = {{45, 4}, {60, 4}, {75, 4}, {60, 2}, {75, 2}, {60, 0}, {75, 0}, {30, -1}, {50, -1}, {70, -1}};
-// pixel tile of the hot kernel (rtd::GTile): k_coop<2> 8x4, k_coop<4> / k_fan<4> 4x4, k_fan<2> 8x4, k_fan<8> 4x2;
-// k_relay (relay) 8x8
-inline void hot_tile(int g, bool relay, int& tw, int& th) {
-    tw = relay ? 8 : g == 2 ? 8 : 4;
-    th = relay ? 8 : g == 8 ? 2 : 4;
+constexpr HotCand HYBRID_CANDS[] = {{0, 0, RT_VARIANT_PERSIST}, {0, 0, RT_VARIANT_SHPOOL},   {45, 4, RT_VARIANT_PERSIST},
+                                    {60, 4, RT_VARIANT_PERSIST}, {75, 4, RT_VARIANT_PERSIST}, {60, 2, RT_VARIANT_PERSIST},
+                                    {75, 2, RT_VARIANT_PERSIST}, {60, 4, RT_VARIANT_SHPOOL},  {75, 2, RT_VARIANT_SHPOOL}};
+// pixel tile of a group kernel (rtd::GTile): k_coop<2> / k_fan<2> 8x4, k_coop<4> / k_fan<4> 4x4, k_fan<8> 4x2
+inline void hot_tile(int g, int& tw, int& th) {
+    tw = g == 2 ? 8 : 4;
+    th = g == 8 ? 2 : 4;
+}
+
+const char* variant_name(int v) {
+    switch (v) {
+        case RT_VARIANT_PERSIST: return "persist";
+        case RT_VARIANT_PERSIST4: return "persist4";
+        case RT_VARIANT_COOP2: return "coop2";
+        case RT_VARIANT_COOP4: return "coop4";
+        case RT_VARIANT_FAN: return "fan";
+        case RT_VARIANT_HYBRID: return "hybrid";
+        case RT_VARIANT_SHPOOL: return "shpool";
+        default: return "default";
+    }
 }
 
 int fail(rt_ctx* c, hipError_t e, const char* what) {
@@ -872,156 +888,105 @@ int resident(K kernel, int device, int cap = 8, size_t dyn_lds = 0, int block = 
     return std::max(1, std::min(per_cu, cap)) * cus;
 }
 
-// k_persist (the persistent one-lane-per-path kernel) in configuration `variant`:
-//   RT_VARIANT_PERSIST   k_persist, <= 168 VGPRs (3 waves per SIMD), path levels in registers;
-//   RT_VARIANT_PERSIST4  k_persist, <= 128 VGPRs (4 waves per SIMD), path levels in a path buffer: in LDS after
-//                        the wide stack sized to the scene's wide depth when 4 workgroups of that fit a CU (LDS
-//                        measured 1.2 % faster than the global slab on dragon, 2.3 % on car_boxed), else global;
-// `cap`: workgroups per CU at most (0: the occupancy limit); the grid never exceeds the tiles / 4.
-// the 4-wave k_persist instantiation of a launch: path buffer in LDS (pbl) or global memory, frame batch, spp = 1
-// build, counters; SHP: the per-wave shadow pool (rt_shpool.hpp)
+// The persistent kernels run their frame-batch builds for single frames too: with KArgs::cams null a BATCH kernel
+// takes its one camera from the kernel arguments (rt_kernels.hpp cam_of), so one instantiation serves both.
+using KFn = void (*)(rtd::KArgs);
+
+// the 4-wave k_persist instantiation of a launch: path buffer in LDS (pbl) or global memory, the spp = 1 build,
+// counters; SHP: the per-wave shadow pool (rt_shpool.hpp), which needs the LDS path buffer
 template <int MAXB, bool SHP>
-void (*persist4(bool pbl, bool batch, bool spp1, bool count))(rtd::KArgs) {
+KFn persist4(bool pbl, bool spp1, bool count) {
     using rtd::k_persist;
     if (pbl) {
-        if (batch && spp1) return count ? k_persist<MAXB, false, true, true, 4, false, true, 2, true, true, SHP>
-                                        : k_persist<MAXB, false, false, true, 4, false, true, 2, true, true, SHP>;
-        if (batch) return count ? k_persist<MAXB, false, true, true, 4, false, true, 2, true, false, SHP>
-                                : k_persist<MAXB, false, false, true, 4, false, true, 2, true, false, SHP>;
-        return count ? k_persist<MAXB, false, true, true, 4, false, false, 2, true, false, SHP>
-                     : k_persist<MAXB, false, false, true, 4, false, false, 2, true, false, SHP>;
+        if (spp1) return count ? k_persist<MAXB, false, true, true, 4, false, true, 2, true, true, SHP>
+                               : k_persist<MAXB, false, false, true, 4, false, true, 2, true, true, SHP>;
+        return count ? k_persist<MAXB, false, true, true, 4, false, true, 2, true, false, SHP>
+                     : k_persist<MAXB, false, false, true, 4, false, true, 2, true, false, SHP>;
     }
-    // (deep trees: the LDS holds no path buffer next to the stack)
-    if (batch && spp1) return count ? k_persist<MAXB, false, true, true, 4, false, true, 1, false, true, SHP>
-                                    : k_persist<MAXB, false, false, true, 4, false, true, 1, false, true, SHP>;
-    if (batch) return count ? k_persist<MAXB, false, true, true, 4, false, true, 1, false, false, SHP>
-                            : k_persist<MAXB, false, false, true, 4, false, true, 1, false, false, SHP>;
-    return count ? k_persist<MAXB, false, true, true, 4, false, false, 1, false, false, SHP>
-                 : k_persist<MAXB, false, false, true, 4, false, false, 1, false, false, SHP>;
+    if constexpr (!SHP) {  // (deep trees: the LDS holds no path buffer next to the stack)
+        if (spp1) return count ? k_persist<MAXB, false, true, true, 4, false, true, 1, false, true>
+                               : k_persist<MAXB, false, false, true, 4, false, true, 1, false, true>;
+        return count ? k_persist<MAXB, false, true, true, 4, false, true, 1, false, false>
+                     : k_persist<MAXB, false, false, true, 4, false, true, 1, false, false>;
+    }
+    return nullptr;
 }
 
-// k_persist (the persistent one-lane-per-path kernel) in configuration `variant`:
-//   RT_VARIANT_PERSIST   k_persist, <= 168 VGPRs (3 waves per SIMD), path levels in registers;
-//   RT_VARIANT_PERSIST4  k_persist, <= 128 VGPRs (4 waves per SIMD), path levels in a path buffer: in LDS after
-//                        the wide stack sized to the scene's wide depth when 4 workgroups of that fit a CU (LDS
-//                        measured 1.2 % faster than the global slab on dragon, 2.3 % on car_boxed), else global;
+// dynamic LDS of the 4-wave kernels' LDS layout: the wide stack sized to the scene's wide depth, then the path levels
+template <int MAXB>
+size_t pbl_bytes(const rtd::KArgs& A) {
+    return sizeof(int) * 2 * (size_t)A.wcap * rtd::BLOCK + sizeof(float4) * rtd::BLOCK * MAXB;
+}
+// Does that layout fit 4 workgroups per CU for this scene? (the LDS path buffer measured 1.2 % faster than the global
+// slab on dragon, 2.3 % on car_boxed; the shadow pool needs it)
+template <int MAXB>
+bool pbl_fits(const rtd::KArgs& A, int device) {
+    if (!A.gstack || A.wcap <= 0) return false;
+    (void)device;
+    int per_cu = 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persist4<MAXB, false>(true, true, false), rtd::BLOCK,
+                                                        pbl_bytes<MAXB>(A)) == hipSuccess &&
+           per_cu >= 4;
+}
+
+// k_persist (the persistent one-lane-per-path kernel) in configuration `variant`, and its dynamic LDS:
+//   RT_VARIANT_PERSIST   <= 168 VGPRs (3 waves per SIMD), path levels in registers;
+//   RT_VARIANT_PERSIST4  <= 128 VGPRs (4 waves per SIMD), path levels in a path buffer: in LDS after the wide stack
+//                        when 4 workgroups of that fit a CU, else a global slab;
 //   RT_VARIANT_SHPOOL    PERSIST4 with each bounce level's shadow rays walked as a per-wave pool (rt_shpool.hpp);
+//                        PERSIST4 where the LDS path buffer does not fit;
+// a tile trace (A.tile_trace: the hybrid launch's measuring frame, PRT_TILE_TRACE) runs the 3-wave build with
+// per-tile timestamps.
+template <int MAXB>
+KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, size_t& dyn) {
+    dyn = 0;
+    if (A.tile_trace)
+        return count ? rtd::k_persist<MAXB, false, true, true, 3, true, true> : rtd::k_persist<MAXB, false, false, true, 3, true, true>;
+    if (variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL) {
+        const bool pbl = pbl_fits<MAXB>(A, device);
+        if (pbl) dyn = pbl_bytes<MAXB>(A);
+        // (the bench's batches: the spp = 1 build)
+        return variant == RT_VARIANT_SHPOOL && pbl ? persist4<MAXB, true>(true, A.spp <= 1, count)
+                                                   : persist4<MAXB, false>(pbl, A.spp <= 1, count);
+    }
+    return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true> : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
+}
+
 // `cap`: workgroups per CU at most (0: the occupancy limit); the grid never exceeds the tiles / 4.
 template <int MAXB>
 void launch_paths(const rtd::KArgs& A, int variant, bool count, int device, hipStream_t s, int cap) {
-    const bool batch = A.n_frames > 1;
-    const size_t lds_wide = sizeof(int) * 2 * (size_t)A.wcap * rtd::BLOCK;
-    const size_t lds_pb = sizeof(float4) * rtd::BLOCK * MAXB;
-    const int cu_cap = cap > 0 ? cap : 8;
-    if (A.tile_trace) {  // diagnostics (PRT_TILE_TRACE): the 3-wave kernel with per-tile timestamps
-        auto k = count ? rtd::k_persist<MAXB, false, true, true, 3, true> : rtd::k_persist<MAXB, false, false, true, 3, true>;
-        k<<<std::max(1, std::min(resident(k, device, cu_cap), (A.n_tiles + 3) / 4)), rtd::BLOCK, 0, s>>>(A);
-        return;
-    }
-    auto k = count ? rtd::k_persist<MAXB, false, true> : rtd::k_persist<MAXB, false, false>;
-    if (batch) k = count ? rtd::k_persist<MAXB, false, true, true, 3, false, true> : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
     size_t dyn = 0;
-    if (variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL) {
-        const bool shp = variant == RT_VARIANT_SHPOOL;
-        bool pbl = A.gstack && A.wcap > 0;
-        const size_t lds_vis = shp ? sizeof(unsigned) * rtd::BLOCK : 0;  // the shadow pool's visibility words
-        if (pbl) {
-            int per_cu = 0;
-            auto kp = shp ? persist4<MAXB, true>(true, true, true, false) : persist4<MAXB, false>(true, true, true, false);
-            pbl = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, rtd::BLOCK, lds_wide + lds_pb + lds_vis) ==
-                      hipSuccess &&
-                  per_cu >= 4;
-        }
-        if (pbl) dyn = lds_wide + lds_pb + lds_vis;
-        // (the 4-wave kernels without the LDS path buffer: a global slab; the bench's batches: the spp = 1 build)
-        k = shp ? persist4<MAXB, true>(pbl, batch, A.spp <= 1, count) : persist4<MAXB, false>(pbl, batch, A.spp <= 1, count);
-    }
-    const int blocks = std::max(1, std::min(resident(k, device, cu_cap, dyn), (A.n_tiles + 3) / 4));
+    const KFn k = persist_kernel<MAXB>(A, variant, count, device, dyn);
+    const int blocks = std::max(1, std::min(resident(k, device, cap > 0 ? cap : 8, dyn), (A.n_tiles * A.n_frames + 3) / 4));
     k<<<blocks, rtd::BLOCK, dyn, s>>>(A);
 }
 
 rtd::DBvh dview(const DevView& v) { return rtd::DBvh{v.nodes, v.leaves, v.tris, v.orig, v.root}; }
 
-}  // namespace
-
-namespace {
-// k_pool (rt_pool.hpp): one 16 x 16 tile per workgroup, tile-local ray queues with dynamic fetch; dynamic LDS =
-// the wide stack + ray slots + queue (rtd::pool_lds_bytes); cap = workgroups per CU (0: the occupancy limit)
-template <int MAXB>
-int launch_pool(const rtd::KArgs& A, bool count, int device, hipStream_t s, int cap) {
-    auto k = count ? rtd::k_pool<MAXB, true, 4, false> : rtd::k_pool<MAXB, false, 4, false>;
-    if (A.n_frames > 1) k = count ? rtd::k_pool<MAXB, true, 4, true> : rtd::k_pool<MAXB, false, 4, true>;
-    const size_t dyn = rtd::pool_lds_bytes(A.wcap);
-    const int blocks = std::max(1, std::min(resident(k, device, cap > 0 ? cap : 8, dyn), A.n_tiles * A.n_frames));
-    k<<<blocks, rtd::BLOCK, dyn, s>>>(A);
-    return RT_OK;
-}
-
 // k_fan (rt_fan.hpp): R lanes per pixel (closest chain + R - 1 shadow lanes), 64 / R-pixel tiles
 template <int MAXB>
-int launch_fan(const rtd::KArgs& A, int R, bool count, int device, hipStream_t s, int cap) {
-    auto k = count ? rtd::k_fan<MAXB, true, 4> : rtd::k_fan<MAXB, false, 4>;
-    if (R == 2) k = count ? rtd::k_fan<MAXB, true, 2> : rtd::k_fan<MAXB, false, 2>;
-    if (R == 8) k = count ? rtd::k_fan<MAXB, true, 8> : rtd::k_fan<MAXB, false, 8>;
-    if (A.tile_trace && R == 4)  // diagnostics (PRT_TILE_TRACE with PRT_FAN=1 on a 2-3-light scene)
-        k = count ? rtd::k_fan<MAXB, true, 4, 3, true> : rtd::k_fan<MAXB, false, 4, 3, true>;
-    if (A.n_frames > 1) {  // frame batch: cameras from A.cams
-        k = count ? rtd::k_fan<MAXB, true, 4, 3, false, true> : rtd::k_fan<MAXB, false, 4, 3, false, true>;
-        if (R == 2) k = count ? rtd::k_fan<MAXB, true, 2, 3, false, true> : rtd::k_fan<MAXB, false, 2, 3, false, true>;
-        if (R == 8) k = count ? rtd::k_fan<MAXB, true, 8, 3, false, true> : rtd::k_fan<MAXB, false, 8, 3, false, true>;
-    }
-    const int blocks = std::max(1, std::min(resident(k, device, cap), (A.n_tiles + 3) / 4));
+KFn fan_kernel(int R, bool count) {
+    using rtd::k_fan;
+    if (R == 2) return count ? k_fan<MAXB, true, 2, 3, false, true> : k_fan<MAXB, false, 2, 3, false, true>;
+    if (R == 8) return count ? k_fan<MAXB, true, 8, 3, false, true> : k_fan<MAXB, false, 8, 3, false, true>;
+    return count ? k_fan<MAXB, true, 4, 3, false, true> : k_fan<MAXB, false, 4, 3, false, true>;
+}
+// k_coop (rt_coop.hpp): G = 2 or 4 lanes per ray; one wave per tile of 64 / G pixels
+template <int MAXB>
+KFn coop_kernel(int G, bool count) {
+    using rtd::k_coop;
+    if (G == 2) return count ? k_coop<MAXB, true, 2, 3, false, true> : k_coop<MAXB, false, 2, 3, false, true>;
+    return count ? k_coop<MAXB, true, 4, 3, false, true> : k_coop<MAXB, false, 4, 3, false, true>;
+}
+// never more workgroups than tiles / 4
+template <int MAXB>
+int launch_group(const rtd::KArgs& A, bool fan, int g, bool count, int device, hipStream_t s, int cap) {
+    const KFn k = fan ? fan_kernel<MAXB>(g, count) : coop_kernel<MAXB>(g, count);
+    const int blocks = std::max(1, std::min(resident(k, device, cap), (A.n_tiles * A.n_frames + 3) / 4));
     k<<<blocks, rtd::BLOCK, 0, s>>>(A);
     return RT_OK;
 }
 
-// k_coop (rt_coop.hpp): G lanes per ray; one wave per tile of 64 / G pixels, never more workgroups than
-// tiles / 4
-template <int MAXB>
-int launch_coop(const rtd::KArgs& A, int G, bool count, int device, hipStream_t s, int cap) {
-    auto k = count ? rtd::k_coop<MAXB, true, 4> : rtd::k_coop<MAXB, false, 4>;
-    if (G == 2) k = count ? rtd::k_coop<MAXB, true, 2> : rtd::k_coop<MAXB, false, 2>;
-    if (G == 8) k = count ? rtd::k_coop<MAXB, true, 8> : rtd::k_coop<MAXB, false, 8>;
-    if (A.tile_trace && G == 4)  // diagnostics (PRT_TILE_TRACE with PRT_COOP=4)
-        k = count ? rtd::k_coop<MAXB, true, 4, 3, true> : rtd::k_coop<MAXB, false, 4, 3, true>;
-    if (A.n_frames > 1) {  // frame batch: cameras from A.cams
-        k = count ? rtd::k_coop<MAXB, true, 4, 3, false, true> : rtd::k_coop<MAXB, false, 4, 3, false, true>;
-        if (G == 2) k = count ? rtd::k_coop<MAXB, true, 2, 3, false, true> : rtd::k_coop<MAXB, false, 2, 3, false, true>;
-        if (G == 8) k = count ? rtd::k_coop<MAXB, true, 8, 3, false, true> : rtd::k_coop<MAXB, false, 8, 3, false, true>;
-    }
-    const int blocks = std::max(1, std::min(resident(k, device, cap), (A.n_tiles + 3) / 4));
-    k<<<blocks, rtd::BLOCK, 0, s>>>(A);
-    return RT_OK;
-}
-
-// k_relay (rt_relay.hpp): one workgroup of 1 + lights waves per 8x8 tile (A.tile_order / A.n_tiles), at most
-// `max_blocks` workgroups (0: every resident one) and never more than 4 per CU (the gstack slots of the strict
-// re-walks: 2 per workgroup, 8 per CU allocated)
-template <int MAXB>
-auto relay_kernel(bool count) {
-    return count ? rtd::k_relay<MAXB, true> : rtd::k_relay<MAXB, false>;
-}
-template <int MAXB>
-int relay_resident(const rtd::KArgs& A, bool count, int device) {
-    int cus = 256;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    const int threads = 64 * (1 + A.s.n_lights);
-    return std::min(resident(relay_kernel<MAXB>(count), device, 4, rtd::relay_lds_bytes(MAXB, A.s.n_lights, A.wcap), threads),
-                    4 * cus);
-}
-template <int MAXB>
-int launch_relay(const rtd::KArgs& A, bool count, int device, hipStream_t s, int max_blocks) {
-    const int threads = 64 * (1 + A.s.n_lights);
-    int blocks = std::min(relay_resident<MAXB>(A, count, device), A.n_tiles);
-    if (max_blocks > 0) blocks = std::min(blocks, max_blocks);
-    auto k = relay_kernel<MAXB>(count);
-    if (A.tile_trace) k = count ? rtd::k_relay<MAXB, true, true> : rtd::k_relay<MAXB, false, true>;  // diagnostics
-    k<<<std::max(1, blocks), threads, rtd::relay_lds_bytes(MAXB, A.s.n_lights, A.wcap), s>>>(A);
-    return RT_OK;
-}
-
-template <int MAXB>
-int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count, int cap_a);  // below
 }  // namespace
 
 namespace {
@@ -1061,6 +1026,40 @@ std::vector<int> region_layout(const std::vector<int>& ord, int tx, int ty, int 
 template <int MAXB>
 int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c);  // below
 
+// A frame batch's cameras to d_cams when they differ from the set it holds. The copy runs in stream order (after the
+// renders in flight, which read the old set) from a ring of pinned slots; only a slot whose previous copy has not
+// run yet -- CAM_SLOTS camera sets in flight -- makes the host wait.
+int upload_cams(rt_ctx* ctx, const rt_camera* cams, int n_frames) {
+    static_assert(sizeof(rt_camera) == 48, "rt_camera = 4 x rt_vec3");
+    const size_t nf = 12 * (size_t)n_frames;
+    if ((int)ctx->cams_last.size() == (int)nf && std::memcmp(ctx->cams_last.data(), cams, sizeof(float) * nf) == 0)
+        return RT_OK;
+    if (ctx->cams_cap < n_frames) {  // (rare: a larger batch; hipFree waits for the device)
+        if (ctx->d_cams) HIPC(hipFree(ctx->d_cams));
+        if (ctx->h_cams) {
+            HIPC(hipStreamSynchronize(ctx->stream));
+            HIPC(hipHostFree(ctx->h_cams));
+        }
+        ctx->d_cams = nullptr;
+        ctx->h_cams = nullptr;
+        ctx->cams_cap = 0;
+        const int cap = std::max(n_frames, 32);
+        HIPC(hipMalloc((void**)&ctx->d_cams, sizeof(float) * 12 * cap));
+        HIPC(hipHostMalloc((void**)&ctx->h_cams, sizeof(float) * 12 * cap * rt_ctx::CAM_SLOTS, hipHostMallocDefault));
+        ctx->cams_cap = cap;
+    }
+    const int sl = ctx->cam_slot;
+    ctx->cam_slot = (sl + 1) % rt_ctx::CAM_SLOTS;
+    if (!ctx->cam_ev[sl]) HIPC(hipEventCreateWithFlags(&ctx->cam_ev[sl], hipEventDisableTiming));
+    else HIPC(hipEventSynchronize(ctx->cam_ev[sl]));  // done long ago unless CAM_SLOTS sets are in flight
+    float* h = ctx->h_cams + (size_t)sl * 12 * ctx->cams_cap;
+    std::memcpy(h, cams, sizeof(float) * nf);
+    HIPC(hipMemcpyAsync(ctx->d_cams, h, sizeof(float) * nf, hipMemcpyHostToDevice, ctx->stream));
+    HIPC(hipEventRecord(ctx->cam_ev[sl], ctx->stream));
+    ctx->cams_last.assign(reinterpret_cast<const float*>(cams), reinterpret_cast<const float*>(cams) + nf);
+    return RT_OK;
+}
+
 // rt_render / rt_render_frames: n_frames frames of the same shape (cameras cams[0..n_frames-1]); outputs
 // [n_frames][n_rows][width]... Persistent fast configurations trace the whole batch in ONE launch (frames'
 // tiles interleaved in the dealing order); other kernels launch once per frame.
@@ -1089,8 +1088,13 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     while (g * g < f->spp) g++;
     if (f->spp < 1 || g * g != f->spp || g > 16) return arg_err(ctx, "rt_render: spp must be a square 1..256");
     if (f->kernel < RT_KERNEL_AUTO || f->kernel > RT_KERNEL_FAST) return arg_err(ctx, "rt_render: bad kernel");
-    if (f->variant < RT_VARIANT_DEFAULT || f->variant > RT_VARIANT_SHPOOL || f->variant == 8 || f->variant == 9 ||
-        f->hot_pct < 0 || f->hot_pct > 100 || f->hot_kernel < RT_HOT_COOP4 || f->hot_kernel > RT_HOT_RELAY ||
+    // (variants 3, 6, 8, 9, 10, 12 -- the split pipeline, k_coop<8>, k_chain, k_pool, k_relay -- measured slower
+    // than k_persist and were removed: refused)
+    const bool known = f->variant == RT_VARIANT_DEFAULT || f->variant == RT_VARIANT_PERSIST ||
+                       f->variant == RT_VARIANT_PERSIST4 || f->variant == RT_VARIANT_COOP2 ||
+                       f->variant == RT_VARIANT_COOP4 || f->variant == RT_VARIANT_FAN ||
+                       f->variant == RT_VARIANT_HYBRID || f->variant == RT_VARIANT_SHPOOL;
+    if (!known || f->hot_pct < 0 || f->hot_pct > 100 || f->hot_kernel < RT_HOT_COOP4 || f->hot_kernel > RT_HOT_FAN ||
         f->tune < 0 || f->tune > 1 ||
         f->waves_cap < 0 || f->waves_cap > 8 || f->dealing < RT_DEAL_DEFAULT || f->dealing > RT_DEAL_ROW_MAJOR ||
         f->regroup < 0 || f->regroup > 64)
@@ -1185,26 +1189,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     A.pathbuf = ctx->d_pathbuf;
     A.gstack = ctx->d_gstack;
     A.wcap = ctx->wide_n > 0 ? std::max(1, std::max(ctx->wide_depth, std::max(ctx->unit_depth, ctx->prim_depth))) : 0;
-    if (n_frames > 1) {  // the batch's cameras, uploaded when they change (pinned staging, stream-ordered)
-        const size_t nf = 12 * (size_t)n_frames;
-        static_assert(sizeof(rt_camera) == 48, "rt_camera = 4 x rt_vec3");
-        if (ctx->cams_cap < n_frames) {
-            HIPC(hipStreamSynchronize(ctx->stream));
-            if (ctx->d_cams) HIPC(hipFree(ctx->d_cams));
-            if (ctx->h_cams) HIPC(hipHostFree(ctx->h_cams));
-            ctx->d_cams = nullptr;
-            ctx->h_cams = nullptr;
-            ctx->cams_cap = ctx->cams_n = 0;
-            HIPC(hipMalloc((void**)&ctx->d_cams, sizeof(float) * nf));
-            HIPC(hipHostMalloc((void**)&ctx->h_cams, sizeof(float) * nf, hipHostMallocDefault));
-            ctx->cams_cap = n_frames;
-        }
-        if (ctx->cams_n != n_frames || std::memcmp(ctx->h_cams, cams, sizeof(float) * nf) != 0) {
-            HIPC(hipStreamSynchronize(ctx->stream));  // an earlier copy from h_cams may still be queued
-            std::memcpy(ctx->h_cams, cams, sizeof(float) * nf);
-            HIPC(hipMemcpyAsync(ctx->d_cams, ctx->h_cams, sizeof(float) * nf, hipMemcpyHostToDevice, ctx->stream));
-            ctx->cams_n = n_frames;
-        }
+    if (n_frames > 1) {  // the batch's cameras, uploaded when they change
+        if (int rc = upload_cams(ctx, cams, n_frames)) return rc;
         A.cams = ctx->d_cams;
     }
     A.regroup = f->regroup > 0 ? f->regroup : 16;
@@ -1216,14 +1202,11 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     // diagnostics: PRT_TILE_TRACE=<file> writes 4 x uint64 per tile of a k_persist frame (rt_kernels.hpp)
     // (s_memrealtime, 100 MHz); synchronous, never used by tests or the bench
     const char* trace_path = std::getenv("PRT_TILE_TRACE");
-    // The buffer holds one record per tile of the FINEST tiling any configuration deals (k_coop<8>: 4x2
-    // pixels); trace_n = the tiles of the configuration that ran.
     unsigned long long* d_trace = nullptr;
-    size_t trace_n = (size_t)A.n_tiles;
+    const size_t trace_n = (size_t)A.n_tiles;
     if (trace_path && kernel == RT_KERNEL_FAST && n_frames == 1) {
-        const size_t cap = (size_t)((f->width + 3) / 4) * (size_t)((f->n_rows + 1) / 2);
-        HIPC(hipMalloc((void**)&d_trace, sizeof(unsigned long long) * 4 * cap));
-        HIPC(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * 4 * cap, ctx->stream));
+        HIPC(hipMalloc((void**)&d_trace, sizeof(unsigned long long) * 4 * trace_n));
+        HIPC(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * 4 * trace_n, ctx->stream));
         A.tile_trace = d_trace;
     }
     // Tile dealing order of the persistent kernels: centre-out (default). The frame ends when the slowest
@@ -1249,15 +1232,14 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         return RT_OK;
     };
     if (int rc = order_for(A.tiles_x, A.n_tiles / A.tiles_x, A.tile_order)) return rc;
-    // XCD-aware dealing of k_persist / k_pool: the centre-out order split into 8 spatial regions, region r
-    // drained first by the workgroups on XCD r (rtd::next_item), so each XCD's L2 holds the part of the scene
-    // its region's rays touch. rt_frame.dealing: BLOCKS = 4 x 2 blocks of tiles, ROWS = 8 bands of tile
-    // rows, COLUMNS = 8 bands of tile columns, GLOBAL = one counter. Same-box, ms per frame: 16-frame
-    // batches of the full frame, dragon 1.060 (global) / 0.938 (blocks) / 0.980 (rows) / 0.942 (columns),
-    // sportscar 0.599 / 0.504, car_boxed 1.067 / 1.041; a single frame 1.862 / 1.871 (blocks) / 1.732
-    // (rows); an 8-GPU rank's rows, batched, 0.220 / 0.208 (blocks) / 0.202 (rows). Default: blocks for
-    // batches of the full frame, row bands otherwise. Device layout: 9 region offsets, then the
-    // concatenated regions' tiles.
+    // XCD-aware dealing of k_persist: the centre-out order split into 8 spatial regions, region r drained first by
+    // the workgroups on XCD r (rtd::next_item), so each XCD's L2 holds the part of the scene its region's rays
+    // touch. rt_frame.dealing: BLOCKS = 4 x 2 blocks of tiles, ROWS = 8 bands of tile rows, COLUMNS = 8 bands of
+    // tile columns, GLOBAL = one counter. Same-box, ms per frame: 16-frame batches of the full frame, dragon 1.060
+    // (global) / 0.938 (blocks) / 0.980 (rows) / 0.942 (columns), sportscar 0.599 / 0.504, car_boxed 1.067 / 1.041;
+    // a single frame 1.862 / 1.871 (blocks) / 1.732 (rows); an 8-GPU rank's rows, batched, 0.220 / 0.208 (blocks) /
+    // 0.202 (rows). Default: blocks for batches of the full frame, row bands otherwise. Device layout: 9 region
+    // offsets, then the concatenated regions' tiles.
     const int* region_off = nullptr;
     const int* region_order = nullptr;
     const bool full_frame = f->row_offset == 0 && f->n_rows == f->height;
@@ -1285,49 +1267,39 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     if (int rc = regions_for(A.tiles_x, A.n_tiles / A.tiles_x, region_off, region_order)) return rc;
     // RT_KERNEL_FAST launch configurations (rt_frame.variant; every one renders the same bits):
     //   PERSIST / PERSIST4  k_persist, one lane per pixel path, walks in lockstep, 8x8 tiles;
-    //   SPLIT               (1 spp, single frames) closest chains, shadow batches, resolve (rt_split.hpp);
-    //   COOP2/4/8           k_coop (rt_coop.hpp): G lanes per ray, 64/G-pixel tiles — shorter chains per tile,
+    //   SHPOOL              k_persist at 4 waves with each level's shadow rays walked as a per-wave pool;
+    //   COOP2/4             k_coop (rt_coop.hpp): G lanes per ray, 64/G-pixel tiles — shorter chains per tile,
     //                       which is what a frame split over many GPUs (few tiles per wave) is bound by;
-    //   FAN                 k_fan (rt_fan.hpp): 1 + lights lanes per pixel.
-    // Default rule (measured): PERSIST4 for frame batches and spp > 1, HYBRID for single 1-spp frames
-    // (k_persist where a frame has no costly tail, or with frame_shift / tile traces). rt_frame.tune = 1 measures instead: the first frame of a (scene upload, frame shape) runs each
-    // candidate TUNE_REPS times (all into the same outputs), the next frame of that shape reads the timings
-    // and keeps the fastest; PRT_TUNE_LOG=1 prints them.
-    // (split: batch items (frame, tile) are packed into 24 bits of a shadow batch entry)
-    const bool split_ok = kernel == RT_KERNEL_FAST && f->spp == 1 && ctx->n_lights >= 1 && ctx->n_lights <= 32 &&
-                          !A.tile_trace && (long long)A.n_tiles * n_frames < (1ll << 24);
+    //   FAN                 k_fan (rt_fan.hpp): 1 + lights lanes per pixel;
+    //   HYBRID              single frames: the costliest tiles through k_coop on a second stream (§3e).
     const bool wide_ok = kernel == RT_KERNEL_FAST && ctx->wide_n > 0;
     const bool fan_ok = wide_ok && ctx->n_lights >= 1 && ctx->n_lights <= 7;
     const int fan_r = ctx->n_lights <= 1 ? 2 : ctx->n_lights <= 3 ? 4 : 8;  // lanes per pixel: 1 + lights
-    // k_relay: single 1-spp frames of 1..7 lights (1 + lights waves per workgroup), dynamic-LDS wide stacks
-    const bool relay_ok = wide_ok && ctx->n_lights >= 1 && ctx->n_lights <= rtd::RELAY_MAXL && f->spp == 1 &&
-                          n_frames == 1 && fs == 0 && A.gstack && A.wcap > 0 && !A.tile_trace;
+    // the shadow pool: 1..32 lights (a 32-bit visibility word per pixel) and the LDS path buffer at 4 workgroups per CU
+    const bool shp_ok = wide_ok && ctx->n_lights >= 1 && ctx->n_lights <= 32 &&
+                        (f->bounces <= 4 ? pbl_fits<4>(A, ctx->device) : pbl_fits<8>(A, ctx->device));
     auto usable = [&](int v) {
-        if (v == RT_VARIANT_RELAY) return relay_ok || (A.tile_trace && wide_ok && ctx->n_lights >= 1 &&
-                                                       ctx->n_lights <= rtd::RELAY_MAXL && f->spp == 1 && fs == 0 &&
-                                                       A.gstack && A.wcap > 0);  // (diagnostics: its tile trace)
-        if (v == RT_VARIANT_SPLIT) return split_ok;
+        if (A.tile_trace) return v == RT_VARIANT_PERSIST;  // (diagnostics: the 3-wave kernel's tile trace)
         if (v == RT_VARIANT_FAN) return fan_ok;
-        if (v >= RT_VARIANT_COOP2 && v <= RT_VARIANT_COOP8) return wide_ok;
-        if (v == 8 || v == 9) return false;  // (k_chain, removed in round 2)
-        if (v == RT_VARIANT_POOL) return wide_ok && !A.tile_trace && A.wcap > 0;
-        if (v == RT_VARIANT_SHPOOL) return wide_ok && ctx->n_lights <= 32;  // (a 32-bit visibility mask per pixel)
-        if (v == RT_VARIANT_HYBRID) return wide_ok && !A.tile_trace && n_frames == 1 && fs == 0;
+        if (v == RT_VARIANT_COOP2 || v == RT_VARIANT_COOP4) return wide_ok;
+        if (v == RT_VARIANT_SHPOOL) return shp_ok;
+        if (v == RT_VARIANT_HYBRID) return wide_ok && n_frames == 1 && fs == 0 && f->spp == 1;
         return true;
     };
+    // The default rule (measured): frame batches and spp > 1 fill the chip, so the kernel with the best
+    // throughput — the shadow pool for scenes of 2+ lights whose LDS path buffer fits (dragon 0.708 -> 0.666 ms per
+    // frame in 20-frame batches; one light leaves nothing to pool: car_boxed 0.868 vs 0.902), else k_persist at 4
+    // waves; a single 1-spp frame is tail-bound: the hybrid launch, which measures its candidates on the frames of
+    // the shape and keeps the fastest (k_persist where it cannot run).
+    const bool pool_rule = shp_ok && ctx->n_lights >= 2;
     int mode = f->variant;
     if (mode == RT_VARIANT_DEFAULT)
-        // (a multi-sample frame fills the chip like a batch: car_boxed 4K 64 spp 195 ms at 4 waves vs 219 at 3)
-        // (single 1-spp frames: the hybrid launch, which measures and keeps k_persist where that is faster; the split
-        // pipeline lost to it on every BASELINE scene in round 3, sportscar 3.76 vs 3.04 ms)
-        // (batches of 2..3-light scenes: the per-wave shadow pool, DESIGN.md §3g — dragon 0.708 -> 0.666 ms per frame;
-        // it loses on 1 light (car_boxed 0.868 vs 0.902: nothing to pool) and on the 4-light sportscar, 0.922 vs 0.953)
-        mode = (n_frames > 1 || f->spp > 1)
-                   ? (ctx->n_lights >= 2 && ctx->n_lights <= 3 && usable(RT_VARIANT_SHPOOL) ? RT_VARIANT_SHPOOL
-                                                                                          : RT_VARIANT_PERSIST4)
-                   : RT_VARIANT_HYBRID;
+        mode = (n_frames > 1 || f->spp > 1) ? (pool_rule ? RT_VARIANT_SHPOOL : RT_VARIANT_PERSIST4) : RT_VARIANT_HYBRID;
+    if (mode == RT_VARIANT_SHPOOL && !shp_ok) mode = RT_VARIANT_PERSIST4;  // (no room for the pool: PERSIST4 itself)
     if (!usable(mode)) mode = RT_VARIANT_PERSIST;  // (no wide view, or a diagnostics trace)
-    int cap = f->waves_cap > 0 ? f->waves_cap : (mode == RT_VARIANT_SPLIT ? 2 : 0);
+    // the whole-frame kernel of a single frame while the hybrid launch measures or tries its candidates
+    const int single_rule = pool_rule ? RT_VARIANT_SHPOOL : RT_VARIANT_PERSIST;
+    int cap = f->waves_cap;
     const bool tunable = kernel == RT_KERNEL_FAST && f->tune == 1 && f->variant == RT_VARIANT_DEFAULT && !A.tile_trace;
     rt_ctx::Tune* Tp = nullptr;
     auto same_shape = [&](const rt_ctx::Tune& t) {
@@ -1360,10 +1332,9 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         T.shift = fs;
         T.dealing = f->dealing;
         T.cap_req = f->waves_cap;
-        // candidates (COOP8 is 3x slower than COOP4 everywhere measured: a variant, not a candidate)
-        const int md[7] = {RT_VARIANT_PERSIST, RT_VARIANT_PERSIST4, RT_VARIANT_PERSIST, RT_VARIANT_SPLIT,
+        const int md[7] = {RT_VARIANT_PERSIST, RT_VARIANT_PERSIST4, RT_VARIANT_PERSIST, RT_VARIANT_SHPOOL,
                            RT_VARIANT_COOP4,   RT_VARIANT_COOP2,    RT_VARIANT_FAN};
-        const int cp[7] = {0, 0, 2, 2, 0, 0, 0};
+        const int cp[7] = {0, 0, 2, 0, 0, 0, 0};
         for (int i = 0; i < 7 && T.n < rt_ctx::TUNE_MAX; i++)
             if (usable(md[i])) {
                 T.mode[T.n] = md[i];
@@ -1374,27 +1345,32 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     bool trial = false;
     if (tunable) {
         rt_ctx::Tune& T = *Tp;
-        if (T.pending) {
-            HIPC(hipEventSynchronize(T.e1[T.n * rt_ctx::TUNE_REPS - 1]));
-            int best = 0;
-            for (int c = 0; c < T.n; c++) {
-                float m = 1e30f;
-                for (int r = 0; r < rt_ctx::TUNE_REPS; r++) {
-                    float ms = 0.0f;
-                    HIPC(hipEventElapsedTime(&ms, T.e0[r * T.n + c], T.e1[r * T.n + c]));
-                    m = std::min(m, ms);
+        if (T.pending) {  // the trials' timings: read once, without waiting while they run
+            const hipError_t q = hipEventQuery(T.e1[T.n * rt_ctx::TUNE_REPS - 1]);
+            if (q == hipSuccess) {
+                int best = 0;
+                for (int c = 0; c < T.n; c++) {
+                    float m = 1e30f;
+                    for (int r = 0; r < rt_ctx::TUNE_REPS; r++) {
+                        float ms = 0.0f;
+                        HIPC(hipEventElapsedTime(&ms, T.e0[r * T.n + c], T.e1[r * T.n + c]));
+                        m = std::min(m, ms);
+                    }
+                    T.ms[c] = m;
+                    if (m < T.ms[best]) best = c;
                 }
-                T.ms[c] = m;
-                if (m < T.ms[best]) best = c;
-            }
-            T.choice = best;
-            T.pending = false;
-            if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1) {
-                static const char* names[] = {"default", "persist", "persist4", "split", "coop2", "coop4",
-                                              "coop8",   "fan",     "-",        "-",      "pool"};
-                std::fprintf(stderr, "[prt tune] %dx%d b%d spp%d f%d:", T.W, T.rows, T.bounces, T.spp, T.frames);
-                for (int c = 0; c < T.n; c++) std::fprintf(stderr, " %s/%d %.3f ms", names[T.mode[c]], T.cap[c], T.ms[c]);
-                std::fprintf(stderr, " -> %d\n", best);
+                T.choice = best;
+                T.pending = false;
+                if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1) {
+                    std::fprintf(stderr, "[prt tune] %dx%d b%d spp%d f%d:", T.W, T.rows, T.bounces, T.spp, T.frames);
+                    for (int c = 0; c < T.n; c++)
+                        std::fprintf(stderr, " %s/%d %.3f ms", variant_name(T.mode[c]), T.cap[c], T.ms[c]);
+                    std::fprintf(stderr, " -> %d\n", best);
+                }
+            } else if (q != hipErrorNotReady) {
+                return fail(ctx, q, "rt_render: tuning trials");
+            } else {
+                (void)hipGetLastError();  // not an error: the trials are still running
             }
         } else if (T.choice < 0) {
             trial = !count;  // counters would add up over the trial launches: such a frame keeps the default
@@ -1404,22 +1380,37 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             cap = T.cap[T.choice];
         }
     }
-    // RT_VARIANT_HYBRID: which launch this frame of the shape and camera gets. The first frame measures (k_persist
-    // with per-tile times, copied to the host behind it); once they have arrived, the tile lists of every candidate
-    // threshold are built at once, and the next frames try the candidates, twice each — k_persist itself and the
-    // hybrid launch for each of HYBRID_CANDS — reading their HIP-event times (the minimum of the two) without
-    // blocking once the last has finished, and keep the fastest (PRT_TUNE_LOG=1 prints them). rt_frame.hot_pct > 0
-    // fixes the threshold instead (no trials). Returns -2: measure; -1: a k_persist frame; c >= 0: candidate c's
-    // hybrid launch (lists at ctx->hy). rc: a HIP failure.
-    auto hybrid_pick = [&](int& rc) -> int {
+    rt_launch_info li{};  // what this render runs (rt_get_launch_info)
+    li.settled = 1;
+    li.trial = trial || (Tp && tunable && Tp->choice < 0) ? 1 : 0;
+    if (li.trial) li.settled = 0;
+    // RT_VARIANT_HYBRID: what this single frame runs. The state is keyed by the frame's SHAPE, not its camera (a
+    // walkthrough moves it every frame). The first frame of a shape measures: k_persist with per-tile times, copied to
+    // pinned host memory behind it. Once they have arrived (an event query, never a wait) the tile lists of every
+    // candidate are built and copied in stream order, and the next frames try the candidates ROUNDS times each,
+    // timed by their own HIP events; when the last trial has finished (a query) the fastest minimum renders from then
+    // on (PRT_TUNE_LOG=1 prints them). Every REFRESH frames of the shape a measuring frame renews the tile lists for
+    // a moving camera (the choice stays). While a measurement or the trials are in flight, a frame runs the static
+    // rule's whole-frame kernel. rt_frame.hot_pct > 0 fixes the threshold (no trials).
+    // kind 0: measuring frame; 1: whole-frame variant c; 2: hybrid candidate c's launch (lists at ctx->hy)
+    struct Pick {
+        int kind, c;
+    };
+    auto hybrid_pick = [&](int& rc) -> Pick {
         rt_ctx::Hybrid& h = ctx->hy;
-        const float cv[12] = {cam->pos.x,   cam->pos.y,   cam->pos.z,   cam->ul.x,    cam->ul.y,    cam->ul.z,
-                              cam->inc_x.x, cam->inc_x.y, cam->inc_x.z, cam->inc_y.x, cam->inc_y.y, cam->inc_y.z};
         const bool same = h.scene == ctx->scene_gen && h.W == f->width && h.rows == f->n_rows && h.off == f->row_offset &&
-                          h.stride == f->row_stride && h.block == rb && h.bounces == f->bounces && h.spp == f->spp &&
-                          h.dealing == f->dealing && h.pct_req == f->hot_pct && h.hk_req == f->hot_kernel &&
-                          std::memcmp(h.cam, cv, sizeof cv) == 0;
-        auto err = [&](hipError_t e, const char* what) { rc = fail(ctx, e, what); return -1; };
+                          h.stride == f->row_stride && h.block == rb && h.bounces == f->bounces &&
+                          h.dealing == f->dealing && h.pct_req == f->hot_pct && h.hk_req == f->hot_kernel;
+        auto err = [&](hipError_t e, const char* what) { rc = fail(ctx, e, what); return Pick{1, single_rule}; };
+        auto in_flight = [&](hipEvent_t e, bool& done) -> hipError_t {  // query, never wait
+            const hipError_t q = hipEventQuery(e);
+            done = q == hipSuccess;
+            if (q == hipErrorNotReady) {
+                (void)hipGetLastError();  // not an error: still running
+                return hipSuccess;
+            }
+            return q;
+        };
         if (!h.ev) {
             hipError_t e = hipEventCreateWithFlags(&h.ev, hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&h.fork, hipEventDisableTiming);
@@ -1427,10 +1418,13 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&h.s2, hipStreamNonBlocking);
             if (e != hipSuccess) return err(e, "rt_render: hybrid events / stream");
         }
-        if (!same) {  // a new shape or camera: measure it
-            if (h.state == 1) {  // an earlier measurement's copy into h_tr must land first
-                const hipError_t e = hipEventSynchronize(h.ev);
-                if (e != hipSuccess) return err(e, "rt_render: hybrid measurement");
+        li.settled = 0;
+        li.trial = 1;
+        if (!same) {  // a new shape: measure it, once an earlier measurement in flight has landed in h_tr
+            if (h.state == 1) {
+                bool done = false;
+                if (hipError_t e = in_flight(h.ev, done); e != hipSuccess) return err(e, "rt_render: hybrid measurement");
+                if (!done) return Pick{1, single_rule};
             }
             h.scene = ctx->scene_gen;
             h.W = f->width;
@@ -1439,13 +1433,12 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             h.stride = f->row_stride;
             h.block = rb;
             h.bounces = f->bounces;
-            h.spp = f->spp;
             h.dealing = f->dealing;
             h.pct_req = f->hot_pct;
             h.hk_req = f->hot_kernel;
-            std::memcpy(h.cam, cv, sizeof cv);
+            h.choice = -1;
             h.n_tiles = (size_t)A.n_tiles;
-            if (h.tr_cap < h.n_tiles) {
+            if (h.tr_cap < h.n_tiles) {  // (no measurement in flight writes h_tr now)
                 if (h.d_tr) (void)hipFree(h.d_tr);
                 if (h.h_tr) (void)hipHostFree(h.h_tr);
                 h.d_tr = h.h_tr = nullptr;
@@ -1458,15 +1451,13 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             }
             h.state = 0;
         }
-        if (h.state == 0) return -2;
+        if (h.state == 2 && h.choice >= 0 && ++h.frames >= rt_ctx::Hybrid::REFRESH) h.state = 0;  // renew the lists
+        if (h.state == 0) return Pick{0, 0};
         if (h.state == 1) {
-            const hipError_t q = hipEventQuery(h.ev);
-            if (q == hipErrorNotReady) {
-                (void)hipGetLastError();  // not an error: the measuring frame is still running
-                return -1;
-            }
-            if (q != hipSuccess) return err(q, "rt_render: hybrid measurement");
-            // the tile lists of every candidate threshold: [hot coop tiles][cold 8x8 tiles], one after another
+            bool done = false;
+            if (hipError_t e = in_flight(h.ev, done); e != hipSuccess) return err(e, "rt_render: hybrid measurement");
+            if (!done) return Pick{1, h.choice >= 0 && h.pct[h.choice] == 0 ? h.cold[h.choice] : single_rule};
+            // the tile lists of every candidate threshold: [hot tiles][cold 8x8 tiles], one after another
             const int tx = A.tiles_x, ty = A.n_tiles / A.tiles_x;
             std::vector<long long> dur(h.n_tiles);
             long long cmax = 1;
@@ -1478,26 +1469,21 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             if (!dealt_centre_out)
                 for (int t = 0; t < (int)ord.size(); t++) ord[t] = t;  // RT_DEAL_ROW_MAJOR
             h.cold_regions = xcd_mode >= 1 && xcd_mode <= 3 && dealt_centre_out;
-            h.nc = 0;
-            if (f->hot_pct > 0) {
-                const int hk = (f->hot_kernel == RT_HOT_FAN && !fan_ok) || (f->hot_kernel == RT_HOT_RELAY && !relay_ok)
-                                   ? RT_HOT_COOP4
-                                   : f->hot_kernel;
-                h.pct[0] = f->hot_pct;
-                h.lanes[0] = hk == RT_HOT_COOP2 ? 2 : hk == RT_HOT_FAN ? fan_r : hk == RT_HOT_RELAY ? 1 : 4;
-                h.fan[0] = hk == RT_HOT_FAN;
-                h.relay[0] = hk == RT_HOT_RELAY;
-                h.nc = 1;
-            } else {
-                h.pct[0] = 0;  // k_persist
-                h.fan[0] = h.relay[0] = false;
-                h.nc = 1;
-                for (const HotCand& hc : HYBRID_CANDS) {
-                    if ((hc.lanes == 0 && !fan_ok) || (hc.lanes < 0 && !relay_ok)) continue;
-                    h.pct[h.nc] = hc.pct;
-                    h.fan[h.nc] = hc.lanes == 0;
-                    h.relay[h.nc] = hc.lanes < 0;
-                    h.lanes[h.nc++] = hc.lanes == 0 ? fan_r : hc.lanes < 0 ? 1 : hc.lanes;
+            const bool keep = h.choice >= 0;  // a refresh: new lists, the same candidates and choice
+            if (!keep) {
+                h.nc = 0;
+                auto add = [&](int pct, int lanes, bool fan, int cold) {
+                    if (h.nc >= rt_ctx::Hybrid::NCAND || !usable(cold)) return;
+                    h.pct[h.nc] = pct;
+                    h.lanes[h.nc] = lanes;
+                    h.fan[h.nc] = fan;
+                    h.cold[h.nc++] = cold;
+                };
+                if (f->hot_pct > 0) {
+                    const bool fan = f->hot_kernel == RT_HOT_FAN && fan_ok;
+                    add(f->hot_pct, fan ? fan_r : f->hot_kernel == RT_HOT_COOP2 ? 2 : 4, fan, RT_VARIANT_PERSIST);
+                } else {
+                    for (const HotCand& hc : HYBRID_CANDS) add(hc.pct, hc.lanes, false, hc.cold);
                 }
             }
             std::vector<int> lists;
@@ -1510,11 +1496,10 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                     if (dur[t] * 100 > (long long)h.pct[c] * cmax) hot8.push_back((int)t);
                 std::stable_sort(hot8.begin(), hot8.end(), [&](int a, int b) { return dur[a] > dur[b]; });
                 if (hot8.size() > h.n_tiles / 2) hot8.resize(h.n_tiles / 2);  // k_coop costs ~2x the wave time
-                if (h.relay[c] && hot8.size() > 1024) hot8.resize(1024);  // k_relay: at most one round of workgroups
                 std::vector<char> is_hot(h.n_tiles, 0);
                 // each 8x8 tile = (8 / TW) x (8 / TH) tiles of the hot kernel (rtd::GTile), hottest first
                 int tw, th;
-                hot_tile(h.lanes[c], h.relay[c], tw, th);
+                hot_tile(h.lanes[c], tw, th);
                 const int ctw = (f->width + tw - 1) / tw, cth = (f->n_rows + th - 1) / th;
                 for (int t : hot8) {
                     is_hot[t] = 1;
@@ -1532,39 +1517,55 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 if (h.cold_regions) cold = region_layout(cold, tx, ty, xcd_mode);
                 lists.insert(lists.end(), cold.begin(), cold.end());
             }
-            if (h.lists_cap < lists.size()) {  // nothing in flight reads the lists: the measuring frame has finished
-                if (h.d_lists) (void)hipFree(h.d_lists);
-                h.d_lists = nullptr;
-                h.lists_cap = 0;
-                const hipError_t e = hipMalloc((void**)&h.d_lists, sizeof(int) * std::max<size_t>(1, lists.size()));
-                if (e != hipSuccess) return err(e, "rt_render: hybrid lists");
-                h.lists_cap = lists.size();
-            }
             if (!lists.empty()) {
-                const hipError_t e = hipMemcpy(h.d_lists, lists.data(), sizeof(int) * lists.size(), hipMemcpyHostToDevice);
+                // pinned staging: the last copy out of it ran before the measuring frame (stream order), which has
+                // finished; the device copy is stream-ordered after every frame that read the old lists
+                if (h.hl_cap < lists.size()) {
+                    if (h.h_lists) (void)hipHostFree(h.h_lists);
+                    h.h_lists = nullptr;
+                    h.hl_cap = 0;
+                    const hipError_t e = hipHostMalloc((void**)&h.h_lists, sizeof(int) * lists.size(), hipHostMallocDefault);
+                    if (e != hipSuccess) return err(e, "rt_render: hybrid lists");
+                    h.hl_cap = lists.size();
+                }
+                if (h.lists_cap < lists.size()) {  // (rare: a new shape; hipFree waits for the device)
+                    if (h.d_lists) (void)hipFree(h.d_lists);
+                    h.d_lists = nullptr;
+                    h.lists_cap = 0;
+                    const hipError_t e = hipMalloc((void**)&h.d_lists, sizeof(int) * lists.size());
+                    if (e != hipSuccess) return err(e, "rt_render: hybrid lists");
+                    h.lists_cap = lists.size();
+                }
+                std::memcpy(h.h_lists, lists.data(), sizeof(int) * lists.size());
+                const hipError_t e = hipMemcpyAsync(h.d_lists, h.h_lists, sizeof(int) * lists.size(),
+                                                    hipMemcpyHostToDevice, ctx->stream);
                 if (e != hipSuccess) return err(e, "rt_render: hybrid lists");
             }
-            for (int c = 0; c < h.nc; c++)  // (k_persist too: the measuring frame also copied)
-                for (int r = 0; r < rt_ctx::Hybrid::ROUNDS; r++) h.launch[c][r] = -1;
-            h.choice = h.nc == 1 ? 0 : -1;
+            if (!keep) {
+                for (int c = 0; c < h.nc; c++)
+                    for (int r = 0; r < rt_ctx::Hybrid::ROUNDS; r++) h.launch[c][r] = -1;
+                h.choice = h.nc == 1 ? 0 : -1;
+            }
+            h.frames = 0;
             h.state = 2;
         }
-        if (h.choice >= 0) return h.pct[h.choice] == 0 ? -1 : h.choice;
+        if (h.choice >= 0) {
+            li.settled = 1;
+            li.trial = 0;
+            return h.pct[h.choice] == 0 ? Pick{1, h.cold[h.choice]} : Pick{2, h.choice};
+        }
         for (int r = 0; r < rt_ctx::Hybrid::ROUNDS; r++)
             for (int c = 0; c < h.nc; c++)
                 if (h.launch[c][r] < 0 || ctx->launches - h.launch[c][r] >= rt_ctx::NEV) {  // untried (or events reused)
                     h.launch[c][r] = ctx->launches;
-                    return h.pct[c] == 0 ? -1 : c;
+                    return h.pct[c] == 0 ? Pick{1, h.cold[c]} : Pick{2, c};
                 }
         long long last = 0;
         for (int c = 0; c < h.nc; c++)
             for (int r = 0; r < rt_ctx::Hybrid::ROUNDS; r++) last = std::max(last, h.launch[c][r]);
-        const hipError_t q = hipEventQuery(ctx->ev1s[last % rt_ctx::NEV]);
-        if (q == hipErrorNotReady) {
-            (void)hipGetLastError();
-            return -1;  // the trials are still running
-        }
-        if (q != hipSuccess) return err(q, "rt_render: hybrid trials");
+        bool done = false;
+        if (hipError_t e = in_flight(ctx->ev1s[last % rt_ctx::NEV], done); e != hipSuccess) return err(e, "rt_render: hybrid trials");
+        if (!done) return Pick{1, single_rule};  // the trials are still running
         int best = 0;
         for (int c = 0; c < h.nc; c++) {
             h.ms[c] = 1e30f;
@@ -1578,14 +1579,17 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             if (h.ms[c] < h.ms[best]) best = c;
         }
         h.choice = best;
+        h.frames = 0;
         if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1) {
             std::fprintf(stderr, "[prt hybrid] %dx%d b%d:", f->width, f->n_rows, f->bounces);
             for (int c = 0; c < h.nc; c++)
-                std::fprintf(stderr, " %s%d/%s%d %.3f ms", h.pct[c] ? "hot>" : "persist", h.pct[c],
-                             h.relay[c] ? "relay" : h.fan[c] ? "fan" : "coop", h.lanes[c], h.ms[c]);
+                std::fprintf(stderr, " %s%d/%s%d/%s %.3f ms", h.pct[c] ? "hot>" : "whole", h.pct[c], h.fan[c] ? "fan" : "coop",
+                             h.lanes[c], variant_name(h.cold[c]), h.ms[c]);
             std::fprintf(stderr, " -> %d\n", best);
         }
-        return h.pct[best] == 0 ? -1 : best;
+        li.settled = 1;
+        li.trial = 0;
+        return h.pct[best] == 0 ? Pick{1, h.cold[best]} : Pick{2, best};
     };
     // one frame of configuration (variant, cap); d_work holds the persistent grids' work counters, and the
     // ray counters restart with every launch (rt_get_stats reports the frame, not the trial launches)
@@ -1593,56 +1597,25 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         if (!ctx->batch_sum)  // a per-frame loop of a batch keeps adding to the batch's counters
             HIPC(hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT, ctx->stream));
         HIPC(hipMemsetAsync(ctx->d_work, 0, 1024, ctx->stream));
+        li.variant = md;
         if (kernel == RT_KERNEL_STRICT) {
+            li.variant = 0;
             auto k = count ? rtd::k_tiles<4, true, true> : rtd::k_tiles<4, true, false>;
             if (f->bounces > 4) k = count ? rtd::k_tiles<8, true, true> : rtd::k_tiles<8, true, false>;
             k<<<grid, rtd::BLOCK, 0, ctx->stream>>>(A);
             return RT_OK;
         }
-        if (md == RT_VARIANT_SPLIT) {
-            rtd::KArgs P = A;
-            if (region_off && n_frames > 1) {  // batches: k_persist's XCD-aware regions
-                P.region_off = region_off;
-                P.tile_order = region_order;
-            }
-            return f->bounces <= 4 ? launch_split<4>(ctx, P, count, cp) : launch_split<8>(ctx, P, count, cp);
-        }
-        if (md == RT_VARIANT_FAN || (md >= RT_VARIANT_COOP2 && md <= RT_VARIANT_COOP8)) {
+        if (md == RT_VARIANT_FAN || md == RT_VARIANT_COOP2 || md == RT_VARIANT_COOP4) {
             rtd::KArgs B = A;
-            const int gr = md == RT_VARIANT_FAN ? fan_r : md == RT_VARIANT_COOP2 ? 2 : md == RT_VARIANT_COOP4 ? 4 : 8;
-            const int tw = gr == 2 ? 8 : 4, th = gr == 8 ? 2 : 4;  // rtd::GTile<gr>
+            const int gr = md == RT_VARIANT_FAN ? fan_r : md == RT_VARIANT_COOP2 ? 2 : 4;
+            int tw, th;
+            hot_tile(gr, tw, th);  // rtd::GTile<gr>
             B.tiles_x = (f->width + tw - 1) / tw;
             const int ty = (f->n_rows + th - 1) / th;
             B.n_tiles = B.tiles_x * ty;
             if (int rc = order_for(B.tiles_x, ty, B.tile_order)) return rc;
-            trace_n = (size_t)B.n_tiles;
-            if (md == RT_VARIANT_FAN)
-                return f->bounces <= 4 ? launch_fan<4>(B, gr, count, ctx->device, ctx->stream, cp)
-                                       : launch_fan<8>(B, gr, count, ctx->device, ctx->stream, cp);
-            return f->bounces <= 4 ? launch_coop<4>(B, gr, count, ctx->device, ctx->stream, cp)
-                                   : launch_coop<8>(B, gr, count, ctx->device, ctx->stream, cp);
-        }
-        if (md == RT_VARIANT_RELAY) {  // k_relay (rt_relay.hpp): every 8x8 tile, centre-out
-            return f->bounces <= 4 ? launch_relay<4>(A, count, ctx->device, ctx->stream, 0)
-                                   : launch_relay<8>(A, count, ctx->device, ctx->stream, 0);
-        }
-        if (md == RT_VARIANT_POOL) {  // k_pool (rt_pool.hpp): 16 x 16 pixel tiles per workgroup
-            rtd::KArgs B = A;
-            B.tiles_x = (f->width + 15) / 16;
-            const int ty = (f->n_rows + 15) / 16;
-            B.n_tiles = B.tiles_x * ty;
-            const int* roff = nullptr;
-            const int* rord = nullptr;
-            if (int rc = regions_for(B.tiles_x, ty, roff, rord)) return rc;
-            if (roff) {
-                B.region_off = roff;
-                B.tile_order = rord;
-            } else if (int rc = order_for(B.tiles_x, ty, B.tile_order)) {
-                return rc;
-            }
-            trace_n = (size_t)B.n_tiles;
-            return f->bounces <= 4 ? launch_pool<4>(B, count, ctx->device, ctx->stream, cp)
-                                   : launch_pool<8>(B, count, ctx->device, ctx->stream, cp);
+            return f->bounces <= 4 ? launch_group<4>(B, md == RT_VARIANT_FAN, gr, count, ctx->device, ctx->stream, cp)
+                                   : launch_group<8>(B, md == RT_VARIANT_FAN, gr, count, ctx->device, ctx->stream, cp);
         }
         rtd::KArgs P = A;
         if (region_off) {
@@ -1651,13 +1624,21 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         }
         if (md == RT_VARIANT_HYBRID) {
             int rc = RT_OK;
-            const int pick = hybrid_pick(rc);
+            const Pick pk = hybrid_pick(rc);
             if (rc) return rc;
             // the frame's HIP-event time starts here, after the host work of the pick (the trials compare them)
             HIPC(hipEventRecord(ctx->ev0, ctx->stream));
-            if (pick >= 0) return f->bounces <= 4 ? launch_hybrid<4>(ctx, A, count, pick) : launch_hybrid<8>(ctx, A, count, pick);
+            if (pk.kind == 2) {
+                li.hot_pct = ctx->hy.pct[pk.c];
+                li.hot_lanes = ctx->hy.lanes[pk.c];
+                li.cold_variant = ctx->hy.cold[pk.c];
+                return f->bounces <= 4 ? launch_hybrid<4>(ctx, A, count, pk.c) : launch_hybrid<8>(ctx, A, count, pk.c);
+            }
             rt_ctx::Hybrid& h = ctx->hy;
-            if (pick == -2) {  // measuring frame: k_persist with per-tile times, copied to the host behind it
+            if (pk.kind == 0) {  // measuring frame: k_persist with per-tile times, copied to the host behind it
+                li.variant = RT_VARIANT_PERSIST;
+                li.trial = 1;
+                li.settled = 0;
                 P.tile_trace = h.d_tr;
                 if (f->bounces <= 4) launch_paths<4>(P, RT_VARIANT_PERSIST, count, ctx->device, ctx->stream, cp);
                 else launch_paths<8>(P, RT_VARIANT_PERSIST, count, ctx->device, ctx->stream, cp);
@@ -1668,7 +1649,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 h.state = 1;
                 return RT_OK;
             }
-            md = RT_VARIANT_PERSIST;  // k_persist chosen, or the measurement / trials still on their way
+            md = pk.c;  // a whole-frame kernel: chosen, tried, or while the measurement / trials are on their way
+            li.variant = md;
         }
         if (f->bounces <= 4) launch_paths<4>(P, md, count, ctx->device, ctx->stream, cp);
         else launch_paths<8>(P, md, count, ctx->device, ctx->stream, cp);
@@ -1703,11 +1685,12 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         HIPC(hipStreamSynchronize(ctx->stream));
         HIPC(hipMemcpy(h.data(), d_trace, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
         HIPC(hipFree(d_trace));
-        if (FILE* f = std::fopen(trace_path, "wb")) {
-            std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
-            std::fclose(f);
+        if (FILE* fp = std::fopen(trace_path, "wb")) {
+            std::fwrite(h.data(), sizeof(unsigned long long), h.size(), fp);
+            std::fclose(fp);
         }
     }
+    ctx->last_launch = li;
     ctx->launches++;
     ctx->last_rgb = rgb;
     ctx->last_bgra = bgra;
@@ -1733,6 +1716,16 @@ extern "C" int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* f, c
 extern "C" int rt_render_frames(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_frame* f,
                                 const rt_outputs* out) {
     return render_batch(ctx, cams, n_frames, f, out);
+}
+
+extern "C" int rt_get_launch_info(rt_ctx* ctx, rt_launch_info* info) {
+    if (!ctx || !info) return RT_E_ARG;
+    if (!ctx->rendered) {
+        ctx->err = "rt_get_launch_info: nothing rendered";
+        return RT_E_STATE;
+    }
+    *info = ctx->last_launch;
+    return RT_OK;
 }
 
 extern "C" int rt_sync(rt_ctx* ctx, float* kernel_ms) {
@@ -1797,57 +1790,19 @@ int grow(rt_ctx* ctx, T** p, size_t& cap, size_t n) {
 }  // namespace
 
 namespace {
-// the split pipeline (rt_split.hpp): closest chains, shadow batches, resolve — three launches
-template <int MAXB>
-int launch_split(rt_ctx* ctx, rtd::KArgs& A, bool count, int cap_a) {
-    const int nl = A.s.n_lights;
-    // a record slot per lane of every (frame, tile) item of the batch: item * 64 + lane (rt_split.hpp)
-    const size_t items = (size_t)A.n_tiles * (size_t)A.n_frames;
-    A.nslots = items * 64;
-    int rc;
-    if ((rc = grow(ctx, &ctx->d_srec, ctx->srec_cap, (size_t)A.bounces * A.nslots * 3)) ||
-        (rc = grow(ctx, &ctx->d_spinfo, ctx->spinfo_cap, A.nslots)) ||
-        (rc = grow(ctx, &ctx->d_svis, ctx->svis_cap, (size_t)A.bounces * std::max(nl, 1) * A.nslots)) ||
-        (rc = grow(ctx, &ctx->d_sbatch, ctx->sbatch_cap, items * A.bounces * std::max(nl, 1))))
-        return rc;
-    A.srec = ctx->d_srec;
-    A.spinfo = ctx->d_spinfo;
-    A.svis = ctx->d_svis;
-    A.sbatch = ctx->d_sbatch;
-    hipStream_t s = ctx->stream;
-    auto ka = count ? rtd::k_split_closest<MAXB, true> : rtd::k_split_closest<MAXB, false>;
-    if (A.n_frames > 1) ka = count ? rtd::k_split_closest<MAXB, true, true> : rtd::k_split_closest<MAXB, false, true>;
-    auto kb = count ? rtd::k_split_shadow<true> : rtd::k_split_shadow<false>;
-    // persistent grids; a block is one wave per SIMD, so the cap is waves per SIMD
-    const int ga = std::max(1, (int)std::min<size_t>((size_t)resident(ka, ctx->device, cap_a), (items + 3) / 4));
-    const int gb = std::max(1, resident(kb, ctx->device, 8));
-    ka<<<ga, rtd::BLOCK, 0, s>>>(A);
-    kb<<<gb, rtd::BLOCK, 0, s>>>(A);
-    rtd::k_split_resolve<MAXB><<<(int)((A.nslots + 255) / 256), 256, 0, s>>>(A);
-    return RT_OK;
-}
-}  // namespace
-
-namespace {
-// RT_VARIANT_HYBRID, one frame: the hot coop tiles (ctx->hy lists) through k_coop<4> on the context's second
-// stream while k_persist renders the cold 8x8 tiles on the context stream; both persistent grids together fill
-// the chip (the coop grid is sized to start every hot tile at once), and the context stream waits for both.
+// RT_VARIANT_HYBRID, one frame: the hot tiles (ctx->hy lists) through k_coop / k_fan on the context's second stream
+// while the cold kernel (k_persist, or the shadow pool) renders the cold 8x8 tiles on the context stream; both
+// persistent grids together fill the chip (the hot grid is sized to start every hot tile at once, at most half the
+// chip), and the context stream waits for both.
 template <int MAXB>
 int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c) {
     rt_ctx::Hybrid& h = ctx->hy;
     const int n_hot = h.n_hot[c], n_cold = h.n_cold[c];
     int* lists = h.d_lists + h.at[c];
-    auto kp = count ? rtd::k_persist<MAXB, false, true> : rtd::k_persist<MAXB, false, false>;
     const int g = h.lanes[c];
-    auto kc = count ? rtd::k_coop<MAXB, true, 4> : rtd::k_coop<MAXB, false, 4>;
-    if (g == 2) kc = count ? rtd::k_coop<MAXB, true, 2> : rtd::k_coop<MAXB, false, 2>;
-    if (h.fan[c]) {
-        kc = count ? rtd::k_fan<MAXB, true, 4> : rtd::k_fan<MAXB, false, 4>;
-        if (g == 2) kc = count ? rtd::k_fan<MAXB, true, 2> : rtd::k_fan<MAXB, false, 2>;
-        if (g == 8) kc = count ? rtd::k_fan<MAXB, true, 8> : rtd::k_fan<MAXB, false, 8>;
-    }
+    const KFn kc = h.fan[c] ? fan_kernel<MAXB>(g, count) : coop_kernel<MAXB>(g, count);
     int tw, th;
-    hot_tile(g, h.relay[c], tw, th);
+    hot_tile(g, tw, th);
     rtd::KArgs B = A;  // the hot kernel's tiles, dealt hottest first from their own work counter
     B.tiles_x = (A.W + tw - 1) / tw;
     B.n_tiles = n_hot;
@@ -1858,19 +1813,17 @@ int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c) {
     P.n_tiles = n_cold;
     P.region_off = h.cold_regions ? lists + n_hot : nullptr;
     P.tile_order = lists + n_hot + (h.cold_regions ? 9 : 0);
-    const int rp = resident(kp, ctx->device);
-    const int rcp = h.relay[c] ? relay_resident<MAXB>(B, count, ctx->device) : resident(kc, ctx->device);
-    // the hot grid starts every hot tile at once (k_relay: one workgroup per tile), at most half the chip
-    const int nc = std::max(1, std::min(h.relay[c] ? n_hot : (n_hot + 3) / 4, rcp / 2));
+    size_t dyn = 0;
+    const KFn kp = persist_kernel<MAXB>(P, h.cold[c], count, ctx->device, dyn);
+    const int rp = resident(kp, ctx->device, 8, dyn);
+    const int rcp = resident(kc, ctx->device);
+    const int nc = std::max(1, std::min((n_hot + 3) / 4, rcp / 2));
     const int np = std::max(1, std::min(rp - (int)((long long)nc * rp / rcp), (n_cold + 3) / 4));
     HIPC(hipEventRecord(h.fork, ctx->stream));  // after the work / counter resets
     HIPC(hipStreamWaitEvent(h.s2, h.fork, 0));
-    if (n_hot > 0) {
-        if (h.relay[c]) launch_relay<MAXB>(B, count, ctx->device, h.s2, nc);
-        else kc<<<nc, rtd::BLOCK, 0, h.s2>>>(B);
-    }
+    if (n_hot > 0) kc<<<nc, rtd::BLOCK, 0, h.s2>>>(B);
     HIPC(hipGetLastError());
-    if (n_cold > 0) kp<<<np, rtd::BLOCK, 0, ctx->stream>>>(P);
+    if (n_cold > 0) kp<<<np, rtd::BLOCK, dyn, ctx->stream>>>(P);
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(h.join, h.s2));
     HIPC(hipStreamWaitEvent(ctx->stream, h.join, 0));
@@ -2384,7 +2337,7 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     for (auto& o : ctx->orders) (void)hipFree(o.second);
     for (void* p : {(void*)ctx->d_full, (void*)ctx->d_full_hit, (void*)ctx->d_stage, (void*)ctx->d_bmp,
-                    (void*)ctx->d_full_bgra, (void*)ctx->d_srec, (void*)ctx->d_spinfo, (void*)ctx->d_svis, (void*)ctx->d_sbatch})
+                    (void*)ctx->d_full_bgra})
         if (p) (void)hipFree(p);
     if (ctx->d_work) (void)hipFree(ctx->d_work);
     for (int i = 0; i < rt_ctx::NEV; i++) {
@@ -2400,6 +2353,9 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     if (ctx->hy.d_tr) (void)hipFree(ctx->hy.d_tr);
     if (ctx->hy.h_tr) (void)hipHostFree(ctx->hy.h_tr);
     if (ctx->hy.d_lists) (void)hipFree(ctx->hy.d_lists);
+    if (ctx->hy.h_lists) (void)hipHostFree(ctx->hy.h_lists);
+    for (hipEvent_t e : ctx->cam_ev)
+        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : {ctx->hy.ev, ctx->hy.fork, ctx->hy.join})
         if (e) (void)hipEventDestroy(e);
     if (ctx->hy.s2) (void)hipStreamDestroy(ctx->hy.s2);

@@ -864,16 +864,17 @@ __device__ __forceinline__ v3 primary_dir(const KArgs& A, float fx, float fy) {
     return primary_dir(cam_of(A, 0), fx, fy);
 }
 
-// trace_path with each level's shadow rays walked as a wave-level pool (rt_shpool.hpp, RT_VARIANT_SHPOOL)
-template <int MAXB, bool COUNT, int PB>
-__device__ v3 trace_path_shp(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0,
-                             int bh_pix, int* __restrict__ sstk, int wcap);
+// the shadow-pool kernels' pixel (rt_shpool.hpp, RT_VARIANT_SHPOOL): every lane of the wave calls it
+struct UCtr;
+template <int MAXB, bool COUNT, bool SPP1>
+__device__ __forceinline__ void render_pixel_shp(const KArgs& A, const Cam& C, int frame, int x, int k, bool valid,
+                                                 int* __restrict__ stk, Ctr& c, UCtr& u, int* __restrict__ sstk,
+                                                 int wcap);
+__device__ __forceinline__ void flush_u(const UCtr& u, unsigned long long* g);
 
 // Pixel (x, compact row k) of frame `frame` of the launch (outputs at frame * frame_px).
 // SPP1: a build for spp = 1 only (the stratified-sample loop compiled out, fewer live values around the path)
-// SHP: the paths' shadow rays through the per-wave shadow pool (trace_path_shp; PB kernels)
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0, bool SPP1 = false,
-          bool SHP = false>
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0, bool SPP1 = false>
 __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int frame, int x, int k,
                                              int* __restrict__ stk, Ctr& c, unsigned q = 0,
                                              int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
@@ -886,11 +887,7 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
     if (A.bounce_hit)
         for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
     if (SPP1 || A.spp <= 1) {
-        if constexpr (SHP)
-            col = clamp01(trace_path_shp<MAXB, COUNT, PB>(A, C.pos, primary_dir(C, (float)x, (float)y), stk, c, hit0,
-                                                          t0, (int)o, sstk, wcap));
-        else
-            col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB>(A, C.pos, primary_dir(C, (float)x, (float)y),
+        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB>(A, C.pos, primary_dir(C, (float)x, (float)y),
                                                                       stk, c, hit0, t0, (int)o, q, sstk, wcap));
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples
         const int g = A.spp_grid;
@@ -902,11 +899,7 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
                 int h;
                 float tt;
                 v3 cs;
-                if constexpr (SHP)
-                    cs = clamp01(trace_path_shp<MAXB, COUNT, PB>(A, C.pos, primary_dir(C, fx, fy), stk, c, h, tt,
-                                                                 si == 0 && sj == 0 ? (int)o : -1, sstk, wcap));
-                else
-                    cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB>(
+                cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB>(
                         A, C.pos, primary_dir(C, fx, fy), stk, c, h, tt, si == 0 && sj == 0 ? (int)o : -1, q, sstk, wcap));
                 acc = add(acc, cs);
                 if (si == 0 && sj == 0) {
@@ -980,11 +973,16 @@ __device__ __forceinline__ bool next_item(const KArgs& A, int lane, int& reg, in
 // DYN: the wide walk's stack in dynamic LDS sized to the scene's wide depth (2 * wcap ints per lane instead
 // of STACK = 34) and the binary walks' (rare strict fallbacks) in global memory, so that more workgroups
 // fit a CU's LDS: the kernels with OCC > 4 waves per SIMD.
+template <bool SHP> struct UCtrSel { struct type {}; };
+template <> struct UCtrSel<true> { using type = UCtr; };
+template <bool SHP> using UCtrOf = typename UCtrSel<SHP>::type;
+
 template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int OCC = 3, bool TRACE = false, bool BATCH = false,
           int PB = 0, bool DYN = false, bool SPP1 = false, bool SHP = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(OCC > 0 ? OCC : 1)))
 void k_persist(KArgs A) {
     static_assert(PB != 2 || DYN, "an LDS path buffer lives in the DYN kernels' dynamic LDS");
+    static_assert(!SHP || PB == 2, "the shadow pool hands its rays over through the LDS path buffer");
     int* stk;
     int* sstk = nullptr;
     int wcap = WSTACK;
@@ -999,6 +997,7 @@ void k_persist(KArgs A) {
     }
     const int lane = threadIdx.x & 63;
     Ctr c = {};
+    UCtrOf<SHP> u = {};  // SHP: the wave-uniform ray counts (rt_shpool.hpp)
     // frame batches: dealt item t = (tile t / n_frames of the dealing order, frame t % n_frames), so the
     // expensive (central) tiles of every frame of the batch start first
     int reg = 0;
@@ -1011,8 +1010,12 @@ void k_persist(KArgs A) {
         unsigned long long t0 = 0;
         const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
         if (TRACE) t0 = __builtin_amdgcn_s_memrealtime();
-        if (x < A.W && k < A.n_rows) render_pixel<MAXB, STRICT, COUNT, REG, 1, PB, SPP1, SHP>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, 0u,
-                                                                              sstk, wcap);
+        if constexpr (SHP)
+            render_pixel_shp<MAXB, COUNT, SPP1>(A, cam_of<BATCH>(A, frame), frame, x, k, x < A.W && k < A.n_rows, stk, c,
+                                                u, sstk, wcap);
+        else if (x < A.W && k < A.n_rows)
+            render_pixel<MAXB, STRICT, COUNT, REG, 1, PB, SPP1>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, 0u, sstk,
+                                                                wcap);
         if (TRACE) {  // {begin, end, wave | fallbacks << 32, wave steps | lane node visits << 32} (COUNT)
             const unsigned fb = wave_sum(c.fb - fb0), ws = wave_sum(c.ws - ws0), nv = wave_sum(c.chi + c.shi - nd0);
             if (lane == 0) {
@@ -1024,6 +1027,7 @@ void k_persist(KArgs A) {
         }
     }
     flush<COUNT>(c, A.counters);
+    if constexpr (SHP) flush_u(u, A.counters);
 }
 
 }  // namespace rtd

@@ -55,51 +55,57 @@ __device__ __forceinline__ unsigned long long drop_low(unsigned long long m, uns
     return p >= 63 ? 0ull : m & ~((2ull << p) - 1ull);
 }
 
-// the pool's cursor past exhausted lights: the next light with owners past the back-face test (wave-uniform; one
-// ballot per light, the skip / shadow counts per owner as path_step keeps them)
-__device__ __forceinline__ void pool_advance(const DScene& s, bool has, v3 ip, v3 n, int nl, int& cj,
-                                             unsigned long long& cm, Ctr& c) {
-    while (cm == 0 && cj + 1 < nl) {
-        cj = uni(cj + 1);
-        const v3 tmp2 = sub(xyz(s.lights[2 * cj]), ip);
-        const bool ok = has && !(dot(tmp2, n) < 0);
-        if (has) {
-            if (ok) c.shad++;
-            else c.skip++;
-        }
-        cm = uni64(__ballot(ok));
-    }
+// Wave-uniform ray counts of the shadow-pool kernels. Their path loop runs in step over the wave (every lane takes
+// part, lanes outside the frame as walkers only), so each count is a popcount of a ballot and lives in a scalar
+// register, instead of one vector register per counter and lane held across every walk (the register budget of the
+// 4-wave kernel is 128 VGPRs; what does not fit spills).
+struct UCtr {
+    unsigned prim, refl, shad, skip, hits, pix;
+};
+__device__ __forceinline__ unsigned popc_wave(bool v) { return (unsigned)__builtin_popcountll(uni64(__ballot(v))); }
+__device__ __forceinline__ void flush_u(const UCtr& u, unsigned long long* g) {
+    if ((threadIdx.x & 63u) != 0u) return;
+    const unsigned v[6] = {u.prim, u.refl, u.shad, u.skip, u.hits, u.pix};
+    const int at[6] = {C_PRIM, C_REFL, C_SHAD, C_SKIP, C_HITS, C_PIX};
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+        if (v[i]) atomicAdd(g + at[i], (unsigned long long)v[i]);
 }
 
-// The shadow rays of one bounce level of the calling lanes' paths, walked as a wave-level pool.
-// has: this lane's path hit a surface at this level (hit point ip, normal n). Returns bit j = 1 iff light j is
-// visible from ip along the reference's shadow ray; lights behind the surface (dot(L - ip, n) < 0, the
-// reference's early-out, raytracer.c:66-67) are not walked and read 0. regroup: idle lanes that trigger a refill
-// (all lanes idle always do). Must be called by every lane of the wave that runs the path loop (uniform flow).
+// The shadow rays of one bounce level of the wave's paths, walked as a wave-level pool.
+// okm: bit j = this lane's path hit a surface at this level and light j passed the back-face test (dot(L - ip, n)
+// >= 0, the reference's early-out, raytracer.c:66-67; failing lights are not walked). lvl: the wave's 64 path-buffer
+// slots of this level (LDS); the owner lane p has stored its hit point in lvl[p].xyz and 0 in lvl[p].w, and the
+// walkers set bit j of lvl[p].w (as an unsigned) when light j is visible from it along the reference's shadow ray.
+// regroup: idle lanes that trigger a refill (all lanes idle always do). Called by every lane of the wave.
 template <bool COUNT>
-__device__ __forceinline__ unsigned shadow_pool(const DScene& s, bool has, v3 ip, v3 n, int* __restrict__ stk,
-                                                int* __restrict__ sstk, int wcap, int regroup, unsigned* visw,
-                                                Ctr& c) {
+__device__ __forceinline__ void shadow_pool(const DScene& s, unsigned okm, float4* lvl, int* __restrict__ stk,
+                                            int* __restrict__ sstk, int wcap, int regroup, Ctr& c, UCtr& u) {
     const unsigned lane = threadIdx.x & 63u;
     const unsigned long long all = uni64(__ballot(1));
     const int nl = s.n_lights;
     const DWide& W = wide_for(s, true);  // |d| = 1: the unit-direction view
-    visw[lane] = 0u;  // the wave's 64 visibility words (LDS): bit j of word p = light j visible from lane p's hit
     // the cursor (wave-uniform): light cj, and the owner lanes whose ray toward cj is still unassigned
     int cj = -1;
     unsigned long long cm = 0;
-#define PRT_POOL_ADVANCE() pool_advance(s, has, ip, n, nl, cj, cm, c)
+    auto advance = [&]() {  // the next light with owners past the back-face test
+        while (cm == 0 && cj + 1 < nl) {
+            cj = uni(cj + 1);
+            cm = uni64(__ballot((okm >> cj) & 1u));
+            u.shad += (unsigned)__builtin_popcountll(cm);
+        }
+    };
     // this lane's ray (owner lane | light << 8) and its walk state (visible_wide's)
     bool busy = false;
     int wo = 0;
-    v3 o = ip, d = ip;
+    v3 o = mk(0.0f, 0.0f, 0.0f), d = o;
     RayPre p = {};
     unsigned oct = 0;
     float ld2 = 0.0f, reach = 0.0f, best = FMAX;
     int sp = 0;
     WNode N = {};
     for (;;) {
-        PRT_POOL_ADVANCE();
+        advance();
         const unsigned long long idle = uni64(__ballot(!busy));
         if (idle == all && cm == 0) break;
         if (cm != 0) {  // refill every idle lane while there is work
@@ -118,18 +124,16 @@ __device__ __forceinline__ unsigned shadow_pool(const DScene& s, bool has, v3 ip
                 if (nreq >= nav) {
                     req = uni64(drop_low(req, nav));
                     cm = 0ull;
-                    PRT_POOL_ADVANCE();
+                    advance();
                 } else {
                     cm = uni64(drop_low(cm, nreq));
                     req = 0ull;
                 }
             }
-            // the owner's hit point (every lane reads: a cross-lane read needs its source lane active)
-            const int src = wo & 63;
-            const float px = __shfl(ip.x, src, 64), py = __shfl(ip.y, src, 64), pz = __shfl(ip.z, src, 64);
             if (got) {
-                // the reference's shadow ray, light_v (raytracer.c:62-99) as path_step forms it
-                const v3 ipo = mk(px, py, pz);
+                // the reference's shadow ray, light_v (raytracer.c:62-99) as path_step forms it, from the owner's hit
+                // point (its path-buffer slot)
+                const v3 ipo = xyz(lvl[wo & 63]);
                 const v3 Lp = xyz(s.lights[2 * (wo >> 8)]);
                 v3 l = sub(Lp, ipo);
                 const float mg = mag(l);
@@ -141,7 +145,7 @@ __device__ __forceinline__ unsigned shadow_pool(const DScene& s, bool has, v3 ip
                 if (degenerate(d)) {  // zero direction component: the reference's NaN slabs, walked strictly
                     c.fb++;
                     if (visible_walk<true, COUNT, true>(s.ref, o, d, ld2, sstk ? sstk : stk, c))
-                        atomicOr(visw + (wo & 63), 1u << ((wo >> 8) & 31));
+                        atomicOr(reinterpret_cast<unsigned*>(lvl + (wo & 63)) + 3, 1u << ((wo >> 8) & 31));
                 } else {
                     p = ray_pre(o, d);
                     oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
@@ -188,7 +192,8 @@ __device__ __forceinline__ unsigned shadow_pool(const DScene& s, bool has, v3 ip
                 }
                 if (occ || next < 0) {
                     if (!occ && next == -2) c.err++;
-                    if (!occ) atomicOr(visw + (wo & 63), 1u << ((wo >> 8) & 31));  // the owner's visibility bit
+                    if (!occ)  // the owner's visibility bit
+                        atomicOr(reinterpret_cast<unsigned*>(lvl + (wo & 63)) + 3, 1u << ((wo >> 8) & 31));
                     busy = false;
                 }
             }
@@ -197,68 +202,77 @@ __device__ __forceinline__ unsigned shadow_pool(const DScene& s, bool has, v3 ip
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    return visw[lane];
 }
-#undef PRT_POOL_ADVANCE
 
 // trace_path (rt_kernels.hpp) with each level's shadow rays walked by shadow_pool: the path loop runs in step over
-// the wave (a lane whose path has ended stays in it as a shadow worker) and a level's colour is formed after the
-// pool with path_step's expressions in the reference's order. Path levels in the path buffer (PB kernels).
-template <int MAXB, bool COUNT, int PB>
-__device__ v3 trace_path_shp(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0,
-                             int bh_pix, int* __restrict__ sstk, int wcap) {
-    static_assert(PB != 0, "the shadow pool keeps path levels in a path buffer");
-    float4* pb;
-    if constexpr (PB == 2) {
-        extern __shared__ int lds_dyn[];
-        pb = (float4*)(lds_dyn + 2 * wcap * BLOCK) + (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
-    } else {
-        pb = A.pathbuf + ((size_t)(blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6)) * MAXB) * 64 + (threadIdx.x & 63);
-    }
-    unsigned* visw;  // the shadow pool's visibility words: after the path buffer (PB = 2, launch_paths adds them)
-    if constexpr (PB == 2) {
-        extern __shared__ int lds_dyn[];
-        visw = (unsigned*)((float4*)(lds_dyn + 2 * wcap * BLOCK) + (size_t)BLOCK * MAXB) + (threadIdx.x & ~63u);
-    } else {
-        __shared__ unsigned visw_s[BLOCK];
-        visw = visw_s + (threadIdx.x & ~63u);
-    }
+// the wave (a lane whose path has ended, or that holds no pixel, stays in it as a shadow worker) and a level's
+// colour is formed after the pool with path_step's expressions in the reference's order. Path levels in the LDS
+// path buffer (PB = 2): a level's slot holds the hit point and the visibility word while the pool runs, and the
+// level's colour and material afterwards. Across the pool a lane keeps only its direction, the hit triangle and the
+// lights' back-face mask; the hit point comes back from the slot, the normal and material from the shading record.
+// hpix >= 0: the pixel's output index, for hit / t (level 0) and bounce_hit.
+template <int MAXB, bool COUNT>
+__device__ __forceinline__ v3 trace_path_shp(const KArgs& A, bool alive, v3 o, v3 d, int* __restrict__ stk, Ctr& c,
+                                             UCtr& u, int hpix, int* __restrict__ sstk, int wcap) {
+    extern __shared__ int lds_dyn[];
+    float4* pb = (float4*)(lds_dyn + 2 * wcap * BLOCK) + (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
+    float4* pbw = pb - (threadIdx.x & 63);  // the wave's slots of level 0
     const DScene& s = A.s;
     const v3 amb = mk(s.amb_x, s.amb_y, s.amb_z);
     int L = 0;
-    bool tail = false, alive = true;
+    bool tail = false;
     for (int it = 0; it < A.bounces; ++it) {
-        if (uni64(__ballot(alive)) == 0ull) break;
-        bool has = false;
-        v3 ip = mk(0.0f, 0.0f, 0.0f), n = ip;
-        int m = 0;
+        const unsigned na = popc_wave(alive);
+        if (na == 0) break;
+        if (it == 0) u.prim += na;
+        else u.refl += na;
+        int hit = -1;  // the hit triangle (original index) | nd << 31 ... as two fields below
+        bool nd_side = false;
+        unsigned okm = 0;
         if (alive) {  // raytracer.c:101-147 as path_step
             float best;
             int nd;
-            if (it == 0) c.prim++;
-            else c.refl++;
             const int orig = closest<false, COUNT, true>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0);
-            if (it == 0) {
-                hit0 = orig;
-                t0 = best;
+            if (hpix >= 0) {
+                if (it == 0) {
+                    if (A.hit) A.hit[hpix] = orig;
+                    if (A.t) A.t[hpix] = best;
+                }
+                if (A.bounce_hit) A.bounce_hit[(size_t)hpix * A.bounces + it] = orig;
             }
-            if (A.bounce_hit && bh_pix >= 0) A.bounce_hit[(size_t)bh_pix * A.bounces + it] = orig;
             if (orig < 0) {  // raytracer.c:132-135
                 pb[it * 64] = make_float4(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z, __int_as_float(0));
                 L = it + 1;
                 tail = false;
                 alive = false;
             } else {
-                c.hits++;
-                ip = add(o, mul(d, best));
-                const float4 sh0 = s.shade[2 * orig], sh1 = s.shade[2 * orig + 1];
-                m = __float_as_int(sh0.w);
-                n = nd ? xyz(sh1) : xyz(sh0);
-                has = true;
+                hit = orig;
+                nd_side = nd != 0;
+                const v3 ip = add(o, mul(d, best));
+                const float4 sh = s.shade[2 * orig + (nd ? 1 : 0)];
+                const v3 n = xyz(sh);
+                for (int j = 0; j < s.n_lights; ++j) {  // light_v's back-face test (raytracer.c:66-67)
+                    const v3 tmp2 = sub(xyz(s.lights[2 * j]), ip);
+                    okm |= dot(tmp2, n) < 0 ? 0u : (1u << j);
+                }
+                pb[it * 64] = make_float4(ip.x, ip.y, ip.z, __uint_as_float(0u));
             }
         }
-        const unsigned vis = shadow_pool<COUNT>(s, has, ip, n, stk, sstk, wcap, A.regroup, visw, c);
-        if (has) {  // raytracer.c:144-172 as path_step, the lights' visibility from the pool
+        const unsigned nh = popc_wave(hit >= 0);
+        u.hits += nh;
+        if (nh) {
+            u.skip += nh * (unsigned)s.n_lights;  // less the rays walked (shadow_pool counts those in u.shad)
+            const unsigned sh0 = u.shad;
+            shadow_pool<COUNT>(s, okm, pbw + it * 64, stk, sstk, wcap, A.regroup, c, u);
+            u.skip -= u.shad - sh0;
+        }
+        if (hit >= 0) {  // raytracer.c:144-172 as path_step, the lights' visibility from the pool
+            const float4 e = pb[it * 64];
+            const v3 ip = xyz(e);
+            const unsigned vis = __float_as_uint(e.w) & okm;
+            const float4 sh0 = s.shade[2 * hit], sh1 = s.shade[2 * hit + 1];
+            const int m = __float_as_int(sh0.w);
+            const v3 n = nd_side ? xyz(sh1) : xyz(sh0);
             const v3 kd0 = xyz(s.mats[3 * m + 1]);
             v3 col = mk(0.0f + kd0.x * amb.x, 0.0f + kd0.y * amb.y, 0.0f + kd0.z * amb.z);
             const v3 v = mul(d, -1.0f);
@@ -268,8 +282,7 @@ __device__ v3 trace_path_shp(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, 
                 float mg = mag(l);
                 l = dvs(l, mg);
                 mg *= mg;
-                const v3 tmp2 = sub(Lp, ip);
-                const int V = dot(tmp2, n) < 0 ? 0 : (int)((vis >> j) & 1u);
+                const int V = (int)((vis >> j) & 1u);  // 0 behind the surface (okm), else the shadow ray's answer
                 const v3 kl = xyz(s.lights[2 * j + 1]);
                 const v3 ks = xyz(s.mats[3 * m]), kd = xyz(s.mats[3 * m + 1]);
                 const float ndl = dot(n, l);
@@ -302,6 +315,40 @@ __device__ v3 trace_path_shp(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, 
         }
     }
     return fold_pb<MAXB>(s, pb, L, tail);
+}
+
+// render_pixel (rt_kernels.hpp) for the shadow-pool kernels: called by EVERY lane of the wave (valid = the lane
+// holds a pixel of the frame), so that the path loop and the pool run in uniform control flow
+template <int MAXB, bool COUNT, bool SPP1>
+__device__ __forceinline__ void render_pixel_shp(const KArgs& A, const Cam& C, int frame, int x, int k, bool valid,
+                                                 int* __restrict__ stk, Ctr& c, UCtr& u, int* __restrict__ sstk,
+                                                 int wcap) {
+    const int y = image_row(A, k, frame);
+    valid = valid && y < A.H;  // frame_shift: a rotated rank's compact rows past the image
+    u.pix += popc_wave(valid);
+    const size_t o = (size_t)frame * A.frame_px + (size_t)k * A.W + x;
+    const int hpix = valid ? (int)o : -1;
+    if (A.bounce_hit && valid)
+        for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
+    v3 col;
+    if (SPP1 || A.spp <= 1) {
+        col = clamp01(trace_path_shp<MAXB, COUNT>(A, valid, C.pos, primary_dir(C, (float)x, (float)y), stk, c, u,
+                                                  hpix, sstk, wcap));
+    } else {  // stratified g x g sub-pixel grid, mean of clamped samples; hit / t from the first sample
+        const int g = A.spp_grid;
+        v3 acc = mk(0.0f, 0.0f, 0.0f);
+        for (int sj = 0; sj < g; ++sj)
+            for (int si = 0; si < g; ++si) {
+                const float fx = (float)x + ((float)si + 0.5f) / (float)g;
+                const float fy = (float)y + ((float)sj + 0.5f) / (float)g;
+                const v3 cs = clamp01(trace_path_shp<MAXB, COUNT>(A, valid, C.pos, primary_dir(C, fx, fy), stk, c, u,
+                                                                  si == 0 && sj == 0 ? hpix : -1, sstk, wcap));
+                acc = add(acc, cs);
+            }
+        const float nn = (float)(g * g);
+        col = mk(acc.x / nn, acc.y / nn, acc.z / nn);
+    }
+    if (valid) store_px(A.rgb, A.bgra, o, col);
 }
 
 }  // namespace rtd

@@ -84,6 +84,11 @@ class SceneInfo(ctypes.Structure):  # rt_scene_info
                 ("unit_depth", ctypes.c_int), ("primary_triangles", ctypes.c_int), ("primary_nodes", ctypes.c_int)]
 
 
+class LaunchInfo(ctypes.Structure):  # rt_launch_info
+    _fields_ = [("variant", ctypes.c_int), ("hot_pct", ctypes.c_int), ("hot_lanes", ctypes.c_int),
+                ("cold_variant", ctypes.c_int), ("trial", ctypes.c_int), ("settled", ctypes.c_int)]
+
+
 _host = None
 _hip = None
 
@@ -150,6 +155,7 @@ def hip():
         L.rt_destroy.restype = None
         L.rt_gather.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         L.rt_get_scene_info.argtypes = [ctypes.c_void_p, P(SceneInfo)]
+        L.rt_get_launch_info.argtypes = [ctypes.c_void_p, P(LaunchInfo)]
         L.rt_gather_to.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.rt_comm_get_id.argtypes = [ctypes.c_void_p]
         L.rt_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_void_p)]

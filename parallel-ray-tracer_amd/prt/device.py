@@ -15,9 +15,9 @@ P = ctypes.POINTER
 KERNELS = {"auto": 0, "strict": 1, "fast": 2}
 # rt_frame.variant (launch configurations of the fast kernel, include/rt_hip.h); a variant name is also
 # accepted as `kernel` (kernel="coop4" == kernel="fast", variant="coop4")
-VARIANTS = {"default": 0, "persist": 1, "persist4": 2, "split": 3, "coop2": 4, "coop4": 5, "coop8": 6, "fan": 7,
-            "pool": 10, "hybrid": 11, "relay": 12, "shpool": 13}
-HOT_KERNELS = {"coop4": 0, "coop2": 1, "fan": 2, "relay": 3}  # rt_frame.hot_kernel (RT_HOT_*)
+VARIANTS = {"default": 0, "persist": 1, "persist4": 2, "coop2": 4, "coop4": 5, "fan": 7, "hybrid": 11, "shpool": 13}
+VARIANT_NAMES = {v: k for k, v in VARIANTS.items()}
+HOT_KERNELS = {"coop4": 0, "coop2": 1, "fan": 2}  # rt_frame.hot_kernel (RT_HOT_*)
 DEALING = {"default": 0, "global": 1, "rows": 2, "columns": 3, "blocks": 4, "row_major": 5}
 ACCEL = {"auto": 0, "reference": 1, "gpu": 2, "host": 3}
 ACCEL_NAMES = {v: k for k, v in ACCEL.items()}
@@ -292,6 +292,17 @@ class Renderer:
         self._chk(_L.rt_get_scene_info(self._ctx, ctypes.byref(i)), "rt_get_scene_info")
         d = {f: getattr(i, f) for f, _ in _lib.SceneInfo._fields_}
         d["accel_built"] = ACCEL_NAMES.get(d["accel_built"], d["accel_built"])
+        return d
+
+    def launch_info(self):
+        """rt_get_launch_info: what the last render ran (variant name, hot tiles, cold kernel) and whether it was a
+        measuring / trial frame of the default rule (`trial`) or the shape's decided configuration (`settled`);
+        no synchronisation"""
+        i = _lib.LaunchInfo()
+        self._chk(_L.rt_get_launch_info(self._ctx, ctypes.byref(i)), "rt_get_launch_info")
+        d = {f: getattr(i, f) for f, _ in _lib.LaunchInfo._fields_}
+        d["variant"] = VARIANT_NAMES.get(d["variant"], d["variant"])
+        d["cold_variant"] = VARIANT_NAMES.get(d["cold_variant"], d["cold_variant"])
         return d
 
     def stats(self):

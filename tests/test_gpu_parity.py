@@ -19,10 +19,9 @@ RGB_TOL = 1e-5
 # every kernel and launch configuration the C-ABI exposes (rt_frame.kernel / rt_frame.variant): STRICT, FAST
 # with its default rule ("fast"), and each variant forced: k_persist at 4 waves/SIMD ("persist4"), k_coop
 # ("coopG": G lanes per ray), k_fan ("fan":
-# 1 + lights lanes per pixel). k_pool ("pool": tile-local ray queues with dynamic fetch; measured slower, never
-# a default) and the split pipeline have their own tests. "shpool": k_persist with each level's shadow rays walked
-# as a per-wave pool (rt_shpool.hpp).
-KERNELS = ["strict", "fast", "persist4", "coop2", "coop4", "coop8", "fan", "shpool"]
+# 1 + lights lanes per pixel). "shpool": k_persist with each level's shadow rays walked as a per-wave pool
+# (rt_shpool.hpp).
+KERNELS = ["strict", "fast", "persist4", "coop2", "coop4", "fan", "shpool"]
 
 
 def select(kernel):
@@ -80,21 +79,6 @@ def test_small_frames_vs_reference_fixture(dev, scenes, kernel, scene, W, H):
     np.testing.assert_array_equal(out["hit"], ref["hit"])
     assert same_bits(out["t"], ref["t"])
     assert same_bits(out["rgb"], ref["rgb"]), np.abs(out["rgb"] - ref["rgb"]).max()
-
-
-def test_pool_variant_vs_reference(dev, scenes):
-    """k_pool (RT_VARIANT_POOL: measured slower, never a default, so not in the KERNELS loops): the car scenes'
-    fixtures, the full 1080p car_boxed frame's md5 and its ray counts"""
-    for scene in ("car_boxed", "car_only"):
-        out = render(dev, scenes[scene], 160, 90, "pool")
-        ref = np.load(os.path.join(GOLD, f"{scene}_160x90_strict.npz"))
-        np.testing.assert_array_equal(out["hit"], ref["hit"])
-        assert same_bits(out["t"], ref["t"]) and same_bits(out["rgb"], ref["rgb"])
-    import hashlib
-    out = render(dev, scenes["car_boxed"], 1920, 1080, "pool", counters=True)
-    md5 = hashlib.md5(out["hit"].astype(np.int32).tobytes() + out["t"].tobytes() + out["rgb"].tobytes()).hexdigest()
-    assert md5 == G["frames"]["car_boxed_1920x1080_strict"]["md5"]
-    assert out["stats"]["rays"] == G["rays"]["car_boxed_1920x1080"]["total"]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -193,7 +177,7 @@ def test_strict_traversal_counters_match_reference_order(dev, scenes):
         assert st[k] == c[k], k
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan"])
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "shpool"])
 @pytest.mark.parametrize("spp", [4, 16])
 def test_spp_matches_oracle(dev, scenes, spp, kernel):
     from tests.oracle_bind import OracleScene
@@ -204,6 +188,25 @@ def test_spp_matches_oracle(dev, scenes, spp, kernel):
     out = render(dev, scenes["car_only"], 64, 36, kernel, spp=spp, counters=True)
     assert same_bits(out["rgb"], ref)
     assert out["stats"]["primary"] == 64 * 36 * spp
+
+
+@pytest.mark.parametrize("kernel", ["default", "shpool", "persist4"])
+@pytest.mark.parametrize("spp", [4, 16])
+def test_spp_of_a_two_light_scene_matches_oracle(dev, spp, kernel):
+    """the default rule sends spp > 1 frames of 2+-light scenes through the shadow pool's multi-sample path
+    (render_pixel_shp): dragon (2 lights) at 4 and 16 spp against the oracle's stratified render_spp, bit for bit,
+    with the oracle's ray counts"""
+    from tests.oracle_bind import OracleScene
+    from tests.scenes import scene_paths
+    o = OracleScene.load(*scene_paths("dragon"))
+    o.build_bvh(3)
+    ref, c = o.render_spp(64, 36, spp)
+    s = host.Scene.named("dragon").build_bvh(3)
+    out = render(dev, s, 64, 36, kernel, spp=spp, counters=True)
+    assert same_bits(out["rgb"], ref), np.abs(out["rgb"] - ref).max()
+    assert out["stats"]["primary"] == 64 * 36 * spp
+    for k in ("primary", "reflection", "shadow"):
+        assert out["stats"][k] == c[k], k
 
 
 _SPP64 = {}
@@ -394,47 +397,7 @@ def test_cli_drop_in_writes_the_reference_bmp(tmp_path):
     assert len(list(cache.iterdir())) == 2
 
 
-@pytest.mark.parametrize("name", ["car_boxed", "sportscar", "dragon"])
-def test_split_pipeline_equals_persistent_kernel(dev, name):
-    """RT_VARIANT_SPLIT (closest/shadow/resolve; measured slower than k_persist in round 3) against RT_VARIANT_PERSIST, on
-    1-, 4- and 2-light scenes: bit-exact to each other and to the fixtures, with identical ray counts"""
-    s = host.Scene.named(name).build_bvh(3)
-    outs = {}
-    for v in ("persist", "split"):
-        outs[v] = render(dev, s, 96, 54, v, counters=True)
-    a, b = outs["persist"], outs["split"]
-    np.testing.assert_array_equal(a["hit"], b["hit"])
-    assert same_bits(a["t"], b["t"]) and same_bits(a["rgb"], b["rgb"])
-    for k in ("primary", "reflection", "shadow", "shadow_skipped", "hits", "pixels"):
-        assert a["stats"][k] == b["stats"][k], k
-    fx = f"{name}_96x54_strict.npz" if name != "car_boxed" else None
-    if fx:
-        ref = np.load(os.path.join(GOLD, fx))
-        assert same_bits(b["rgb"], ref["rgb"])
-    # a frame batch (three cameras, XCD-aware dealing of (frame, tile) items) through the three kernels
-    import torch
-    W, H = 96, 54
-    cams = [host.camera(W, H), moved_camera(W, H, 0.25, 0.0), moved_camera(W, H, -0.4, 0.3)]
-    bat = {}
-    for v in ("persist4", "split"):
-        r = dev.Renderer(0, counters=True)
-        r.upload(s)
-        rgb = torch.full((3, H, W, 3), -1.0, dtype=torch.float32, device="cuda")
-        hit = torch.full((3, H, W), -7, dtype=torch.int32, device="cuda")
-        bg = torch.zeros((3, H, W), dtype=torch.int32, device="cuda")
-        r.render_frames(cams, W, H, kernel=v, rgb=rgb, hit=hit, bgra=bg)
-        r.sync()
-        bat[v] = (rgb.cpu().numpy(), hit.cpu().numpy(), bg.cpu().numpy(), r.stats())
-        r.close()
-    a, b = bat["persist4"], bat["split"]
-    assert same_bits(a[0], b[0]) and same_bits(b[0][0], outs["split"]["rgb"])
-    np.testing.assert_array_equal(a[1], b[1])
-    np.testing.assert_array_equal(a[2], b[2])
-    for k in ("primary", "reflection", "shadow", "shadow_skipped", "hits", "pixels"):
-        assert a[3][k] == b[3][k], k
-
-
-@pytest.mark.parametrize("name,n_cand", [("sportscar", 7), ("car_boxed", 7), ("dragon", 7)])
+@pytest.mark.parametrize("name,n_cand", [("sportscar", 6), ("car_boxed", 7), ("dragon", 7)])
 def test_autotuned_frames_equal_forced_configuration(dev, name, n_cand, monkeypatch, capfd):
     """rt_render's launch autotuner (rt_frame.tune = 1, rt_hip.hip): the trial frame (every candidate, each
     TUNE_REPS times, into the same outputs) and the frames after the decision are bit-exact to a forced
@@ -471,7 +434,7 @@ def moved_camera(W, H, dx, dz):
     return c
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "strict", "split", "shpool"])
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "strict", "shpool"])
 @pytest.mark.parametrize("name", ["car_boxed", "dragon"])
 def test_frame_batch_equals_single_frames(dev, name, kernel):
     """rt_render_frames: a batch of frames (different cameras, one persistent launch on the fast paths)
@@ -560,7 +523,7 @@ def quantise(rgb):
     return q[..., 2] | (q[..., 1] << 8) | (q[..., 0] << 16) | np.uint32(255 << 24)
 
 
-@pytest.mark.parametrize("kernel", KERNELS + ["split"])
+@pytest.mark.parametrize("kernel", KERNELS)
 def test_bgra_output_is_the_bmp_writers_quantisation(dev, scenes, kernel):
     """rt_outputs.bgra (the kernels quantise as they store): equal to vec_to_bgra of the same
     frame's f32 pixels, with or without an rgb output, for a frame, a row-block subset and a frame batch;
@@ -598,13 +561,13 @@ def test_bgra_output_is_the_bmp_writers_quantisation(dev, scenes, kernel):
 
 @pytest.mark.parametrize("name", ["dragon", "car_boxed"])
 def test_path_level_placements_render_the_same_frames(dev, name):
-    """path levels in registers (k_persist, 3 waves/SIMD; k_pool), in the LDS path buffer (k_persist at 4 waves/
-    SIMD): the same bits for a frame, a frame batch with a moved camera and 4 spp, with the same ray counts"""
+    """path levels in registers (k_persist, 3 waves/SIMD), in the LDS path buffer (k_persist at 4 waves/SIMD, and the
+    shadow pool's hand-off slots): the same bits for a frame, a frame batch with a moved camera and 4 spp, with the same ray counts"""
     import torch
     s = host.Scene.named(name).build_bvh(3)
     W, H = 200, 120
     outs = {}
-    for v in ("persist", "persist4", "pool"):
+    for v in ("persist", "persist4", "shpool"):
         a = render(dev, s, W, H, v, counters=True)
         b = render(dev, s, W, H, v, spp=4)
         r = dev.Renderer(0)
@@ -617,7 +580,7 @@ def test_path_level_placements_render_the_same_frames(dev, name):
         r.close()
     a0, b0, f0 = outs["persist"]
     assert same_bits(f0[0], a0["rgb"]) and same_bits(f0[2], a0["rgb"])
-    for v in ("persist4", "pool"):
+    for v in ("persist4", "shpool"):
         a1, b1, f1 = outs[v]
         assert same_bits(a0["rgb"], a1["rgb"]) and same_bits(b0["rgb"], b1["rgb"]) and same_bits(f0, f1), v
         np.testing.assert_array_equal(a0["hit"], a1["hit"])

@@ -15,7 +15,7 @@ scene = sys.argv[1] if len(sys.argv) > 1 else "dragon"
 W, H = 1920, 1080
 s = host.Scene.named(scene).build_bvh(3)
 out = {}
-for k in sys.argv[2:] or ["fast", "persist4", "pool", "strict"]:
+for k in sys.argv[2:] or ["fast", "persist4", "shpool", "strict"]:
     r = device.Renderer(0, counters=True)
     r.upload(s)
     rgb = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")

@@ -26,8 +26,8 @@ for s in "${@:-smoke pytest bench}"; do
       bench)  run bench 600 python bench.py --steps 20 --warmup 5 ;;
       benchq) run bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
       prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
-      ab)     run ab 600 python tools/ab_variants.py persist persist4 pool coop4 fan ;;
-      abcar)  run abcar 600 python tools/ab_variants.py --scene car_boxed persist persist4 pool coop4 fan ;;
+      ab)     run ab 600 python tools/ab_variants.py persist persist4 shpool coop4 fan ;;
+      abcar)  run abcar 600 python tools/ab_variants.py --scene car_boxed persist persist4 shpool coop4 fan ;;
       ranks)  run ranks 300 python tools/rank_rows.py
               run ranks_car 300 python tools/rank_rows.py --scene car_boxed ;;
       *) echo "unknown step $step"; exit 2 ;;

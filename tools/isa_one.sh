@@ -1,0 +1,24 @@
+#!/bin/bash
+# VGPR / scratch of single k_persist instantiations, fast: a device-only compile of a translation unit that
+# instantiates only the kernels named on the command line (template argument lists of rtd::k_persist), e.g.
+#   tools/isa_one.sh "4,false,false,true,4,false,true,2,true,true,true"
+# Prints vgpr / scratch / lds / sgpr per kernel and leaves the assembly in /tmp/isa/one.s (no GPU needed).
+cd "$(dirname "$0")/.."
+mkdir -p /tmp/isa
+{
+  echo '#include "rt_kernels.hpp"'
+  echo '#include "rt_shpool.hpp"'
+  for a in "$@"; do echo "template __global__ void rtd::k_persist<$a>(rtd::KArgs);"; done
+} > /tmp/isa/one.hip
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
+    -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -Iparallel-ray-tracer_amd/csrc/hip \
+    --cuda-device-only -S -o /tmp/isa/one.s /tmp/isa/one.hip || exit 1
+python3 - <<'PY'
+import re
+s = open('/tmp/isa/one.s').read()
+for b in s.split('.amdhsa_kernel ')[1:]:
+    name = b.split('\n')[0]
+    g = lambda k: re.search(k + r'\s+(\d+)', b).group(1)
+    print(f"{name[:80]:80s} vgpr {g(r'.amdhsa_next_free_vgpr'):>4} sgpr {g(r'.amdhsa_next_free_sgpr'):>4} "
+          f"scratch {g(r'.amdhsa_private_segment_fixed_size'):>4} lds {g(r'.amdhsa_group_segment_fixed_size'):>6}")
+PY
