@@ -237,6 +237,9 @@ def main():
     ap.add_argument("--no-single-thread", action="store_true", help="skip the 1-thread CPU baseline sample")
     ap.add_argument("--kernel", default="fast")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the single-frame latency measurement (tools/profile.sh: the profiled launches are then "
+                         "only the batches, whose kernel is the same instantiation as a single frame's)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the CPU baseline (default 16, the GPU box's CPU share; also timed at every "
                          "host CPU, the line's cpu_baseline.all_cpus)")
@@ -247,7 +250,8 @@ def main():
                     "(bmp_write_file's bytes; from the device-quantised pixels with --output bgra8)")
     ap.add_argument("--gather", choices=("auto", "native", "torch"), default="auto",
                     help="N > 1: how frames reach rank 0 — native: the library's RCCL gather (rt_comm_init_rank / "
-                         "rt_comm_gather, one communicator per context; torch.distributed only hands out the ids); "
+                         "rt_comm_gather_from, one communicator per rank shared by its contexts; torch.distributed only hands out "
+                         "the id); "
                          "torch: torch.distributed.gather of the compact blocks (prt.dist.FrameGather); auto: native "
                          "on RCCL, torch on gloo (the one-GPU rehearsal: RCCL refuses two ranks on one device)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -339,8 +343,8 @@ def main():
     gmode = ("native" if args.gather == "native" else "none") if world == 1 else \
         (args.gather if args.gather != "auto" else ("native" if backend == "nccl" else "torch"))
     gather_note = {"none": "single GPU", "torch": "torch.distributed.gather of the compact row blocks (prt.dist."
-                   "FrameGather)", "native": "rt_comm_gather (the library's RCCL send/recv group, one communicator per "
-                   "context; prt.dist.NativeGather)"}[gmode]
+                   "FrameGather)", "native": "rt_comm_gather_from (the library's RCCL send/recv group, one communicator per rank "
+                   "shared by its contexts, row sets exchanged once per layout; prt.dist.NativeGather)"}[gmode]
     ng = None
     if gmode == "native":
         err = ""
@@ -391,14 +395,22 @@ def main():
                 if fg.pending(b):
                     fg.finish(b)
 
-    # setup, like the upload: with --tune the first launch of a scene and batch shape is rt_render's
-    # launch-autotuning launch (every candidate configuration timed, rt_hip.hip) and the next launch of
-    # that shape reads the timings; each batch size of the plan goes through that here (without --tune
-    # these are plain warm-up launches), then `warmup` frames run untimed.
+    # setup, like the upload: the library's default rule measures its candidates on the first launches of a shape
+    # (PERSIST4 vs the shadow pool, rt_get_launch_info: trial / settled; with --tune the autotuner's trial launch), so
+    # each batch size of the plan runs here until every context has settled, then `warmup` frames run untimed.
     rays_of = {}  # this rank's rays of a launch of nf frames (the same camera path every launch: deterministic)
     for nf in sorted(set(plan)):
-        for _ in range(2 * n_streams):  # per context: the tuning launch, then the launch reading its timings
+        for i in range(32):
             launch(nf)
+            if i >= 2 * n_streams - 1:
+                torch.cuda.synchronize()
+                settled = [all(r.launch_info()["settled"] for r in rends)]
+                if dist:  # every rank stops together (the gathers are collective), once all have settled
+                    every = [None] * world
+                    dist.all_gather_object(every, settled[0])
+                    settled = [all(every)]
+                if settled[0]:
+                    break
         rays_of[nf] = rends[(launch_no[0] - 1) % n_streams].stats()["rays"]
     if gmode == "native":  # untimed check of the native gather: rank 0's gathered frames == one GPU's frames
         drain()
@@ -455,6 +467,7 @@ def main():
     # frame, the frames' totals do not)
     assert rends[timed[-1][0]].stats()["rays"] == rays_of[plan[-1]]  # (deterministic: the same launch, again)
     rays_local = sum(rays_of[nf] for nf in plan)
+    timed_launch = rends[timed[-1][0]].launch_info()  # what the timed launches ran (the rule's choice)
     if args.bmp and rank == 0:  # the BMP written from the root rank (untimed): frame 0 = the reference camera
         frames = ng.frames_of(latest[2]) if gmode == "native" else (fg.frame if world > 1 else fg.target(latest[0]))
         px = (frames if frames.dim() == 3 else frames[0]).cpu().numpy()
@@ -474,7 +487,8 @@ def main():
     rc = device.Renderer(local, counters=True, stream=stream)
     rc.upload(scene, accel=args.accel, ploc_radius=args.ploc_radius)
     rc.render_frames(path(F), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
-                     kernel=args.kernel, variant=args.variant, **out(fg.target(0)))
+                     kernel=args.kernel, variant=timed_launch["variant"] if args.kernel != "strict" else args.variant,
+                     **out(fg.target(0)))
     stc = rc.stats()
     rc.close()
     bytes_launch = alg_bytes(stc, F * W * n_r, len(scene.lights), 4 if bgra else 12)
@@ -510,9 +524,10 @@ def main():
         c.pos.x += i * args.orbit
         c.ul.x += i * args.orbit
         return c
-    lat_default, settle_frames, seam_info = seam(lambda i: cam)
-    lat_walk, settle_walk, _ = seam(walk)
-    lat_tuned, _, _ = seam(lambda i: cam, tune=True)
+    nan = float("nan")
+    lat_default, settle_frames, seam_info = seam(lambda i: cam) if not args.no_latency else (nan, None, None)
+    lat_walk, settle_walk, _ = seam(walk) if not args.no_latency else (nan, None, None)
+    lat_tuned, _, _ = seam(lambda i: cam, tune=True) if not args.no_latency else (nan, None, None)
     lat = torch.tensor([lat_default], dtype=torch.float64, device="cuda")
     if dist:
         dist.all_reduce(lat, op=dist.ReduceOp.MAX)
@@ -565,9 +580,11 @@ def main():
                        "width": W, "height": H, "bvh": args.bvh, "accel": args.accel, "kernel": args.kernel,
                        "rays_per_frame": rays_frame, "output": args.output, "parallelism": f"{B}-row blocks cyclic x{world} + RCCL gather"
                        if world > 1 else "single GPU", "frames_per_launch": F, "gather": gather_note,
-                       "accel_built": info["accel_built"], "accel_build_ms": info["build_ms"],
+                       # the native gather's communicator over the whole run: gathers, row-set exchanges (1 per layout)
+                       "gather_comm": ng.info() if ng else None,
+                       "launch": timed_launch, "accel_built": info["accel_built"], "accel_build_ms": info["build_ms"],
                        "wide_depth": info["wide_depth"]},
-            "frame_latency_ms": lat.item(),
+            "frame_latency_ms": lat.item() if not args.no_latency else None,
             "frame_latency_detail": {"default_rule_ms": lat_default, "walkthrough_ms": lat_walk, "tuned_ms": lat_tuned,
                                      "settle_frames": settle_frames, "settle_frames_walkthrough": settle_walk,
                                      "choice": seam_info,
@@ -603,7 +620,13 @@ def main():
                                      # wave steps by active lanes 1-16 / 17-32 / 33-48 / 49-64 (fractions)
                                      "wave_steps_by_active_lanes": [stc[k] / max(1, stc["wave_steps"]) for k in (
                                          "steps_lanes_16", "steps_lanes_32", "steps_lanes_48", "steps_lanes_64")],
-                                     "strict_fallbacks": stc["fallbacks"]},
+                                     "strict_fallbacks": stc["fallbacks"],
+                                     # the same wave steps by walk kind x bounce level (0, 1, 2, 3+) x active lanes
+                                     # (1-16, 17-32, 33-48, 49-64), each a fraction of all the launch's wave steps
+                                     "wave_steps_by_kind_level": {
+                                         kind: [[round(v / max(1, stc["wave_steps"]), 5) for v in lv]
+                                                for lv in stc["steps_hist"][k]]
+                                         for k, kind in enumerate(("closest", "shadow"))}},
                          # measured by rocprofv3 PMC passes of this command (profiles/pmc_traffic.json)
                          "hbm_frac_measured": (traffic / (k_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
                          "traffic_over_pixels": (traffic / (F * W * n_r * (4 if bgra else 12))) if traffic else None,

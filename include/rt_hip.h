@@ -96,10 +96,11 @@ enum {
 
 /* rt_frame.variant: launch configuration of RT_KERNEL_FAST */
 enum {
-    RT_VARIANT_DEFAULT = 0,  /* the library's rule: frame batches and spp > 1 run RT_VARIANT_SHPOOL when the scene has 2+
-                                lights and the shadow pool's LDS path buffer fits, else RT_VARIANT_PERSIST4; single 1-spp
-                                frames run RT_VARIANT_HYBRID (RT_VARIANT_PERSIST where it cannot run); with rt_frame.tune
-                                = 1 the measured fastest candidate instead */
+    RT_VARIANT_DEFAULT = 0,  /* the library's rule, measured per frame shape: frame batches and spp > 1 try
+                                RT_VARIANT_PERSIST4, RT_VARIANT_SHPOOL and (1 spp) RT_VARIANT_STREAM on their first
+                                launches and keep the fastest (RT_VARIANT_PERSIST4 where the pool's LDS path buffer does
+                                not fit); single 1-spp frames run RT_VARIANT_HYBRID (RT_VARIANT_PERSIST where it cannot
+                                run); with rt_frame.tune = 1 the autotuner's candidates instead (rt_get_launch_info) */
     RT_VARIANT_PERSIST = 1,  /* k_persist: one lane per pixel path, walks in lockstep, 3 waves per SIMD */
     RT_VARIANT_PERSIST4 = 2, /* k_persist at 4 waves per SIMD (path levels in LDS) */
     /* 3: the split pipeline (closest chains / shadow batches / resolve), measured slower, removed in round 4: refused */
@@ -117,10 +118,14 @@ enum {
                                 camera. Nothing waits on the host: measurements and trials are read by event queries
                                 (rt_frame.hot_pct > 0: that threshold and rt_frame.hot_kernel, no trials) */
     /* 12: k_relay (1 + lights waves per tile, LDS hand-off), measured slower, removed in round 4: refused */
-    RT_VARIANT_SHPOOL = 13   /* k_persist at 4 waves per SIMD with each bounce level's shadow rays (every pixel's, every
+    RT_VARIANT_SHPOOL = 13,  /* k_persist at 4 waves per SIMD with each bounce level's shadow rays (every pixel's, every
                                 light's) walked as ONE per-wave pool: a lane whose walk ends takes the next unassigned ray,
                                 lanes of ended paths included (rt_frame.regroup = idle lanes per refill; 1..32 lights; the
                                 LDS path buffer must fit 4 workgroups per CU, else RT_VARIANT_PERSIST4 runs) */
+    RT_VARIANT_STREAM = 14   /* k_stream (1 spp): a lane whose path ends stores its pixel and takes the next pixel of its
+                                wave's tile (the wave takes its next tile when the current one has none left), so every
+                                round of closest walks, pooled shadow rays and shading runs with the wave's lanes busy;
+                                RT_VARIANT_SHPOOL's conditions, else as RT_VARIANT_SHPOOL */
 };
 
 /* rt_frame.hot_kernel: the kernel RT_VARIANT_HYBRID sends the hot tiles to when rt_frame.hot_pct > 0 */
@@ -205,6 +210,9 @@ typedef struct rt_stats {
     unsigned long long shadow_wave_steps; /* of which shadow walks' (k_persist's walks; RT_FLAG_COUNTERS)     */
     unsigned long long steps_lanes_16, steps_lanes_32, steps_lanes_48, steps_lanes_64; /* k_persist's wave steps
                                           with 1-16 / 17-32 / 33-48 / 49-64 active lanes (RT_FLAG_COUNTERS)  */
+    unsigned long long steps_hist[2][4][4]; /* k_persist's wave steps by walk kind (0 closest: primary + reflection,
+                                          1 shadow) x bounce level (0, 1, 2, 3 and deeper) x active lanes (1-16,
+                                          17-32, 33-48, 49-64) (RT_FLAG_COUNTERS)                               */
 } rt_stats;
 
 int rt_device_count(void);
@@ -263,20 +271,36 @@ int rt_gather_to(rt_ctx* const* ctxs, int n, int root, void* d_dst);
  *                        devices, rank i = ctxs[i] (one context per device);
  *   rt_comm_init_rank -- one rank per process (N processes, one GPU each): ncclCommInitRank with an id that
  *                        rank 0 made with rt_comm_get_id and handed to every rank (any channel: MPI, a file,
- *                        torch.distributed).
+ *                        torch.distributed). One communicator per rank serves every context of that rank on its
+ *                        device (rt_comm_gather_from).
  * rt_comm_gather(comm, root, d_dst): every rank's last render (a frame or frame batch, rgb or BGRA8; the row
  * sets must partition each frame, as for rt_gather) is sent to `root` with ncclSend / ncclRecv in one group,
  * on each context's stream (so after its render), and un-interleaved there into d_dst ([frames][height][width]
  * x 3 floats or x 1 uint32; a device pointer on the root's device) or, with d_dst NULL, into the root
- * context's own buffer, which then is its last render (rt_download / rt_download_bmp). Across processes the
- * ranks first exchange their row-set descriptors (one 64-B ncclAllGather). Collective: every rank calls it.
- * Asynchronous on the streams, except that exchange. Hit indices are not gathered (rt_gather does). */
+ * context's own buffer, which then is its last render (rt_download / rt_download_bmp). Collective: every rank
+ * calls it. Asynchronous on the streams. Hit indices are not gathered (rt_gather does).
+ * Across processes the ranks exchange their 64-B row-set descriptors (one ncclAllGather, a host wait) only when
+ * a rank's own part changes -- the first gather, and a new frame shape or row set, which changes every rank's
+ * part at once -- and the root checks that exchange's layout partitions each frame and, on the layout's first
+ * gather, that every pixel of the gathered frames arrived (one host wait per layout); later gathers of the same
+ * layout neither exchange nor wait. */
 typedef struct rt_comm rt_comm;
 #define RT_COMM_ID_BYTES 128 /* sizeof(ncclUniqueId) */
+typedef struct rt_comm_info {
+    long long gathers;   /* rt_comm_gather / rt_comm_gather_from calls */
+    long long exchanges; /* row-set descriptor exchanges (multi-process): one per layout */
+    long long checked;   /* layouts whose first gather the root checked pixel by pixel */
+    int nranks, rank;    /* the job's ranks; this communicator's (first local) rank */
+} rt_comm_info;
 int rt_comm_get_id(unsigned char* id /* RT_COMM_ID_BYTES */);
 int rt_comm_init(rt_ctx* const* ctxs, int n, rt_comm** out);
 int rt_comm_init_rank(rt_ctx* ctx, int nranks, int rank, const unsigned char* id, rt_comm** out);
 int rt_comm_gather(rt_comm* comm, int root, void* d_dst);
+/* rt_comm_gather of the last render of `src`, a context of this rank on the communicator's device (NULL: the
+ * context the communicator was built with); multi-process communicators only. Successive gathers of one
+ * communicator run in their call order, whatever streams their contexts use. */
+int rt_comm_gather_from(rt_comm* comm, rt_ctx* src, int root, void* d_dst);
+int rt_comm_get_info(rt_comm* comm, rt_comm_info* info);
 const char* rt_comm_last_error(rt_comm* comm);
 void rt_comm_destroy(rt_comm* comm);
 /* bmp_write_file's bytes of the last frame (cpu/src/bmp_writer.c:88-211): 54-B header + BGRA8 rows

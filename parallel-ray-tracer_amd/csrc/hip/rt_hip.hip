@@ -21,6 +21,7 @@
 #include "rt_host.h"
 #include "rt_kernels.hpp"
 #include "rt_shpool.hpp"
+#include "rt_stream.hpp"
 #include "rt_coop.hpp"
 #include "rt_fan.hpp"
 #include "rt_output.hpp"
@@ -137,6 +138,16 @@ struct rt_ctx {
         float ms[TUNE_MAX] = {};
         hipEvent_t e0[TUNE_MAX * TUNE_REPS] = {}, e1[TUNE_MAX * TUNE_REPS] = {};
     };
+    // the default rule of frame batches and spp > 1 (PERSIST4 or SHPOOL), measured per shape (render_batch)
+    struct BatchRule {
+        long long scene = -1;
+        int W = 0, rows = 0, off = 0, stride = 0, block = 0, shift = 0, bounces = 0, spp = 0, frames = 0, dealing = 0,
+            cap_req = 0;
+        static constexpr int ROUNDS = 2;
+        long long launch[3][ROUNDS] = {{-1, -1}, {-1, -1}, {-1, -1}};
+        int choice = -1;
+    };
+    std::vector<BatchRule> brules;
     // one tuning state per (scene upload, frame shape: width, rows, their offset / stride / block / shift,
     // bounces, spp, frames, dealing, waves cap): a context that alternates frame shapes keeps every decision
     std::vector<Tune> tunes;
@@ -181,7 +192,8 @@ namespace {
 struct HotCand {
     int pct, lanes, cold;
 };
-constexpr HotCand HYBRID_CANDS[] = {{0, 0, RT_VARIANT_PERSIST}, {0, 0, RT_VARIANT_SHPOOL},   {45, 4, RT_VARIANT_PERSIST},
+constexpr HotCand HYBRID_CANDS[] = {{0, 0, RT_VARIANT_PERSIST}, {0, 0, RT_VARIANT_SHPOOL},   {0, 0, RT_VARIANT_STREAM},
+                                    {45, 4, RT_VARIANT_PERSIST},
                                     {60, 4, RT_VARIANT_PERSIST}, {75, 4, RT_VARIANT_PERSIST}, {60, 2, RT_VARIANT_PERSIST},
                                     {75, 2, RT_VARIANT_PERSIST}, {60, 4, RT_VARIANT_SHPOOL},  {75, 2, RT_VARIANT_SHPOOL}};
 // pixel tile of a group kernel (rtd::GTile): k_coop<2> / k_fan<2> 8x4, k_coop<4> / k_fan<4> 4x4, k_fan<8> 4x2
@@ -199,6 +211,7 @@ const char* variant_name(int v) {
         case RT_VARIANT_FAN: return "fan";
         case RT_VARIANT_HYBRID: return "hybrid";
         case RT_VARIANT_SHPOOL: return "shpool";
+        case RT_VARIANT_STREAM: return "stream";
         default: return "default";
     }
 }
@@ -935,6 +948,8 @@ bool pbl_fits(const rtd::KArgs& A, int device) {
 //                        when 4 workgroups of that fit a CU, else a global slab;
 //   RT_VARIANT_SHPOOL    PERSIST4 with each bounce level's shadow rays walked as a per-wave pool (rt_shpool.hpp);
 //                        PERSIST4 where the LDS path buffer does not fit;
+//   RT_VARIANT_STREAM    k_stream (rt_stream.hpp): a lane takes the next pixel of its wave's tile when its path ends;
+//                        1 spp with the LDS path buffer, else SHPOOL's rule;
 // a tile trace (A.tile_trace: the hybrid launch's measuring frame, PRT_TILE_TRACE) runs the 3-wave build with
 // per-tile timestamps.
 template <int MAXB>
@@ -942,11 +957,15 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
     dyn = 0;
     if (A.tile_trace)
         return count ? rtd::k_persist<MAXB, false, true, true, 3, true, true> : rtd::k_persist<MAXB, false, false, true, 3, true, true>;
-    if (variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL) {
+    if (variant == RT_VARIANT_STREAM && A.spp <= 1 && pbl_fits<MAXB>(A, device)) {
+        dyn = pbl_bytes<MAXB>(A);
+        return count ? rtd::k_stream<MAXB, true> : rtd::k_stream<MAXB, false>;
+    }
+    if (variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_STREAM) {
         const bool pbl = pbl_fits<MAXB>(A, device);
         if (pbl) dyn = pbl_bytes<MAXB>(A);
         // (the bench's batches: the spp = 1 build)
-        return variant == RT_VARIANT_SHPOOL && pbl ? persist4<MAXB, true>(true, A.spp <= 1, count)
+        return variant != RT_VARIANT_PERSIST4 && pbl ? persist4<MAXB, true>(true, A.spp <= 1, count)
                                                    : persist4<MAXB, false>(pbl, A.spp <= 1, count);
     }
     return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true> : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
@@ -990,16 +1009,25 @@ int launch_group(const rtd::KArgs& A, bool fan, int g, bool count, int device, h
 }  // namespace
 
 namespace {
-// Centre-out order of a tx x ty tile grid (the persistent kernels' default dealing order)
+// Centre-out order of a tx x ty tile grid (the persistent kernels' default dealing order), by runs of SUPER tiles
+// side by side in a row: an 8x8 tile of 4-B pixels stores 32-B row pieces, so SUPER = 4 neighbouring tiles fill
+// whole 128-B lines, and dealt back to back they are written while the line is still in the XCD's L2 (a line
+// left partly written leaves L2 once per piece: WRITE_SIZE).
+constexpr int SUPER = 4;
 std::vector<int> centre_out(int tx, int ty) {
     const int n = tx * ty;
     std::vector<int> ord(n);
     for (int i = 0; i < n; i++) ord[i] = i;
     const float cx = 0.5f * tx, cy = 0.5f * ty;
+    auto d2 = [&](int t) {
+        const int x0 = (t % tx) / SUPER * SUPER, x1 = std::min(tx, x0 + SUPER);
+        const float dx = 0.5f * (x0 + x1) - cx, dy = t / tx + 0.5f - cy;
+        return dx * dx + dy * dy;
+    };
     std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
-        const float ax = a % tx + 0.5f - cx, ay = a / tx + 0.5f - cy;
-        const float bx = b % tx + 0.5f - cx, by = b / tx + 0.5f - cy;
-        return ax * ax + ay * ay < bx * bx + by * by;
+        const float da = d2(a), db = d2(b);
+        if (da != db) return da < db;
+        return a / tx != b / tx ? a / tx < b / tx : a < b;  // a run's tiles together, left to right
     });
     return ord;
 }
@@ -1093,7 +1121,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     const bool known = f->variant == RT_VARIANT_DEFAULT || f->variant == RT_VARIANT_PERSIST ||
                        f->variant == RT_VARIANT_PERSIST4 || f->variant == RT_VARIANT_COOP2 ||
                        f->variant == RT_VARIANT_COOP4 || f->variant == RT_VARIANT_FAN ||
-                       f->variant == RT_VARIANT_HYBRID || f->variant == RT_VARIANT_SHPOOL;
+                       f->variant == RT_VARIANT_HYBRID || f->variant == RT_VARIANT_SHPOOL ||
+                       f->variant == RT_VARIANT_STREAM;
     if (!known || f->hot_pct < 0 || f->hot_pct > 100 || f->hot_kernel < RT_HOT_COOP4 || f->hot_kernel > RT_HOT_FAN ||
         f->tune < 0 || f->tune > 1 ||
         f->waves_cap < 0 || f->waves_cap > 8 || f->dealing < RT_DEAL_DEFAULT || f->dealing > RT_DEAL_ROW_MAJOR ||
@@ -1283,6 +1312,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         if (v == RT_VARIANT_FAN) return fan_ok;
         if (v == RT_VARIANT_COOP2 || v == RT_VARIANT_COOP4) return wide_ok;
         if (v == RT_VARIANT_SHPOOL) return shp_ok;
+        if (v == RT_VARIANT_STREAM) return shp_ok && f->spp == 1;
         if (v == RT_VARIANT_HYBRID) return wide_ok && n_frames == 1 && fs == 0 && f->spp == 1;
         return true;
     };
@@ -1295,7 +1325,9 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     int mode = f->variant;
     if (mode == RT_VARIANT_DEFAULT)
         mode = (n_frames > 1 || f->spp > 1) ? (pool_rule ? RT_VARIANT_SHPOOL : RT_VARIANT_PERSIST4) : RT_VARIANT_HYBRID;
-    if (mode == RT_VARIANT_SHPOOL && !shp_ok) mode = RT_VARIANT_PERSIST4;  // (no room for the pool: PERSIST4 itself)
+    if ((mode == RT_VARIANT_SHPOOL || mode == RT_VARIANT_STREAM) && !shp_ok)
+        mode = RT_VARIANT_PERSIST4;  // (no room for the pool: PERSIST4 itself)
+    if (mode == RT_VARIANT_STREAM && f->spp != 1) mode = RT_VARIANT_SHPOOL;
     if (!usable(mode)) mode = RT_VARIANT_PERSIST;  // (no wide view, or a diagnostics trace)
     // the whole-frame kernel of a single frame while the hybrid launch measures or tries its candidates
     const int single_rule = pool_rule ? RT_VARIANT_SHPOOL : RT_VARIANT_PERSIST;
@@ -1384,6 +1416,72 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     li.settled = 1;
     li.trial = trial || (Tp && tunable && Tp->choice < 0) ? 1 : 0;
     if (li.trial) li.settled = 0;
+    // The default rule for frame batches and spp > 1 where the shadow pool can run: measured, not guessed. Whether the
+    // pool pays depends on the scene (dragon 20-frame batches 0.708 -> 0.666 ms per frame; two_cars 4K 1.881 vs 1.917,
+    // car_boxed 0.868 vs 0.902), so the first launches of a shape try PERSIST4 and SHPOOL ROUNDS times each (their own
+    // HIP events, read by a query once the last has run) and the faster per frame renders from then on. A context with
+    // traversal counters never tries (the counters of a trial would be another kernel's): it keeps the static rule.
+    if (f->variant == RT_VARIANT_DEFAULT && !tunable && kernel == RT_KERNEL_FAST && !A.tile_trace && !count &&
+        (n_frames > 1 || f->spp > 1) && shp_ok) {
+        rt_ctx::BatchRule* br = nullptr;
+        for (auto& b : ctx->brules)
+            if (b.scene == ctx->scene_gen && b.W == f->width && b.rows == f->n_rows && b.off == f->row_offset &&
+                b.stride == f->row_stride && b.block == rb && b.shift == fs && b.bounces == f->bounces &&
+                b.spp == f->spp && b.frames == n_frames && b.dealing == f->dealing && b.cap_req == f->waves_cap)
+                br = &b;
+        if (!br) {
+            if (ctx->brules.size() >= 16) ctx->brules.erase(ctx->brules.begin());
+            ctx->brules.emplace_back();
+            br = &ctx->brules.back();
+            *br = rt_ctx::BatchRule{ctx->scene_gen, f->width, f->n_rows, f->row_offset, f->row_stride, rb, fs,
+                                     f->bounces, f->spp, n_frames, f->dealing, f->waves_cap};
+        }
+        rt_ctx::BatchRule& b = *br;
+        const int cand[3] = {RT_VARIANT_PERSIST4, RT_VARIANT_SHPOOL, RT_VARIANT_STREAM};
+        const int nc = usable(RT_VARIANT_STREAM) ? 3 : 2;
+        int pick = -1;
+        if (b.choice < 0) {
+            for (int r = 0; r < rt_ctx::BatchRule::ROUNDS && pick < 0; r++)
+                for (int c = 0; c < nc && pick < 0; c++)
+                    if (b.launch[c][r] < 0 || ctx->launches - b.launch[c][r] >= rt_ctx::NEV) {  // untried (or events reused)
+                        b.launch[c][r] = ctx->launches;
+                        pick = c;
+                    }
+            if (pick < 0) {  // every trial enqueued: decide once the last has run (a query, never a wait)
+                long long last = 0;
+                for (int c = 0; c < nc; c++)
+                    for (long long x : b.launch[c]) last = std::max(last, x);
+                const hipError_t q = hipEventQuery(ctx->ev1s[last % rt_ctx::NEV]);
+                if (q == hipSuccess) {
+                    float ms[3] = {1e30f, 1e30f, 1e30f};
+                    for (int c = 0; c < nc; c++)
+                        for (int r = 0; r < rt_ctx::BatchRule::ROUNDS; r++) {
+                            const int sl = (int)(b.launch[c][r] % rt_ctx::NEV);
+                            float t = 0.0f;
+                            HIPC(hipEventElapsedTime(&t, ctx->ev0s[sl], ctx->ev1s[sl]));
+                            ms[c] = std::min(ms[c], t);
+                        }
+                    b.choice = 0;
+                    for (int c = 1; c < nc; c++)
+                        if (ms[c] < ms[b.choice]) b.choice = c;
+                    if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1)
+                        std::fprintf(stderr, "[prt batch] %dx%d f%d spp%d: persist4 %.3f ms, shpool %.3f ms, stream %.3f ms -> %s\n",
+                                     f->width, f->n_rows, n_frames, f->spp, ms[0], ms[1], ms[2], variant_name(cand[b.choice]));
+                } else if (q != hipErrorNotReady) {
+                    return fail(ctx, q, "rt_render: batch rule trials");
+                } else {
+                    (void)hipGetLastError();  // not an error: the trials are still running
+                }
+            }
+        }
+        if (b.choice >= 0) {
+            mode = cand[b.choice];
+        } else {
+            mode = pick >= 0 ? cand[pick] : (pool_rule ? RT_VARIANT_SHPOOL : RT_VARIANT_PERSIST4);
+            li.trial = 1;
+            li.settled = 0;
+        }
+    }
     // RT_VARIANT_HYBRID: what this single frame runs. The state is keyed by the frame's SHAPE, not its camera (a
     // walkthrough moves it every frame). The first frame of a shape measures: k_persist with per-tile times, copied to
     // pinned host memory behind it. Once they have arrived (an event query, never a wait) the tile lists of every
@@ -2009,17 +2107,24 @@ extern "C" int rt_gather_to(rt_ctx* const* ctxs, int n, int root, void* d_dst) {
 
 // ---------------------------------------------------------------- RCCL communicator (rt_comm_*)
 struct rt_comm {
-    std::vector<rt_ctx*> ctxs;       // the local ranks: ranks rank0 .. rank0 + ctxs.size() - 1
+    std::vector<rt_ctx*> ctxs;  // rt_comm_init: the local ranks rank0 .. rank0 + n - 1; rt_comm_init_rank: this rank's
+    std::vector<int> devices;   // their devices
     std::vector<ncclComm_t> comms;
     int nranks = 0, rank0 = 0;
-    Part* d_desc = nullptr;  // multi-process: every rank's descriptor (ncclAllGather), on ctxs[0]'s device
+    bool multi = false;  // rt_comm_init_rank: one rank of a multi-process job (row sets exchanged over RCCL)
+    // multi-process: the layout -- every rank's descriptor as last exchanged (ncclAllGather), and this rank's part
+    // at that exchange. A gather exchanges again only when this rank's part differs from it (a new frame shape or row
+    // set; every rank's part changes with a layout, so the ranks exchange together).
+    std::vector<Part> layout;
+    Part mine{};
+    bool have_layout = false;
+    Part* d_desc = nullptr;  // every rank's descriptor (ncclAllGather) + this rank's staging slot, on its device
     Part* h_desc = nullptr;  // pinned
-    // multi-process: the descriptor exchange runs on its own stream, so the host waits for the exchange only,
-    // not for the render in flight on the context's stream; it starts after the previous gather's send/recv
-    // group (`done`) so that the communicator's operations run in one order on every rank
-    hipStream_t side = nullptr;
-    hipEvent_t done = nullptr;
+    unsigned long long* d_count = nullptr;  // the root's coverage check of a layout's first gather
+    hipStream_t side = nullptr;  // the exchange's stream: the host waits for the exchange only, not for renders
+    hipEvent_t done = nullptr;   // after the last send / recv group: the next operation on the communicator waits
     bool issued = false;
+    rt_comm_info info{};
     std::string err;
 };
 
@@ -2117,8 +2222,10 @@ extern "C" int rt_comm_init(rt_ctx* const* ctxs, int n, rt_comm** out) {
     }
     rt_comm* cm = new rt_comm;
     cm->ctxs.assign(ctxs, ctxs + n);
+    cm->devices = devs;
     cm->comms.resize(n);
     cm->nranks = n;
+    cm->info.nranks = n;
     const ncclResult_t r = rccl().CommInitAll(cm->comms.data(), n, devs.data());
     if (r != ncclSuccess) {
         comm_fail(cm, r, "ncclCommInitAll");
@@ -2139,9 +2246,13 @@ extern "C" int rt_comm_init_rank(rt_ctx* ctx, int nranks, int rank, const unsign
     HIPC(hipSetDevice(ctx->device));
     rt_comm* cm = new rt_comm;
     cm->ctxs = {ctx};
+    cm->devices = {ctx->device};
     cm->comms.resize(1);
     cm->nranks = nranks;
     cm->rank0 = rank;
+    cm->multi = true;
+    cm->info.nranks = nranks;
+    cm->info.rank = rank;
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
     ncclResult_t r = rccl().CommInitRank(&cm->comms[0], nranks, u, rank);
@@ -2152,6 +2263,7 @@ extern "C" int rt_comm_init_rank(rt_ctx* ctx, int nranks, int rank, const unsign
     }
     hipError_t e = hipMalloc((void**)&cm->d_desc, sizeof(Part) * (nranks + 1));
     if (e == hipSuccess) e = hipHostMalloc((void**)&cm->h_desc, sizeof(Part) * (nranks + 1));
+    if (e == hipSuccess) e = hipMalloc((void**)&cm->d_count, sizeof(unsigned long long));
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&cm->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&cm->done, hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -2163,39 +2275,113 @@ extern "C" int rt_comm_init_rank(rt_ctx* ctx, int nranks, int rank, const unsign
     return RT_OK;
 }
 
-extern "C" int rt_comm_gather(rt_comm* cm, int root, void* d_dst) {
-    if (!cm || root < 0 || root >= cm->nranks) return RT_E_ARG;
-    const int nl = (int)cm->ctxs.size();
-    // every rank's descriptor: at hand in one process, exchanged over RCCL (4 B x 16 per rank) otherwise. A rank
-    // whose context has not rendered still joins the exchange (with W = 0), so that every rank fails together
-    // in check_parts instead of the others waiting in the collective for it
-    std::vector<Part> ps(cm->nranks);
-    if (nl == cm->nranks) {
-        for (rt_ctx* c : cm->ctxs)
-            if (!c->rendered) return comm_arg(cm, "rt_comm_gather: a context has not rendered");
-        for (int i = 0; i < nl; i++) ps[i] = part_of(cm->ctxs[i]);
-    } else {
-        rt_ctx* ctx = cm->ctxs[0];
-        HIPC(hipSetDevice(ctx->device));
-        cm->h_desc[cm->nranks] = ctx->rendered ? part_of(ctx) : Part{};
+namespace {
+// The multi-process gather: `src` (a context of this rank on the communicator's device) sends its last render to
+// the root. One communicator serves every context of the rank (bench.py alternates two on two streams): each
+// gather's send / recv group runs on its source's stream (so after that render) and after the previous group on
+// the communicator (an event), so every rank runs the communicator's operations in one order.
+int comm_gather_multi(rt_comm* cm, rt_ctx* src, int root, void* d_dst) {
+    rt_ctx* ctx = src;
+    HIPC(hipSetDevice(ctx->device));
+    // this rank's part; a rank whose context has not rendered still takes part (W = 0), so that every rank fails
+    // together in check_parts instead of the others waiting in the collective for it
+    const Part mine = ctx->rendered ? part_of(ctx) : Part{};
+    const bool fresh = !cm->have_layout || std::memcmp(&mine, &cm->mine, sizeof mine) != 0;
+    if (fresh) {  // a new layout: exchange the 64-B descriptors (ncclAllGather) and check that they partition the frames
+        cm->h_desc[cm->nranks] = mine;
         if (cm->issued) HIPC(hipStreamWaitEvent(cm->side, cm->done, 0));
         HIPC(hipMemcpyAsync(cm->d_desc + cm->nranks, cm->h_desc + cm->nranks, sizeof(Part), hipMemcpyHostToDevice, cm->side));
         NCCLC(rccl().AllGather(cm->d_desc + cm->nranks, cm->d_desc, sizeof(Part) / 4, ncclInt32, cm->comms[0], cm->side));
         HIPC(hipMemcpyAsync(cm->h_desc, cm->d_desc, sizeof(Part) * cm->nranks, hipMemcpyDeviceToHost, cm->side));
         HIPC(hipStreamSynchronize(cm->side));
-        for (int i = 0; i < cm->nranks; i++) ps[i] = cm->h_desc[i];
+        cm->info.exchanges++;
+        cm->layout.assign(cm->h_desc, cm->h_desc + cm->nranks);
+        cm->have_layout = false;
+        const std::string why = check_parts(cm->layout);
+        if (!why.empty()) return comm_arg(cm, "rt_comm_gather: " + why);
+        cm->mine = mine;
+        cm->have_layout = true;
     }
+    const std::vector<Part>& ps = cm->layout;
+    const Part& a = ps[0];
+    const int words = a.words;
+    const bool is_root = cm->rank0 == root;
+    std::vector<size_t> at(cm->nranks, 0);
+    void* dst = nullptr;
+    int* dst_hit = nullptr;
+    if (is_root) {
+        size_t stage = 0;
+        for (int q = 0; q < cm->nranks; q++) {
+            at[q] = stage;
+            if (q != root) stage += part_px(ps[q]) * 4 * words;
+        }
+        int rc;
+        if (stage && (rc = grow(ctx, &ctx->d_stage, ctx->stage_cap, stage))) return rc;
+        if ((rc = full_target(ctx, a, d_dst, &dst, &dst_hit, false))) return rc;
+    }
+    if (cm->issued) HIPC(hipStreamWaitEvent(ctx->stream, cm->done, 0));
+    const size_t full_px = (size_t)a.frames * a.W * a.H;
+    if (is_root && fresh)  // coverage check of a layout's first gather: no render writes this value (k_count_unwritten)
+        HIPC(hipMemsetAsync(dst, words == 1 ? 0 : 0xFF, full_px * 4 * words, ctx->stream));
+    NCCLC(rccl().GroupStart());
+    if (!is_root) {
+        NCCLC(rccl().Send(payload_of(ctx), part_px(ps[cm->rank0]) * words, ncclUint32, root, cm->comms[0], ctx->stream));
+    } else {
+        for (int q = 0; q < cm->nranks; q++)
+            if (q != root)
+                NCCLC(rccl().Recv(ctx->d_stage + at[q], part_px(ps[q]) * words, ncclUint32, q, cm->comms[0], ctx->stream));
+    }
+    NCCLC(rccl().GroupEnd());
+    HIPC(hipEventRecord(cm->done, ctx->stream));
+    cm->issued = true;
+    cm->info.gathers++;
+    if (!is_root) return RT_OK;
+    int rc;
+    for (int q = 0; q < cm->nranks; q++) {
+        const void* s = q == root ? payload_of(ctx) : (const void*)(ctx->d_stage + at[q]);
+        if ((rc = unshuffle(ctx, s, dst, ps[q], words, ctx->stream))) return rc;
+    }
+    if ((rc = finish_gather(ctx, a, dst, dst_hit))) return rc;
+    if (fresh) {  // the layout's first gather, checked pixel by pixel on the root (once per layout: a host wait)
+        unsigned long long left = 0;
+        HIPC(hipMemsetAsync(cm->d_count, 0, sizeof left, ctx->stream));
+        const int grid = (int)std::max<size_t>(1, std::min<size_t>((full_px + 255) / 256, 4096));
+        rtd::k_count_unwritten<<<grid, 256, 0, ctx->stream>>>((const unsigned*)dst, full_px, words, cm->d_count);
+        HIPC(hipGetLastError());
+        HIPC(hipMemcpyAsync(&left, cm->d_count, sizeof left, hipMemcpyDeviceToHost, ctx->stream));
+        HIPC(hipStreamSynchronize(ctx->stream));
+        cm->info.checked++;
+        if (left)  // (the layout stays: every rank keeps the same view of it, so the next gathers stay matched)
+            return comm_arg(cm, "rt_comm_gather: the gathered frames miss " + std::to_string(left) + " pixels");
+    }
+    return RT_OK;
+}
+}  // namespace
+
+extern "C" int rt_comm_gather_from(rt_comm* cm, rt_ctx* src, int root, void* d_dst) {
+    if (!cm || root < 0 || root >= cm->nranks) return RT_E_ARG;
+    if (cm->multi) {
+        if (!src) src = cm->ctxs[0];
+        if (src->device != cm->ctxs[0]->device)
+            return comm_arg(cm, "rt_comm_gather_from: the context is not on the communicator's device");
+        return comm_gather_multi(cm, src, root, d_dst);
+    }
+    if (src && src != cm->ctxs[0]) return comm_arg(cm, "rt_comm_gather_from: a one-process communicator gathers its own contexts");
+    const int nl = (int)cm->ctxs.size();
+    // one process: every rank's descriptor at hand
+    std::vector<Part> ps(cm->nranks);
+    for (rt_ctx* c : cm->ctxs)
+        if (!c->rendered) return comm_arg(cm, "rt_comm_gather: a context has not rendered");
+    for (int i = 0; i < nl; i++) ps[i] = part_of(cm->ctxs[i]);
     const std::string why = check_parts(ps);
     if (!why.empty()) return comm_arg(cm, "rt_comm_gather: " + why);
     const Part& a = ps[0];
     const int words = a.words;
-    // the root (when it is local): a staging slot per peer, in rank order
-    const int lroot = root - cm->rank0;
-    rt_ctx* rctx = lroot >= 0 && lroot < nl ? cm->ctxs[lroot] : nullptr;
+    rt_ctx* rctx = cm->ctxs[root];
     std::vector<size_t> at(cm->nranks, 0);
     void* dst = nullptr;
     int* dst_hit = nullptr;
-    if (rctx) {
+    {
         rt_ctx* ctx = rctx;
         size_t stage = 0;
         for (int q = 0; q < cm->nranks; q++) {
@@ -2207,14 +2393,13 @@ extern "C" int rt_comm_gather(rt_comm* cm, int root, void* d_dst) {
         if (stage && (rc = grow(ctx, &ctx->d_stage, ctx->stage_cap, stage))) return rc;
         if ((rc = full_target(ctx, a, d_dst, &dst, &dst_hit, false))) return rc;
     }
-    // one group: every local non-root rank sends its compact frames (on its stream: after its render), the root
-    // receives every peer's into its staging slot
+    // one group: every non-root rank sends its compact frames (on its stream: after its render), the root receives
+    // every peer's into its staging slot
     NCCLC(rccl().GroupStart());
     for (int l = 0; l < nl; l++) {
-        const int r = cm->rank0 + l;
         rt_ctx* c = cm->ctxs[l];
-        if (r != root) {
-            NCCLC(rccl().Send(payload_of(c), part_px(ps[r]) * words, ncclUint32, root, cm->comms[l], c->stream));
+        if (l != root) {
+            NCCLC(rccl().Send(payload_of(c), part_px(ps[l]) * words, ncclUint32, root, cm->comms[l], c->stream));
         } else {
             for (int q = 0; q < cm->nranks; q++)
                 if (q != root)
@@ -2222,35 +2407,42 @@ extern "C" int rt_comm_gather(rt_comm* cm, int root, void* d_dst) {
         }
     }
     NCCLC(rccl().GroupEnd());
-    if (nl < cm->nranks) {  // the next descriptor exchange starts after this group (one order on every rank)
-        const hipError_t e = hipEventRecord(cm->done, cm->ctxs[0]->stream);
-        if (e != hipSuccess) return fail(cm->ctxs[0], e, "rt_comm_gather: hipEventRecord");
-        cm->issued = true;
-    }
-    if (!rctx) return RT_OK;
+    cm->info.gathers++;
     rt_ctx* ctx = rctx;
     HIPC(hipSetDevice(ctx->device));
     int rc;
     for (int q = 0; q < cm->nranks; q++) {
-        const void* src = q == root ? payload_of(ctx) : (const void*)(ctx->d_stage + at[q]);
-        if ((rc = unshuffle(ctx, src, dst, ps[q], words, ctx->stream))) return rc;
+        const void* s = q == root ? payload_of(ctx) : (const void*)(ctx->d_stage + at[q]);
+        if ((rc = unshuffle(ctx, s, dst, ps[q], words, ctx->stream))) return rc;
     }
     return finish_gather(ctx, a, dst, dst_hit);
+}
+
+extern "C" int rt_comm_gather(rt_comm* cm, int root, void* d_dst) { return rt_comm_gather_from(cm, nullptr, root, d_dst); }
+
+extern "C" int rt_comm_get_info(rt_comm* cm, rt_comm_info* info) {
+    if (!cm || !info) return RT_E_ARG;
+    *info = cm->info;
+    return RT_OK;
 }
 
 extern "C" const char* rt_comm_last_error(rt_comm* cm) { return cm ? cm->err.c_str() : "null communicator"; }
 
 extern "C" void rt_comm_destroy(rt_comm* cm) {
     if (!cm) return;
+    // (the contexts may be gone already: only the communicator's own devices, events and streams are touched)
+    if (cm->issued && cm->done) {  // the last send / recv group (any context's stream) has run
+        (void)hipSetDevice(cm->devices[0]);
+        (void)hipEventSynchronize(cm->done);
+    }
     for (size_t l = 0; l < cm->comms.size(); l++) {
-        if (cm->ctxs[l]) {
-            (void)hipSetDevice(cm->ctxs[l]->device);
-            (void)hipStreamSynchronize(cm->ctxs[l]->stream);
-        }
+        (void)hipSetDevice(cm->devices[l]);
+        if (!cm->multi) (void)hipDeviceSynchronize();  // (one process: the groups ran on the contexts' streams)
         if (cm->comms[l]) (void)rccl().CommDestroy(cm->comms[l]);
     }
     if (cm->side) (void)hipStreamSynchronize(cm->side);
     if (cm->d_desc) (void)hipFree(cm->d_desc);
+    if (cm->d_count) (void)hipFree(cm->d_count);
     if (cm->h_desc) (void)hipHostFree(cm->h_desc);
     if (cm->side) (void)hipStreamDestroy(cm->side);
     if (cm->done) (void)hipEventDestroy(cm->done);
@@ -2313,6 +2505,8 @@ extern "C" int rt_get_stats(rt_ctx* ctx, rt_stats* st) {
     st->steps_lanes_32 = c[rtd::C_Q2];
     st->steps_lanes_48 = c[rtd::C_Q3];
     st->steps_lanes_64 = c[rtd::C_Q4];
+    std::memcpy(st->steps_hist, c + rtd::C_HIST, sizeof st->steps_hist);
+    static_assert(sizeof st->steps_hist == 32 * sizeof(unsigned long long), "histogram slots");
     if (c[rtd::C_ERR]) {
         ctx->err = "traversal stack overflow: BVH deeper than 32 levels";
         return RT_E_STATE;

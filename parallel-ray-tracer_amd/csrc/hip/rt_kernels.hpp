@@ -37,12 +37,26 @@ enum {
     C_WS,  // wave-level wide-node steps (RT_FLAG_COUNTERS): lane visits / (64 x this) = SIMD efficiency
     C_WSH,  // of which shadow walks' (k_persist's walks, RT_FLAG_COUNTERS)
     C_Q1, C_Q2, C_Q3, C_Q4,  // wave steps with 1-16 / 17-32 / 33-48 / 49-64 active lanes (same)
-    NCOUNT = 21
+    NLANE = 21,              // the counters above: per lane, summed over the wave at the end (flush)
+    // k_persist's wave steps by walk kind (closest, shadow) x bounce level (0, 1, 2, 3+) x active lanes (1-16, 17-32,
+    // 33-48, 49-64): [kind][level][quarter], 32 slots added to by the wave's first active lane (RT_FLAG_COUNTERS)
+    C_HIST = NLANE,
+    NCOUNT = NLANE + 32
 };
 
 struct Ctr {
     unsigned prim, refl, shad, skip, hits, chi, chl, cht, shi, shl, sht, pix, err, fb, nb, ws, wsh, q1, q2, q3, q4;
+    unsigned lvl;    // the bounce level of the walks the lane runs (the histogram's level)
+    unsigned* hist;  // RT_FLAG_COUNTERS kernels that keep the histogram: the workgroup's 32 slots in LDS (hist_lds)
 };
+
+// The wave-step histogram of a counting k_persist workgroup (LDS atomics; the 32 slots go to counters + C_HIST at the
+// end). Instantiated only by the counting kernels, so the others' LDS budget is untouched.
+template <bool COUNT>
+__device__ __forceinline__ unsigned* hist_lds() {
+    __shared__ unsigned h[32];
+    return h;
+}
 
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
 #pragma unroll
@@ -53,10 +67,10 @@ __device__ __forceinline__ unsigned wave_sum(unsigned v) {
 template <bool COUNT>
 __device__ __forceinline__ void flush(const Ctr& c, unsigned long long* g) {
     const bool l0 = (threadIdx.x & 63) == 0;
-    unsigned v[NCOUNT] = {c.prim, c.refl, c.shad, c.skip, c.hits, c.chi, c.chl, c.cht, c.shi, c.shl, c.sht,
+    unsigned v[NLANE] = {c.prim, c.refl, c.shad, c.skip, c.hits, c.chi, c.chl, c.cht, c.shi, c.shl, c.sht,
                           c.pix,  c.err,  c.fb,   c.nb,   c.ws,   c.wsh, c.q1,  c.q2,  c.q3,  c.q4};
 #pragma unroll
-    for (int i = 0; i < NCOUNT; i++) {
+    for (int i = 0; i < NLANE; i++) {
         if (!COUNT && ((i >= C_CHI && i <= C_SHT) || i >= C_NB)) continue;
         unsigned s = wave_sum(v[i]);
         if (l0 && s) atomicAdd(g + i, (unsigned long long)s);
@@ -302,6 +316,7 @@ __device__ __forceinline__ void count_step(Ctr& c, bool shadow) {
     c.q2 += b == 1 ? f : 0u;
     c.q3 += b == 2 ? f : 0u;
     c.q4 += b == 3 ? f : 0u;
+    if (c.hist && f) atomicAdd(c.hist + (shadow ? 16u : 0u) + 4u * (c.lvl < 3u ? c.lvl : 3u) + b, 1u);
 }
 
 __device__ __forceinline__ float ubyte(unsigned w, int b) { return (float)((w >> (8 * b)) & 0xFFu); }
@@ -662,6 +677,7 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
     const v3 amb = mk(s.amb_x, s.amb_y, s.amb_z);
     float best;
     int nd;
+    if (COUNT) c.lvl = (unsigned)it;
     if (it == 0) c.prim++;
     else c.refl++;
     int orig;
@@ -997,6 +1013,11 @@ void k_persist(KArgs A) {
     }
     const int lane = threadIdx.x & 63;
     Ctr c = {};
+    if constexpr (COUNT) {
+        c.hist = hist_lds<true>();
+        if (threadIdx.x < 32) c.hist[threadIdx.x] = 0u;
+        __syncthreads();
+    }
     UCtrOf<SHP> u = {};  // SHP: the wave-uniform ray counts (rt_shpool.hpp)
     // frame batches: dealt item t = (tile t / n_frames of the dealing order, frame t % n_frames), so the
     // expensive (central) tiles of every frame of the batch start first
@@ -1028,6 +1049,10 @@ void k_persist(KArgs A) {
     }
     flush<COUNT>(c, A.counters);
     if constexpr (SHP) flush_u(u, A.counters);
+    if constexpr (COUNT) {  // every wave of the workgroup leaves the tile loop and reaches this point
+        __syncthreads();
+        if (threadIdx.x < 32 && c.hist[threadIdx.x]) atomicAdd(A.counters + C_HIST + threadIdx.x, (unsigned long long)c.hist[threadIdx.x]);
+    }
 }
 
 }  // namespace rtd

@@ -22,6 +22,19 @@ __global__ __launch_bounds__(256) void k_unshuffle_frames(const unsigned* __rest
     }
 }
 
+// Pixels of gathered frames that no rank's part wrote: the root fills the frames with a value no render writes
+// (BGRA8: alpha 0 -- vec_to_bgra always writes 255; f32: NaN -- every pixel is clamped to [0, 1]) before the first
+// gather of a layout, and counts what is left afterwards (rt_comm_gather's coverage check).
+__global__ __launch_bounds__(256) void k_count_unwritten(const unsigned* __restrict__ px, size_t n, int words,
+                                                         unsigned long long* __restrict__ count) {
+    unsigned c = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        if (words == 1) c += (px[i] >> 24) != 255u ? 1u : 0u;
+        else c += (px[3 * i] == 0xFFFFFFFFu || px[3 * i + 1] == 0xFFFFFFFFu || px[3 * i + 2] == 0xFFFFFFFFu) ? 1u : 0u;
+    }
+    if (c) atomicAdd(count, (unsigned long long)c);
+}
+
 // top-down BGRA8 rows -> the BMP file's bottom-up order (cpu/src/bmp_writer.c:131-143)
 __global__ __launch_bounds__(256) void k_flip_rows(const unsigned* __restrict__ in, unsigned* __restrict__ out, int W, int H) {
     const size_t n = (size_t)W * H;

@@ -74,7 +74,7 @@ class WbvhInfo(ctypes.Structure):
 
 
 class Stats(ctypes.Structure):
-    _fields_ = [(f, ctypes.c_ulonglong) for f in STAT_FIELDS]
+    _fields_ = [(f, ctypes.c_ulonglong) for f in STAT_FIELDS] + [("steps_hist", ctypes.c_ulonglong * 32)]
 
 
 class SceneInfo(ctypes.Structure):  # rt_scene_info
@@ -87,6 +87,11 @@ class SceneInfo(ctypes.Structure):  # rt_scene_info
 class LaunchInfo(ctypes.Structure):  # rt_launch_info
     _fields_ = [("variant", ctypes.c_int), ("hot_pct", ctypes.c_int), ("hot_lanes", ctypes.c_int),
                 ("cold_variant", ctypes.c_int), ("trial", ctypes.c_int), ("settled", ctypes.c_int)]
+
+
+class CommInfo(ctypes.Structure):  # rt_comm_info
+    _fields_ = [("gathers", ctypes.c_longlong), ("exchanges", ctypes.c_longlong), ("checked", ctypes.c_longlong),
+                ("nranks", ctypes.c_int), ("rank", ctypes.c_int)]
 
 
 _host = None
@@ -162,6 +167,8 @@ def hip():
         L.rt_comm_init_rank.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                         P(ctypes.c_void_p)]
         L.rt_comm_gather.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        L.rt_comm_gather_from.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        L.rt_comm_get_info.argtypes = [ctypes.c_void_p, P(CommInfo)]
         L.rt_comm_last_error.argtypes = [ctypes.c_void_p]
         L.rt_comm_last_error.restype = ctypes.c_char_p
         L.rt_comm_destroy.argtypes = [ctypes.c_void_p]

@@ -15,7 +15,8 @@ P = ctypes.POINTER
 KERNELS = {"auto": 0, "strict": 1, "fast": 2}
 # rt_frame.variant (launch configurations of the fast kernel, include/rt_hip.h); a variant name is also
 # accepted as `kernel` (kernel="coop4" == kernel="fast", variant="coop4")
-VARIANTS = {"default": 0, "persist": 1, "persist4": 2, "coop2": 4, "coop4": 5, "fan": 7, "hybrid": 11, "shpool": 13}
+VARIANTS = {"default": 0, "persist": 1, "persist4": 2, "coop2": 4, "coop4": 5, "fan": 7, "hybrid": 11, "shpool": 13,
+            "stream": 14}
 VARIANT_NAMES = {v: k for k, v in VARIANTS.items()}
 HOT_KERNELS = {"coop4": 0, "coop2": 1, "fan": 2}  # rt_frame.hot_kernel (RT_HOT_*)
 DEALING = {"default": 0, "global": 1, "rows": 2, "columns": 3, "blocks": 4, "row_major": 5}
@@ -109,21 +110,35 @@ class Comm:
             raise RtError(f"rt_comm_init: {rc} ({_L.rt_last_error(self._r[0]._ctx).decode()})")
         self.rank0 = 0 if rank is None else rank
 
-    def gather(self, root=0, out=None):
+    def gather(self, root=0, out=None, src=None):
         """rt_comm_gather: every rank's last render -> the root's full frames; `out` (root only): a contiguous
         device tensor [frames, H, W, 3] f32 or [frames, H, W] int32 (BGRA8), else the root Renderer's own
-        buffer (its download() / download_bmp() then read the full frame)."""
+        buffer (its download() / download_bmp() then read the full frame). src (multi-process communicators): the
+        Renderer of this rank whose last render to send (rt_comm_gather_from; default: the one it was built with)."""
         ptr = None
+        here = [src] if src is not None else self._r
         if out is not None:
-            ptr = ctypes.c_void_p(_gather_out(self._r[root - self.rank0] if 0 <= root - self.rank0 < len(self._r)
-                                              else self._r[0], out))
-        rc = _L.rt_comm_gather(self._c, root, ptr)
+            ptr = ctypes.c_void_p(_gather_out(here[root - self.rank0] if 0 <= root - self.rank0 < len(here)
+                                              else here[0], out))
+        if src is not None:
+            if all(src is not x for x in self._r):
+                self._r.append(src)  # (kept alive while the communicator may still use its stream)
+            rc = _L.rt_comm_gather_from(self._c, src._ctx, root, ptr)
+        else:
+            rc = _L.rt_comm_gather(self._c, root, ptr)
         if rc != 0:
             raise RtError(f"rt_comm_gather: {rc} ({_L.rt_comm_last_error(self._c).decode()})")
         lr = root - self.rank0
-        if 0 <= lr < len(self._r):
-            r = self._r[lr]
+        if 0 <= lr < len(here):
+            r = here[lr]
             r._last = r._size
+
+    def info(self):
+        """rt_comm_get_info: gathers, descriptor exchanges (one per layout), layouts checked pixel by pixel"""
+        i = _lib.CommInfo()
+        if _L.rt_comm_get_info(self._c, ctypes.byref(i)) != 0:
+            raise RtError("rt_comm_get_info failed")
+        return {f: getattr(i, f) for f, _ in _lib.CommInfo._fields_}
 
     def close(self):
         if self._c:
@@ -310,6 +325,9 @@ class Renderer:
         self._chk(_L.rt_get_stats(self._ctx, ctypes.byref(s)), "rt_get_stats")
         d = {f: getattr(s, f) for f in _lib.STAT_FIELDS}
         d["rays"] = d["primary"] + d["reflection"] + d["shadow"]
+        # wave steps [kind: closest, shadow][level 0, 1, 2, 3+][active lanes 1-16, 17-32, 33-48, 49-64]
+        h = list(s.steps_hist)
+        d["steps_hist"] = [[h[16 * k + 4 * l:16 * k + 4 * l + 4] for l in range(4)] for k in range(2)]
         return d
 
     def close(self):

@@ -192,8 +192,9 @@ class FrameGather:
 
 class NativeGather:
     """The N > 1 frame gather through the boundary's own RCCL code (include/rt_hip.h rt_comm_init_rank /
-    rt_comm_gather, replacing gpu/src/gpu.cu:203-228's load_from_gpu): one communicator per context (bench.py
-    alternates contexts on their own streams), torch.distributed only hands the RCCL ids out. Each context
+    rt_comm_gather_from, replacing gpu/src/gpu.cu:203-228's load_from_gpu): one communicator per rank, shared by its
+    contexts (bench.py alternates contexts on their own streams), torch.distributed only hands the RCCL id out; the
+    row-set descriptors are exchanged once per layout, and the layout's first gather is checked pixel by pixel. Each context
     renders its rows of a frame batch into target(c) (compact rows, as rt_render_frames writes them); gather(c),
     called on every rank right after that render, enqueues the send (or, on rank 0, the receives and the
     un-interleaving into frames(c)) on the context's stream, so the gather of one context's batch overlaps the
@@ -210,10 +211,12 @@ class NativeGather:
         self.blocks = [torch.zeros((frames, n, W, C), dtype=like.dtype, device=like.device) for _ in renderers]
         self.full = [torch.zeros((frames, H, W, C), dtype=like.dtype, device=like.device) for _ in renderers] \
             if rank == 0 else None
-        ids = [device.comm_id() for _ in renderers] if rank == 0 else [None] * len(renderers)
+        ids = [device.comm_id()] if rank == 0 else [None]
         if dist is not None:
             dist.broadcast_object_list(ids, src=0)
-        self.comms = [device.Comm([r], world, rank, uid) for r, uid in zip(renderers, ids)]
+        # one communicator for the rank, shared by its contexts (rt_comm_gather_from)
+        self.comm = device.Comm([renderers[0]], world, rank, ids[0])
+        self.renderers = list(renderers)
 
     def rows(self):
         r = rank_rows(self.H, self.rank, self.world, self.bk)
@@ -228,11 +231,13 @@ class NativeGather:
     def gather(self, c, nf=None):
         """collective (every rank, after context c's render of nf frames): its frames -> rank 0's frames_of(c)"""
         out = self.full[c][:nf or self.frames] if self.rank == 0 else None
-        self.comms[c].gather(root=0, out=out)
+        self.comm.gather(root=0, out=out, src=self.renderers[c])
 
     def frames_of(self, c):
         return self.full[c] if self.rank == 0 else None
 
+    def info(self):
+        return self.comm.info()
+
     def close(self):
-        for cm in self.comms:
-            cm.close()
+        self.comm.close()

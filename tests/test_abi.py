@@ -61,7 +61,8 @@ def test_ctypes_mirrors_match_the_c_layouts(tmp_path):
     structs = {"rt_opts": _lib.Opts, "rt_scene": _lib.SceneDesc, "rt_frame": _lib.Frame, "rt_stats": _lib.Stats,
                "rt_camera": _lib.Camera, "rt_triangle": _lib.Triangle, "rt_bvh_node": _lib.BvhNode,
                "rt_light": _lib.Light, "rth_rng": _lib.Rng, "rth_bvh_stats": _lib.BvhStats,
-               "rth_wbvh_info": _lib.WbvhInfo, "rt_scene_info": _lib.SceneInfo, "rt_launch_info": _lib.LaunchInfo}
+               "rth_wbvh_info": _lib.WbvhInfo, "rt_scene_info": _lib.SceneInfo, "rt_launch_info": _lib.LaunchInfo,
+               "rt_comm_info": _lib.CommInfo}
     if Outputs is not None:
         structs["rt_outputs"] = Outputs
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rt_hip.h"', '#include "rt_host.h"',

@@ -69,7 +69,7 @@ def test_rccl_gather_one_rank(dev, scene, kind, frames, ctor):
     r = dev.Renderer(0)
     r.upload(scene)
     comm = dev.Comm([r]) if ctor == "all" else dev.Comm([r], nranks=1, rank=0, uid=dev.comm_id())
-    rank_render(dev, scene, r, (0, 1, H), frames, kind)
+    keep = rank_render(dev, scene, r, (0, 1, H), frames, kind)  # (the render's output lives until the gather has run)
     out = torch.empty_like(ref, device="cuda")
     comm.gather(0, out)
     torch.cuda.synchronize()
@@ -80,6 +80,7 @@ def test_rccl_gather_one_rank(dev, scene, kind, frames, ctor):
         assert r.download_bmp() == want
     comm.close()
     r.close()
+    del keep
 
 
 @pytest.mark.parametrize("kind", ["rgb", "bgra"])
@@ -136,3 +137,51 @@ def test_cli_rccl_gather_writes_the_reference_bmp(tmp_path):
     assert r.returncode == 0, r.stderr
     assert "Frame gather: RCCL" in r.stdout
     assert out.read_bytes() == host.bmp_encode(ref["rgb"])
+
+
+@pytest.mark.parametrize("kind", ["rgb", "bgra"])
+def test_rccl_rank_comm_exchanges_once_per_layout(dev, scene, kind):
+    """rt_comm_init_rank's gather (the multi-process path, one rank here): the row-set descriptors are exchanged
+    once per layout -- 4 gathers of an unchanged layout, from two contexts sharing ONE communicator
+    (rt_comm_gather_from, as bench.py alternates them), exchange once -- and a new layout (a different frame count)
+    exchanges again; the root checks every layout's first gather pixel by pixel; every gather equals one GPU's frames"""
+    frames = 3
+    ref = full_frames(dev, scene, frames, kind)
+    rs = [dev.Renderer(0), dev.Renderer(0)]
+    for r in rs:
+        r.upload(scene)
+    comm = dev.Comm([rs[0]], nranks=1, rank=0, uid=dev.comm_id())
+    for g in range(4):
+        r = rs[g % 2]
+        keep = rank_render(dev, scene, r, (0, 1, H), frames, kind)
+        out = torch.zeros_like(ref, device="cuda")
+        torch.cuda.synchronize()
+        comm.gather(0, out, src=r)
+        r.sync()
+        assert torch.equal(out.cpu().view(torch.int32), ref.view(torch.int32)), g
+    info = comm.info()
+    assert info["gathers"] == 4 and info["exchanges"] == 1 and info["checked"] == 1, info
+    keep = rank_render(dev, scene, rs[1], (0, 1, H), 1, kind)  # a new layout: one frame
+    out = torch.zeros_like(ref[:1], device="cuda")
+    torch.cuda.synchronize()
+    comm.gather(0, out, src=rs[1])
+    rs[1].sync()
+    assert torch.equal(out.cpu().view(torch.int32), ref[:1].view(torch.int32))
+    info = comm.info()
+    assert info["gathers"] == 5 and info["exchanges"] == 2 and info["checked"] == 2, info
+    comm.close()
+    for r in rs:
+        r.close()
+
+
+def test_rccl_rank_comm_refuses_a_partial_layout(dev, scene):
+    """a layout whose row sets do not cover the frame (here: one rank rendering only half the rows) fails the
+    exchange's partition check instead of gathering a frame with holes"""
+    r = dev.Renderer(0)
+    r.upload(scene)
+    comm = dev.Comm([r], nranks=1, rank=0, uid=dev.comm_id())
+    keep = rank_render(dev, scene, r, (0, 2, (H + 1) // 2), 1, "bgra")
+    with pytest.raises(dev.RtError):
+        comm.gather(0, torch.zeros((1, H, W), dtype=torch.int32, device="cuda"), src=r)
+    comm.close()
+    r.close()

@@ -6,9 +6,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out && export TMP
 base=$1; shift
 for sc in ${@:-dragon car_boxed}; do
   for r in 1 2; do
-    timeout -k 10 300 env PRT_LIB_DIR="$PWD/$base" python tools/ab_variants.py --scene $sc --rounds 3 persist4 \
+    timeout -k 10 300 env PRT_LIB_DIR="$PWD/$base" python tools/ab_variants.py --scene $sc --rounds 3 ${V:-persist4} \
         > gpurun_out/ab_${sc}_base$r.log 2>&1 || exit $?
-    timeout -k 10 300 python tools/ab_variants.py --scene $sc --rounds 3 persist4 > gpurun_out/ab_${sc}_new$r.log 2>&1 || exit $?
+    timeout -k 10 300 python tools/ab_variants.py --scene $sc --rounds 3 ${V:-persist4} > gpurun_out/ab_${sc}_new$r.log 2>&1 || exit $?
   done
 done
 timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_build.py -m gpu -x -q --timeout 300 \

@@ -2,13 +2,20 @@
 # VGPR / scratch of single k_persist instantiations, fast: a device-only compile of a translation unit that
 # instantiates only the kernels named on the command line (template argument lists of rtd::k_persist), e.g.
 #   tools/isa_one.sh "4,false,false,true,4,false,true,2,true,true,true"
+# (an argument of the form name:args instantiates rtd::name<args> instead, e.g. k_stream:4,false)
 # Prints vgpr / scratch / lds / sgpr per kernel and leaves the assembly in /tmp/isa/one.s (no GPU needed).
 cd "$(dirname "$0")/.."
 mkdir -p /tmp/isa
 {
   echo '#include "rt_kernels.hpp"'
   echo '#include "rt_shpool.hpp"'
-  for a in "$@"; do echo "template __global__ void rtd::k_persist<$a>(rtd::KArgs);"; done
+  echo '#include "rt_stream.hpp"'
+  for a in "$@"; do
+    case $a in
+      *:*) echo "template __global__ void rtd::${a%%:*}<${a#*:}>(rtd::KArgs);" ;;
+      *) echo "template __global__ void rtd::k_persist<$a>(rtd::KArgs);" ;;
+    esac
+  done
 } > /tmp/isa/one.hip
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
     -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -Iparallel-ray-tracer_amd/csrc/hip \

@@ -13,6 +13,7 @@ per lane); WRITE_SIZE reads exactly for 16-B stores. Counters come from separate
 usage: tools/pmc_traffic.py gpurun_out/prof_<tag> <round-tag>
 """
 import csv
+import re
 import json
 import os
 import shutil
@@ -62,7 +63,9 @@ def main():
     os.makedirs(pdir, exist_ok=True)
     # kernel trace stats
     stats = rows(os.path.join(prof, "trace", "run_kernel_stats.csv"))
-    PROD = max(stats, key=lambda r: float(r["TotalDurationNs"]))["Name"]
+    # (the counting launch, RT_FLAG_COUNTERS, is a k_persist<MAXB, false, true, ...> instantiation: never the product)
+    PROD = max((r for r in stats if not re.search(r"k_persist<\d+, false, true,", r["Name"])),
+               key=lambda r: float(r["TotalDurationNs"]))["Name"]
     lines = [f"# rocprofv3 --kernel-trace --stats ({tag}, {key})", "",
              f"command: `rocprofv3 --kernel-trace --stats -- {cmd}` ({frames} frames per launch; librt_hip.so md5 "
              f"{lib_md5}); bench line: {line['value']:.0f} Mrays/s, HIP-event kernel {rf['kernel_ms']:.3f} ms per launch",

@@ -18,7 +18,7 @@ step() {  # name timeout cmd...
     echo "=== $name rc=$rc" | tee -a $out/session.log
     if [ $rc -ne 0 ]; then tail -20 $out/$name.log; exit $rc; fi
 }
-B="python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline $args"
+B="python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-latency $args"
 echo "$B" > $out/cmd.txt
 md5sum parallel-ray-tracer_amd/lib/librt_hip.so > $out/lib_md5.txt
 step trace 600 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- $B
