@@ -12,7 +12,7 @@ ARCH     ?= gfx950
 
 # Strict IEEE fp32 everywhere on the parity path: no contraction, no fast-math, IEEE div/sqrt.
 HOST_FLAGS := -O2 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -Wall -Wextra -Iinclude
-HIP_FLAGS  := -O3 -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math \
+HIP_FLAGS  := -O3 -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math $(PRT_DEFS) \
               -fhip-fp32-correctly-rounded-divide-sqrt -fPIC -Wall -Iinclude -I$(CSRC)
 
 .PHONY: all host hip cli oracle clean

@@ -97,9 +97,8 @@ enum {
 /* rt_frame.variant: launch configuration of RT_KERNEL_FAST */
 enum {
     RT_VARIANT_DEFAULT = 0,  /* the library's rule, measured per frame shape: frame batches and spp > 1 try
-                                RT_VARIANT_PERSIST4, RT_VARIANT_SHPOOL and (1 spp) RT_VARIANT_STREAM on their first
-                                launches and keep the fastest (RT_VARIANT_PERSIST4 where the pool's LDS path buffer does
-                                not fit); single 1-spp frames run RT_VARIANT_HYBRID (RT_VARIANT_PERSIST where it cannot
+                                RT_VARIANT_PERSIST4 and RT_VARIANT_SHPOOL on their first launches and keep the faster
+                                (RT_VARIANT_PERSIST4 where the pool's LDS path buffer does not fit); single 1-spp frames run RT_VARIANT_HYBRID (RT_VARIANT_PERSIST where it cannot
                                 run); with rt_frame.tune = 1 the autotuner's candidates instead (rt_get_launch_info) */
     RT_VARIANT_PERSIST = 1,  /* k_persist: one lane per pixel path, walks in lockstep, 3 waves per SIMD */
     RT_VARIANT_PERSIST4 = 2, /* k_persist at 4 waves per SIMD (path levels in LDS) */
@@ -118,14 +117,12 @@ enum {
                                 camera. Nothing waits on the host: measurements and trials are read by event queries
                                 (rt_frame.hot_pct > 0: that threshold and rt_frame.hot_kernel, no trials) */
     /* 12: k_relay (1 + lights waves per tile, LDS hand-off), measured slower, removed in round 4: refused */
-    RT_VARIANT_SHPOOL = 13,  /* k_persist at 4 waves per SIMD with each bounce level's shadow rays (every pixel's, every
+    RT_VARIANT_SHPOOL = 13   /* k_persist at 4 waves per SIMD with each bounce level's shadow rays (every pixel's, every
                                 light's) walked as ONE per-wave pool: a lane whose walk ends takes the next unassigned ray,
                                 lanes of ended paths included (rt_frame.regroup = idle lanes per refill; 1..32 lights; the
                                 LDS path buffer must fit 4 workgroups per CU, else RT_VARIANT_PERSIST4 runs) */
-    RT_VARIANT_STREAM = 14   /* k_stream (1 spp): a lane whose path ends stores its pixel and takes the next pixel of its
-                                wave's tile (the wave takes its next tile when the current one has none left), so every
-                                round of closest walks, pooled shadow rays and shading runs with the wave's lanes busy;
-                                RT_VARIANT_SHPOOL's conditions, else as RT_VARIANT_SHPOOL */
+    /* 14: k_stream (a lane whose path ends takes its tile's next pixel; paths at mixed levels), measured slower in
+       round 4 (dragon 0.781 vs 0.654 ms per frame in 20-frame batches) and removed: refused */
 };
 
 /* rt_frame.hot_kernel: the kernel RT_VARIANT_HYBRID sends the hot tiles to when rt_frame.hot_pct > 0 */

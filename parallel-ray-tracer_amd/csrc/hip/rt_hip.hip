@@ -21,7 +21,6 @@
 #include "rt_host.h"
 #include "rt_kernels.hpp"
 #include "rt_shpool.hpp"
-#include "rt_stream.hpp"
 #include "rt_coop.hpp"
 #include "rt_fan.hpp"
 #include "rt_output.hpp"
@@ -144,7 +143,7 @@ struct rt_ctx {
         int W = 0, rows = 0, off = 0, stride = 0, block = 0, shift = 0, bounces = 0, spp = 0, frames = 0, dealing = 0,
             cap_req = 0;
         static constexpr int ROUNDS = 2;
-        long long launch[3][ROUNDS] = {{-1, -1}, {-1, -1}, {-1, -1}};
+        long long launch[2][ROUNDS] = {{-1, -1}, {-1, -1}};
         int choice = -1;
     };
     std::vector<BatchRule> brules;
@@ -161,13 +160,14 @@ struct rt_ctx {
         int state = 0;  // 0: measure next; 1: a measuring frame's tile times are on their way to h_tr; 2: lists ready
         long long frames = 0;  // frames since the choice or the last list refresh
         static constexpr int NCAND = 12;
-        static constexpr int ROUNDS = 2;    // trials per candidate (the minimum counts: single frames are noisy)
+        static constexpr int ROUNDS = 3;    // trials per candidate, chosen by their median (single frames are noisy, and
+                                            // some two-stream launches bimodal)
         static constexpr int REFRESH = 64;  // frames of a shape between measuring frames once it is decided
         // candidates: hot threshold (0 = the cold kernel over the whole frame), lanes per ray, k_fan or k_coop for
         // the hot tiles, the cold tiles' kernel (RT_VARIANT_PERSIST / SHPOOL); their lists at d_lists + at[c]
         int nc = 0, choice = -1;
         int pct[NCAND] = {}, lanes[NCAND] = {}, cold[NCAND] = {}, n_hot[NCAND] = {}, n_cold[NCAND] = {};
-        bool fan[NCAND] = {};
+        bool fan[NCAND] = {}, lpt[NCAND] = {};
         size_t at[NCAND] = {};
         long long launch[NCAND][ROUNDS] = {};
         float ms[NCAND] = {};
@@ -189,13 +189,17 @@ namespace {
 // slowest tile of the measuring frame go to k_coop with `lanes` lanes per ray while the cold kernel renders the rest
 // (each candidate is tried ROUNDS times; hybrid_pick). Measured: car_boxed hot > 45 % k_coop<4>,
 // sportscar hot > 60 % k_coop<2> / <4>, dragon the whole-frame kernels; k_fan and k_relay hot tiles never won.
+// lpt: the cold tiles dealt costliest first by the measuring frame's per-tile times (longest processing time first,
+// the classic makespan heuristic: a single frame ends with its slowest tile) instead of centre-out; with pct = 0 the
+// whole frame that way.
 struct HotCand {
     int pct, lanes, cold;
+    bool lpt;
 };
-constexpr HotCand HYBRID_CANDS[] = {{0, 0, RT_VARIANT_PERSIST}, {0, 0, RT_VARIANT_SHPOOL},   {0, 0, RT_VARIANT_STREAM},
-                                    {45, 4, RT_VARIANT_PERSIST},
-                                    {60, 4, RT_VARIANT_PERSIST}, {75, 4, RT_VARIANT_PERSIST}, {60, 2, RT_VARIANT_PERSIST},
-                                    {75, 2, RT_VARIANT_PERSIST}, {60, 4, RT_VARIANT_SHPOOL},  {75, 2, RT_VARIANT_SHPOOL}};
+constexpr HotCand HYBRID_CANDS[] = {
+    {0, 0, RT_VARIANT_PERSIST, false},  {0, 0, RT_VARIANT_SHPOOL, false}, {0, 0, RT_VARIANT_PERSIST, true},
+    {0, 0, RT_VARIANT_SHPOOL, true},    {45, 4, RT_VARIANT_PERSIST, true}, {45, 4, RT_VARIANT_PERSIST, false},
+    {60, 4, RT_VARIANT_PERSIST, false}, {60, 2, RT_VARIANT_PERSIST, false}, {45, 4, RT_VARIANT_SHPOOL, true}};
 // pixel tile of a group kernel (rtd::GTile): k_coop<2> / k_fan<2> 8x4, k_coop<4> / k_fan<4> 4x4, k_fan<8> 4x2
 inline void hot_tile(int g, int& tw, int& th) {
     tw = g == 2 ? 8 : 4;
@@ -211,7 +215,6 @@ const char* variant_name(int v) {
         case RT_VARIANT_FAN: return "fan";
         case RT_VARIANT_HYBRID: return "hybrid";
         case RT_VARIANT_SHPOOL: return "shpool";
-        case RT_VARIANT_STREAM: return "stream";
         default: return "default";
     }
 }
@@ -948,8 +951,6 @@ bool pbl_fits(const rtd::KArgs& A, int device) {
 //                        when 4 workgroups of that fit a CU, else a global slab;
 //   RT_VARIANT_SHPOOL    PERSIST4 with each bounce level's shadow rays walked as a per-wave pool (rt_shpool.hpp);
 //                        PERSIST4 where the LDS path buffer does not fit;
-//   RT_VARIANT_STREAM    k_stream (rt_stream.hpp): a lane takes the next pixel of its wave's tile when its path ends;
-//                        1 spp with the LDS path buffer, else SHPOOL's rule;
 // a tile trace (A.tile_trace: the hybrid launch's measuring frame, PRT_TILE_TRACE) runs the 3-wave build with
 // per-tile timestamps.
 template <int MAXB>
@@ -957,15 +958,11 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
     dyn = 0;
     if (A.tile_trace)
         return count ? rtd::k_persist<MAXB, false, true, true, 3, true, true> : rtd::k_persist<MAXB, false, false, true, 3, true, true>;
-    if (variant == RT_VARIANT_STREAM && A.spp <= 1 && pbl_fits<MAXB>(A, device)) {
-        dyn = pbl_bytes<MAXB>(A);
-        return count ? rtd::k_stream<MAXB, true> : rtd::k_stream<MAXB, false>;
-    }
-    if (variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_STREAM) {
+    if (variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL) {
         const bool pbl = pbl_fits<MAXB>(A, device);
         if (pbl) dyn = pbl_bytes<MAXB>(A);
         // (the bench's batches: the spp = 1 build)
-        return variant != RT_VARIANT_PERSIST4 && pbl ? persist4<MAXB, true>(true, A.spp <= 1, count)
+        return variant == RT_VARIANT_SHPOOL && pbl ? persist4<MAXB, true>(true, A.spp <= 1, count)
                                                    : persist4<MAXB, false>(pbl, A.spp <= 1, count);
     }
     return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true> : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
@@ -1121,8 +1118,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     const bool known = f->variant == RT_VARIANT_DEFAULT || f->variant == RT_VARIANT_PERSIST ||
                        f->variant == RT_VARIANT_PERSIST4 || f->variant == RT_VARIANT_COOP2 ||
                        f->variant == RT_VARIANT_COOP4 || f->variant == RT_VARIANT_FAN ||
-                       f->variant == RT_VARIANT_HYBRID || f->variant == RT_VARIANT_SHPOOL ||
-                       f->variant == RT_VARIANT_STREAM;
+                       f->variant == RT_VARIANT_HYBRID || f->variant == RT_VARIANT_SHPOOL;
     if (!known || f->hot_pct < 0 || f->hot_pct > 100 || f->hot_kernel < RT_HOT_COOP4 || f->hot_kernel > RT_HOT_FAN ||
         f->tune < 0 || f->tune > 1 ||
         f->waves_cap < 0 || f->waves_cap > 8 || f->dealing < RT_DEAL_DEFAULT || f->dealing > RT_DEAL_ROW_MAJOR ||
@@ -1312,7 +1308,6 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         if (v == RT_VARIANT_FAN) return fan_ok;
         if (v == RT_VARIANT_COOP2 || v == RT_VARIANT_COOP4) return wide_ok;
         if (v == RT_VARIANT_SHPOOL) return shp_ok;
-        if (v == RT_VARIANT_STREAM) return shp_ok && f->spp == 1;
         if (v == RT_VARIANT_HYBRID) return wide_ok && n_frames == 1 && fs == 0 && f->spp == 1;
         return true;
     };
@@ -1325,9 +1320,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     int mode = f->variant;
     if (mode == RT_VARIANT_DEFAULT)
         mode = (n_frames > 1 || f->spp > 1) ? (pool_rule ? RT_VARIANT_SHPOOL : RT_VARIANT_PERSIST4) : RT_VARIANT_HYBRID;
-    if ((mode == RT_VARIANT_SHPOOL || mode == RT_VARIANT_STREAM) && !shp_ok)
-        mode = RT_VARIANT_PERSIST4;  // (no room for the pool: PERSIST4 itself)
-    if (mode == RT_VARIANT_STREAM && f->spp != 1) mode = RT_VARIANT_SHPOOL;
+    if (mode == RT_VARIANT_SHPOOL && !shp_ok) mode = RT_VARIANT_PERSIST4;  // (no room for the pool: PERSIST4 itself)
     if (!usable(mode)) mode = RT_VARIANT_PERSIST;  // (no wide view, or a diagnostics trace)
     // the whole-frame kernel of a single frame while the hybrid launch measures or tries its candidates
     const int single_rule = pool_rule ? RT_VARIANT_SHPOOL : RT_VARIANT_PERSIST;
@@ -1437,8 +1430,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                                      f->bounces, f->spp, n_frames, f->dealing, f->waves_cap};
         }
         rt_ctx::BatchRule& b = *br;
-        const int cand[3] = {RT_VARIANT_PERSIST4, RT_VARIANT_SHPOOL, RT_VARIANT_STREAM};
-        const int nc = usable(RT_VARIANT_STREAM) ? 3 : 2;
+        const int cand[2] = {RT_VARIANT_PERSIST4, RT_VARIANT_SHPOOL};
+        const int nc = 2;
         int pick = -1;
         if (b.choice < 0) {
             for (int r = 0; r < rt_ctx::BatchRule::ROUNDS && pick < 0; r++)
@@ -1453,7 +1446,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                     for (long long x : b.launch[c]) last = std::max(last, x);
                 const hipError_t q = hipEventQuery(ctx->ev1s[last % rt_ctx::NEV]);
                 if (q == hipSuccess) {
-                    float ms[3] = {1e30f, 1e30f, 1e30f};
+                    float ms[2] = {1e30f, 1e30f};
                     for (int c = 0; c < nc; c++)
                         for (int r = 0; r < rt_ctx::BatchRule::ROUNDS; r++) {
                             const int sl = (int)(b.launch[c][r] % rt_ctx::NEV);
@@ -1465,8 +1458,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                     for (int c = 1; c < nc; c++)
                         if (ms[c] < ms[b.choice]) b.choice = c;
                     if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1)
-                        std::fprintf(stderr, "[prt batch] %dx%d f%d spp%d: persist4 %.3f ms, shpool %.3f ms, stream %.3f ms -> %s\n",
-                                     f->width, f->n_rows, n_frames, f->spp, ms[0], ms[1], ms[2], variant_name(cand[b.choice]));
+                        std::fprintf(stderr, "[prt batch] %dx%d f%d spp%d: persist4 %.3f ms, shpool %.3f ms -> %s\n",
+                                     f->width, f->n_rows, n_frames, f->spp, ms[0], ms[1], variant_name(cand[b.choice]));
                 } else if (q != hipErrorNotReady) {
                     return fail(ctx, q, "rt_render: batch rule trials");
                 } else {
@@ -1570,27 +1563,28 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             const bool keep = h.choice >= 0;  // a refresh: new lists, the same candidates and choice
             if (!keep) {
                 h.nc = 0;
-                auto add = [&](int pct, int lanes, bool fan, int cold) {
+                auto add = [&](int pct, int lanes, bool fan, int cold, bool lpt) {
                     if (h.nc >= rt_ctx::Hybrid::NCAND || !usable(cold)) return;
                     h.pct[h.nc] = pct;
                     h.lanes[h.nc] = lanes;
                     h.fan[h.nc] = fan;
+                    h.lpt[h.nc] = lpt;
                     h.cold[h.nc++] = cold;
                 };
                 if (f->hot_pct > 0) {
                     const bool fan = f->hot_kernel == RT_HOT_FAN && fan_ok;
-                    add(f->hot_pct, fan ? fan_r : f->hot_kernel == RT_HOT_COOP2 ? 2 : 4, fan, RT_VARIANT_PERSIST);
+                    add(f->hot_pct, fan ? fan_r : f->hot_kernel == RT_HOT_COOP2 ? 2 : 4, fan, RT_VARIANT_PERSIST, false);
                 } else {
-                    for (const HotCand& hc : HYBRID_CANDS) add(hc.pct, hc.lanes, false, hc.cold);
+                    for (const HotCand& hc : HYBRID_CANDS) add(hc.pct, hc.lanes, false, hc.cold, hc.lpt);
                 }
             }
             std::vector<int> lists;
             for (int c = 0; c < h.nc; c++) {
                 h.at[c] = lists.size();
                 h.n_hot[c] = h.n_cold[c] = 0;
-                if (h.pct[c] == 0) continue;
+                if (h.pct[c] == 0 && !h.lpt[c]) continue;
                 std::vector<int> hot8;
-                for (size_t t = 0; t < h.n_tiles; t++)
+                for (size_t t = 0; t < h.n_tiles && h.pct[c] > 0; t++)
                     if (dur[t] * 100 > (long long)h.pct[c] * cmax) hot8.push_back((int)t);
                 std::stable_sort(hot8.begin(), hot8.end(), [&](int a, int b) { return dur[a] > dur[b]; });
                 if (hot8.size() > h.n_tiles / 2) hot8.resize(h.n_tiles / 2);  // k_coop costs ~2x the wave time
@@ -1611,6 +1605,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 std::vector<int> cold;
                 for (int t : ord)
                     if (!is_hot[t]) cold.push_back(t);
+                if (h.lpt[c])  // costliest first (ties: centre-out)
+                    std::stable_sort(cold.begin(), cold.end(), [&](int a, int b) { return dur[a] > dur[b]; });
                 h.n_cold[c] = (int)cold.size();
                 if (h.cold_regions) cold = region_layout(cold, tx, ty, xcd_mode);
                 lists.insert(lists.end(), cold.begin(), cold.end());
@@ -1647,16 +1643,17 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             h.frames = 0;
             h.state = 2;
         }
+        auto pick_of = [&](int c) { return h.pct[c] == 0 && !h.lpt[c] ? Pick{1, h.cold[c]} : Pick{2, c}; };
         if (h.choice >= 0) {
             li.settled = 1;
             li.trial = 0;
-            return h.pct[h.choice] == 0 ? Pick{1, h.cold[h.choice]} : Pick{2, h.choice};
+            return pick_of(h.choice);
         }
         for (int r = 0; r < rt_ctx::Hybrid::ROUNDS; r++)
             for (int c = 0; c < h.nc; c++)
                 if (h.launch[c][r] < 0 || ctx->launches - h.launch[c][r] >= rt_ctx::NEV) {  // untried (or events reused)
                     h.launch[c][r] = ctx->launches;
-                    return h.pct[c] == 0 ? Pick{1, h.cold[c]} : Pick{2, c};
+                    return pick_of(c);
                 }
         long long last = 0;
         for (int c = 0; c < h.nc; c++)
@@ -1666,14 +1663,14 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         if (!done) return Pick{1, single_rule};  // the trials are still running
         int best = 0;
         for (int c = 0; c < h.nc; c++) {
-            h.ms[c] = 1e30f;
+            float t[rt_ctx::Hybrid::ROUNDS];
             for (int r = 0; r < rt_ctx::Hybrid::ROUNDS; r++) {
                 const int sl = (int)(h.launch[c][r] % rt_ctx::NEV);
-                float ms = 0.0f;
-                const hipError_t e = hipEventElapsedTime(&ms, ctx->ev0s[sl], ctx->ev1s[sl]);
+                const hipError_t e = hipEventElapsedTime(&t[r], ctx->ev0s[sl], ctx->ev1s[sl]);
                 if (e != hipSuccess) return err(e, "rt_render: hybrid trials");
-                h.ms[c] = std::min(h.ms[c], ms);
             }
+            std::sort(t, t + rt_ctx::Hybrid::ROUNDS);
+            h.ms[c] = t[rt_ctx::Hybrid::ROUNDS / 2];  // the median
             if (h.ms[c] < h.ms[best]) best = c;
         }
         h.choice = best;
@@ -1681,13 +1678,13 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1) {
             std::fprintf(stderr, "[prt hybrid] %dx%d b%d:", f->width, f->n_rows, f->bounces);
             for (int c = 0; c < h.nc; c++)
-                std::fprintf(stderr, " %s%d/%s%d/%s %.3f ms", h.pct[c] ? "hot>" : "whole", h.pct[c], h.fan[c] ? "fan" : "coop",
-                             h.lanes[c], variant_name(h.cold[c]), h.ms[c]);
+                std::fprintf(stderr, " %s%d/%s%d/%s%s %.3f ms", h.pct[c] ? "hot>" : "whole", h.pct[c],
+                             h.fan[c] ? "fan" : "coop", h.lanes[c], variant_name(h.cold[c]), h.lpt[c] ? "/lpt" : "", h.ms[c]);
             std::fprintf(stderr, " -> %d\n", best);
         }
         li.settled = 1;
         li.trial = 0;
-        return h.pct[best] == 0 ? Pick{1, h.cold[best]} : Pick{2, best};
+        return pick_of(best);
     };
     // one frame of configuration (variant, cap); d_work holds the persistent grids' work counters, and the
     // ray counters restart with every launch (rt_get_stats reports the frame, not the trial launches)
@@ -1915,8 +1912,13 @@ int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c) {
     const KFn kp = persist_kernel<MAXB>(P, h.cold[c], count, ctx->device, dyn);
     const int rp = resident(kp, ctx->device, 8, dyn);
     const int rcp = resident(kc, ctx->device);
-    const int nc = std::max(1, std::min((n_hot + 3) / 4, rcp / 2));
+    const int nc = n_hot > 0 ? std::max(1, std::min((n_hot + 3) / 4, rcp / 2)) : 0;
     const int np = std::max(1, std::min(rp - (int)((long long)nc * rp / rcp), (n_cold + 3) / 4));
+    if (n_hot == 0) {  // (a whole frame in the measured order)
+        if (n_cold > 0) kp<<<np, rtd::BLOCK, dyn, ctx->stream>>>(P);
+        HIPC(hipGetLastError());
+        return RT_OK;
+    }
     HIPC(hipEventRecord(h.fork, ctx->stream));  // after the work / counter resets
     HIPC(hipStreamWaitEvent(h.s2, h.fork, 0));
     if (n_hot > 0) kc<<<nc, rtd::BLOCK, 0, h.s2>>>(B);

@@ -331,6 +331,7 @@ __device__ __forceinline__ WNode wload(const DWide& W, int node) {
     return WNode{N[0], N[1], N[2], N[3], N[4]};
 }
 
+
 template <bool COUNT>
 __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsigned oct, float lim, unsigned& nh,
                                           unsigned& th, int& cbase, int& tbase, unsigned& imask, unsigned& nleaf,

@@ -74,13 +74,12 @@ __device__ __forceinline__ void flush_u(const UCtr& u, unsigned long long* g) {
 
 // The shadow rays of one bounce level of the wave's paths, walked as a wave-level pool.
 // okm: bit j = this lane's path hit a surface at this level and light j passed the back-face test (dot(L - ip, n)
-// >= 0, the reference's early-out, raytracer.c:66-67; failing lights are not walked). pbw: the wave's path buffer
-// (LDS, [level][lane] float4); myslot: this lane's slot of its current level in it, where an owner has stored its hit
-// point (.xyz) and 0 (.w), and where the walkers set bit j of .w (as an unsigned) when light j is visible from the
-// hit point along the reference's shadow ray. (Owners may be at different levels: rt_stream.hpp.)
+// >= 0, the reference's early-out, raytracer.c:66-67; failing lights are not walked). lvl: the wave's 64 path-buffer
+// slots of this level (LDS); the owner lane p has stored its hit point in lvl[p].xyz and 0 in lvl[p].w, and the
+// walkers set bit j of lvl[p].w (as an unsigned) when light j is visible from it along the reference's shadow ray.
 // regroup: idle lanes that trigger a refill (all lanes idle always do). Called by every lane of the wave.
 template <bool COUNT>
-__device__ __forceinline__ void shadow_pool(const DScene& s, unsigned okm, float4* pbw, int myslot, int* __restrict__ stk,
+__device__ __forceinline__ void shadow_pool(const DScene& s, unsigned okm, float4* lvl, int* __restrict__ stk,
                                             int* __restrict__ sstk, int wcap, int regroup, Ctr& c, UCtr& u) {
     const unsigned lane = threadIdx.x & 63u;
     const unsigned long long all = uni64(__ballot(1));
@@ -96,7 +95,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, unsigned okm, float
             u.shad += (unsigned)__builtin_popcountll(cm);
         }
     };
-    // this lane's ray (owner's slot | light << 16) and its walk state (visible_wide's)
+    // this lane's ray (owner lane | light << 8) and its walk state (visible_wide's)
     bool busy = false;
     int wo = 0;
     v3 o = mk(0.0f, 0.0f, 0.0f), d = o;
@@ -131,14 +130,11 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, unsigned okm, float
                     req = 0ull;
                 }
             }
-            // the owner's slot (every lane reads: a cross-lane read needs its source lane active)
-            const int oslot = __shfl(myslot, wo & 63, 64);
             if (got) {
-                wo = oslot | ((wo >> 8) << 16);
                 // the reference's shadow ray, light_v (raytracer.c:62-99) as path_step forms it, from the owner's hit
                 // point (its path-buffer slot)
-                const v3 ipo = xyz(pbw[wo & 0xFFFF]);
-                const v3 Lp = xyz(s.lights[2 * (wo >> 16)]);
+                const v3 ipo = xyz(lvl[wo & 63]);
+                const v3 Lp = xyz(s.lights[2 * (wo >> 8)]);
                 v3 l = sub(Lp, ipo);
                 const float mg = mag(l);
                 l = dvs(l, mg);
@@ -149,7 +145,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, unsigned okm, float
                 if (degenerate(d)) {  // zero direction component: the reference's NaN slabs, walked strictly
                     c.fb++;
                     if (visible_walk<true, COUNT, true>(s.ref, o, d, ld2, sstk ? sstk : stk, c))
-                        atomicOr(reinterpret_cast<unsigned*>(pbw + (wo & 0xFFFF)) + 3, 1u << ((wo >> 16) & 31));
+                        atomicOr(reinterpret_cast<unsigned*>(lvl + (wo & 63)) + 3, 1u << ((wo >> 8) & 31));
                 } else {
                     p = ray_pre(o, d);
                     oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
@@ -197,7 +193,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, unsigned okm, float
                 if (occ || next < 0) {
                     if (!occ && next == -2) c.err++;
                     if (!occ)  // the owner's visibility bit
-                        atomicOr(reinterpret_cast<unsigned*>(pbw + (wo & 0xFFFF)) + 3, 1u << ((wo >> 16) & 31));
+                        atomicOr(reinterpret_cast<unsigned*>(lvl + (wo & 63)) + 3, 1u << ((wo >> 8) & 31));
                     busy = false;
                 }
             }
@@ -268,7 +264,7 @@ __device__ __forceinline__ v3 trace_path_shp(const KArgs& A, bool alive, v3 o, v
         if (nh) {
             u.skip += nh * (unsigned)s.n_lights;  // less the rays walked (shadow_pool counts those in u.shad)
             const unsigned sh0 = u.shad;
-            shadow_pool<COUNT>(s, okm, pbw, it * 64 + (int)(threadIdx.x & 63u), stk, sstk, wcap, A.regroup, c, u);
+            shadow_pool<COUNT>(s, okm, pbw + it * 64, stk, sstk, wcap, A.regroup, c, u);
             u.skip -= u.shad - sh0;
         }
         if (hit >= 0) {  // raytracer.c:144-172 as path_step, the lights' visibility from the pool

@@ -114,7 +114,7 @@ def test_unit_direction_view_renders_the_reference_fixture(name, W, H, fixture):
     want = unit_hittable_count(s)
     n = s.n_triangles
     ref = np.load(os.path.join(GOLD, fixture + ".npz"))
-    for kernel in ("fast", "persist4", "coop4", "shpool", "stream"):
+    for kernel in ("fast", "persist4", "coop4", "shpool"):
         out = render(s, W, H, kernel, counters=True)
         info = out["info"]
         assert 0 < want < n and info["unit_triangles"] == want, (info, want, n)

@@ -118,13 +118,13 @@ def test_config_single_frame_vs_reference(name, W, H, tag, kernel):
     assert st["stack_overflows"] == 0
 
 
-@pytest.mark.parametrize("variant", ["default", "persist4", "shpool", "stream"])
+@pytest.mark.parametrize("variant", ["default", "persist4", "shpool"])
 @pytest.mark.parametrize("name,W,H,tag", CONFIGS)
 def test_config_bench_batch_vs_reference(name, W, H, tag, variant):
     """bench.py's instantiation (4 frames of its camera path in one rt_render_frames launch, BGRA8 only) against
-    the reference and against single-frame renders. The default rule measures PERSIST4, the shadow pool and k_stream
-    on the first launches of a shape and keeps the fastest, so the bench runs any of them: all are pinned here, and
-    the default rule's own launches (its trials, then its choice)."""
+    the reference and against single-frame renders. The default rule measures PERSIST4 and the shadow pool on the
+    first launches of a shape and keeps the faster, so the bench runs either: both are pinned here, and the default
+    rule's own launches (its trials, then its choice)."""
     import torch
     from prt import device
     n = 4
@@ -139,7 +139,7 @@ def test_config_bench_batch_vs_reference(name, W, H, tag, variant):
         if variant == "default" and r.launch_info()["settled"]:
             break
     if variant == "default":
-        assert r.launch_info()["settled"] and r.launch_info()["variant"] in ("persist4", "shpool", "stream"), r.launch_info()
+        assert r.launch_info()["settled"] and r.launch_info()["variant"] in ("persist4", "shpool"), r.launch_info()
     frames = px.cpu().numpy().view(np.uint32)
     r.close()
     ref = np.load(os.path.join(GOLD, f"{name}_{tag}_strict_sample.npz"))

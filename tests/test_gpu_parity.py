@@ -20,9 +20,8 @@ RGB_TOL = 1e-5
 # with its default rule ("fast"), and each variant forced: k_persist at 4 waves/SIMD ("persist4"), k_coop
 # ("coopG": G lanes per ray), k_fan ("fan":
 # 1 + lights lanes per pixel). "shpool": k_persist with each level's shadow rays walked as a per-wave pool
-# (rt_shpool.hpp); "stream": k_stream, a lane takes its tile's next pixel when its path ends (rt_stream.hpp; spp = 1,
-# the shadow pool's rule for spp > 1).
-KERNELS = ["strict", "fast", "persist4", "coop2", "coop4", "fan", "shpool", "stream"]
+# (rt_shpool.hpp).
+KERNELS = ["strict", "fast", "persist4", "coop2", "coop4", "fan", "shpool"]
 
 
 def select(kernel):
@@ -435,7 +434,7 @@ def moved_camera(W, H, dx, dz):
     return c
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "strict", "shpool", "stream"])
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "strict", "shpool"])
 @pytest.mark.parametrize("name", ["car_boxed", "dragon"])
 def test_frame_batch_equals_single_frames(dev, name, kernel):
     """rt_render_frames: a batch of frames (different cameras, one persistent launch on the fast paths)
@@ -568,7 +567,7 @@ def test_path_level_placements_render_the_same_frames(dev, name):
     s = host.Scene.named(name).build_bvh(3)
     W, H = 200, 120
     outs = {}
-    for v in ("persist", "persist4", "shpool", "stream"):
+    for v in ("persist", "persist4", "shpool"):
         a = render(dev, s, W, H, v, counters=True)
         b = render(dev, s, W, H, v, spp=4)
         r = dev.Renderer(0)
@@ -581,14 +580,14 @@ def test_path_level_placements_render_the_same_frames(dev, name):
         r.close()
     a0, b0, f0 = outs["persist"]
     assert same_bits(f0[0], a0["rgb"]) and same_bits(f0[2], a0["rgb"])
-    for v in ("persist4", "shpool", "stream"):
+    for v in ("persist4", "shpool"):
         a1, b1, f1 = outs[v]
         assert same_bits(a0["rgb"], a1["rgb"]) and same_bits(b0["rgb"], b1["rgb"]) and same_bits(f0, f1), v
         np.testing.assert_array_equal(a0["hit"], a1["hit"])
         assert a0["stats"]["rays"] == a1["stats"]["rays"], v
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "shpool", "stream"])
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "shpool"])
 def test_rotated_row_blocks_cover_every_frame(dev, kernel):
     """rt_frame.frame_shift: frame f of rank q renders block residue (q + f) % N (prt.dist rotate), rows
     past the image skipped — over the N ranks every frame of the batch is rendered exactly once, bit for

@@ -81,7 +81,7 @@ def test_moving_camera_walkthrough_enqueues_without_waits(dev, name):
 
 def test_single_frame_rule_settles_on_a_moving_camera(dev):
     """the single-frame rule keyed by shape: with a sync per frame (the reference's loop) it settles within its
-    measuring frame + 2 trials per candidate (+ the frames that find the last trial still running), on a camera that
+    measuring frame + 3 trials per candidate (+ the frames that find the last trial still running), on a camera that
     never repeats, and stays settled; rt_get_launch_info names what each frame ran"""
     W, H = 640, 360
     s = host.Scene.named("dragon").build_bvh(3)
@@ -89,16 +89,16 @@ def test_single_frame_rule_settles_on_a_moving_camera(dev):
     r.upload(s)
     px = torch.empty((H, W), dtype=torch.int32, device="cuda")
     infos = []
-    for i in range(44):
+    for i in range(50):
         r.render(walk(W, H, i), W, H, bgra=px)
         r.sync()
         infos.append(r.launch_info())
     r.close()
     first = next(i for i, x in enumerate(infos) if x["settled"])
-    assert first <= 1 + 2 * 10 + 2, (first, infos[:first + 1])
+    assert first <= 1 + 3 * 9 + 2, (first, infos[:first + 1])
     assert all(x["settled"] and not x["trial"] for x in infos[first:first + 60]), infos
     assert infos[0]["trial"] == 1 and infos[0]["variant"] == "persist"  # the measuring frame
-    assert infos[-1]["variant"] in ("persist", "shpool", "stream", "hybrid")
+    assert infos[-1]["variant"] in ("persist", "shpool", "hybrid")
 
 
 @pytest.mark.parametrize("name", ["dragon", "car_boxed"])
@@ -145,6 +145,6 @@ def test_batch_rule_settles_on_the_faster_kernel(dev, name):
             ref = got
         np.testing.assert_array_equal(got, ref, err_msg=str(k))
     r.close()
-    tried = [x["variant"] for x in seen[:6]]
-    assert tried == ["persist4", "shpool", "stream"] * 2 and all(x["trial"] for x in seen[:6]), seen
-    assert seen[6]["settled"] and all(x["settled"] and x["variant"] == seen[6]["variant"] for x in seen[6:]), seen
+    tried = [x["variant"] for x in seen[:4]]
+    assert tried == ["persist4", "shpool"] * 2 and all(x["trial"] for x in seen[:4]), seen
+    assert seen[4]["settled"] and all(x["settled"] and x["variant"] == seen[4]["variant"] for x in seen[4:]), seen

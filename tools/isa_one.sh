@@ -9,7 +9,6 @@ mkdir -p /tmp/isa
 {
   echo '#include "rt_kernels.hpp"'
   echo '#include "rt_shpool.hpp"'
-  echo '#include "rt_stream.hpp"'
   for a in "$@"; do
     case $a in
       *:*) echo "template __global__ void rtd::${a%%:*}<${a#*:}>(rtd::KArgs);" ;;
@@ -19,7 +18,7 @@ mkdir -p /tmp/isa
 } > /tmp/isa/one.hip
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
     -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -Iparallel-ray-tracer_amd/csrc/hip \
-    --cuda-device-only -S -o /tmp/isa/one.s /tmp/isa/one.hip || exit 1
+    $ISA_FLAGS --cuda-device-only -S -o /tmp/isa/one.s /tmp/isa/one.hip || exit 1
 python3 - <<'PY'
 import re
 s = open('/tmp/isa/one.s').read()

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Single-frame latency as the reference's loop sees it (cpu/src/main.c:171-185, gpu/src/main.cu:110-115: one
 render_frame() per iteration, each waited for): per launch configuration, `--iters` frames through rt_render,
-each followed by rt_sync; median HIP-event kernel ms and median host wall ms per frame over the second half, bit-exactness of the
-last frame against the first configuration.
+each followed by rt_sync; median HIP-event kernel ms and median host wall ms per frame over the frames after the
+library's rule has settled (rt_get_launch_info), bit-exactness of the last frame against the first configuration.
 usage: python tools/latency.py [--scene dragon] [--iters 20] persist hybrid hybrid:hot_pct=50 ..."""
 import argparse
 import os
@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--scene", default="dragon")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import numpy as np
@@ -35,20 +35,24 @@ def main():
         r = device.Renderer(0)
         r.upload(s)
         rgb = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
-        ks, ws = [], []
-        for _ in range(a.iters):
+        ks, ws, settled, info = [], [], None, {}
+        for i in range(a.iters):
             t0 = time.perf_counter()
             r.render(cam, W, H, kernel=name, rgb=rgb, **kw)
-            ks.append(r.sync())
-            ws.append((time.perf_counter() - t0) * 1e3)
+            ms = r.sync()
+            info = r.launch_info()
+            if info["settled"]:  # only the frames after the rule's measuring / trial frames
+                settled = i if settled is None else settled
+                ks.append(ms)
+                ws.append((time.perf_counter() - t0) * 1e3)
         got = rgb.cpu().numpy()
         r.close()
         if ref is None:
             ref = got
         same = np.array_equal(got.view(np.int32), ref.view(np.int32))
-        h = a.iters // 2  # the second half: after any measuring / trial frames
-        print(f"{a.scene:10s} {spec:22s} bit-exact {same!s:5s} kernel ms median {statistics.median(ks[h:]):.3f} "
-              f"min {min(ks[h:]):.3f} first {ks[0]:.3f}  wall ms median {statistics.median(ws[h:]):.3f}", flush=True)
+        print(f"{a.scene:10s} {spec:22s} bit-exact {same!s:5s} kernel ms median {statistics.median(ks):.3f} "
+              f"min {min(ks):.3f} max {max(ks):.3f} ({len(ks)} frames after settling at frame {settled})  wall ms median "
+              f"{statistics.median(ws):.3f}  ran {info}", flush=True)
 
 
 if __name__ == "__main__":
