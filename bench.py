@@ -369,6 +369,7 @@ def main():
     n_r = my_rows[2]
     launch_no = [0]
     latest = [0, 0, 0]  # (block, frames, context) of the latest launch
+    variant = [args.variant]  # N > 1: the rule's choice, agreed over the ranks after setup
 
     def launch(nf):
         b = launch_no[0] % 2
@@ -377,14 +378,14 @@ def main():
         latest[:] = [b, nf, c]
         if gmode == "native":  # render, then the gather on the context's stream (ordered after the render)
             rends[c].render_frames(path(nf), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
-                                   kernel=args.kernel, variant=args.variant, tune=args.tune, **out(ng.target(c)[:nf]))
+                                   kernel=args.kernel, variant=variant[0], tune=args.tune, **out(ng.target(c)[:nf]))
             ng.gather(c, nf)
             return
         with torch.cuda.stream(streams[c]):  # block b is rendered by context c on its stream
             if fg.pending(b):
                 fg.finish(b)
             rends[c].render_frames(path(nf), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
-                                   kernel=args.kernel, variant=args.variant, tune=args.tune, **out(fg.target(b)))
+                                   kernel=args.kernel, variant=variant[0], tune=args.tune, **out(fg.target(b)))
             fg.start(b)
 
     def drain():
@@ -411,6 +412,17 @@ def main():
                     settled = [all(every)]
                 if settled[0]:
                     break
+        if dist and variant[0] == "default" and not args.tune:
+            # every rank measured the rule's candidates on its own row set; small, noisy launches may choose
+            # differently, and a rank on the slower kernel would set the pace: every rank takes the choice most
+            # contexts made (ties: rank 0's), explicitly
+            mine = [r.launch_info()["variant"] for r in rends]
+            every = [None] * world
+            dist.all_gather_object(every, mine)
+            votes = [v for vs in every for v in vs]
+            variant[0] = max(dict.fromkeys(votes), key=votes.count)
+            for _ in range(n_streams):
+                launch(nf)
         rays_of[nf] = rends[(launch_no[0] - 1) % n_streams].stats()["rays"]
     if gmode == "native":  # untimed check of the native gather: rank 0's gathered frames == one GPU's frames
         drain()
