@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--iters", type=int, default=40)
+    ap.add_argument("--walk", type=float, default=0.0, help="camera moved by i * WALK along x in frame i (a walkthrough)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import numpy as np
@@ -38,7 +39,12 @@ def main():
         ks, ws, settled, info = [], [], None, {}
         for i in range(a.iters):
             t0 = time.perf_counter()
-            r.render(cam, W, H, kernel=name, rgb=rgb, **kw)
+            c = cam
+            if a.walk:
+                c = host.camera(W, H)
+                c.pos.x += i * a.walk
+                c.ul.x += i * a.walk
+            r.render(c, W, H, kernel=name, rgb=rgb, **kw)
             ms = r.sync()
             info = r.launch_info()
             if info["settled"]:  # only the frames after the rule's measuring / trial frames
