@@ -117,12 +117,16 @@ enum {
                                 camera. Nothing waits on the host: measurements and trials are read by event queries
                                 (rt_frame.hot_pct > 0: that threshold and rt_frame.hot_kernel, no trials) */
     /* 12: k_relay (1 + lights waves per tile, LDS hand-off), measured slower, removed in round 4: refused */
-    RT_VARIANT_SHPOOL = 13   /* k_persist at 4 waves per SIMD with each bounce level's shadow rays (every pixel's, every
+    RT_VARIANT_SHPOOL = 13,  /* k_persist at 4 waves per SIMD with each bounce level's shadow rays (every pixel's, every
                                 light's) walked as ONE per-wave pool: a lane whose walk ends takes the next unassigned ray,
                                 lanes of ended paths included (rt_frame.regroup = idle lanes per refill; 1..32 lights; the
                                 LDS path buffer must fit 4 workgroups per CU, else RT_VARIANT_PERSIST4 runs) */
     /* 14: k_stream (a lane whose path ends takes its tile's next pixel; paths at mixed levels), measured slower in
        round 4 (dragon 0.781 vs 0.654 ms per frame in 20-frame batches) and removed: refused */
+    RT_VARIANT_SHDEFER = 15  /* RT_VARIANT_SHPOOL with ONE pool for all bounce levels: a wave's paths find their closest
+                                hits level by level first, then the shadow rays of every level, pixel and light are walked
+                                as one pool and the levels are shaded after it (RT_VARIANT_PERSIST4 where the larger LDS
+                                path buffer does not fit) */
 };
 
 /* rt_frame.hot_kernel: the kernel RT_VARIANT_HYBRID sends the hot tiles to when rt_frame.hot_pct > 0 */

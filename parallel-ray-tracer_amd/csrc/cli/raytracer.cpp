@@ -4,7 +4,7 @@
 //             [--bounces B] [--iterations K] [--warmup W] [--bvh-heuristic H] [--seed S]
 //             [--gpus N] [--gather auto|rccl|peer] [--spp S] [--kernel fast|strict|VARIANT] [--tune]
 //             [--out FILE.bmp] [--cache DIR]
-//   VARIANT: persist, persist4, coop2, coop4, fan, hybrid, shpool (rt_frame.variant; the fast
+//   VARIANT: persist, persist4, coop2, coop4, fan, hybrid, shpool, shdefer (rt_frame.variant; the fast
 //   kernel's launch configurations, all rendering the same bits); --tune: measure the candidates on the
 //   first frame and keep the fastest (rt_frame.tune)
 //
@@ -164,7 +164,7 @@ int main(int argc, char** argv) {
         int variant;
     } variants[] = {{"fast", RT_VARIANT_DEFAULT}, {"persist", RT_VARIANT_PERSIST}, {"persist4", RT_VARIANT_PERSIST4},
                     {"coop2", RT_VARIANT_COOP2},  {"coop4", RT_VARIANT_COOP4},     {"fan", RT_VARIANT_FAN},
-                    {"hybrid", RT_VARIANT_HYBRID}, {"shpool", RT_VARIANT_SHPOOL}};
+                    {"hybrid", RT_VARIANT_HYBRID}, {"shpool", RT_VARIANT_SHPOOL}, {"shdefer", RT_VARIANT_SHDEFER}};
     int kern = a.kernel == "strict" ? RT_KERNEL_STRICT : -1, variant = RT_VARIANT_DEFAULT;
     for (const auto& v : variants)
         if (kern < 0 && a.kernel == v.name) {

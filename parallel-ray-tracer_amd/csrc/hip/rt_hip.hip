@@ -200,6 +200,7 @@ struct HotCand {
 // order, car_boxed hot > 45 % k_coop<4> with LPT cold tiles, sportscar hot > 60 % k_coop<4> / <2>) plus k_persist in
 // LPT order: few candidates keep the trial frames few (3 each) and the choice robust to frame-to-frame noise (a moving
 // camera changes every trial frame's cost; nine candidates picked a 12 % slower one on a walkthrough).
+// (RT_VARIANT_SHPOOL here stands for the rule's pool kernel: RT_VARIANT_SHDEFER where its path buffer fits.)
 constexpr HotCand HYBRID_CANDS[] = {{0, 0, RT_VARIANT_SHPOOL, true},   {0, 0, RT_VARIANT_PERSIST, true},
                                     {45, 4, RT_VARIANT_PERSIST, true}, {60, 4, RT_VARIANT_PERSIST, false},
                                     {60, 2, RT_VARIANT_PERSIST, false}};
@@ -218,6 +219,7 @@ const char* variant_name(int v) {
         case RT_VARIANT_FAN: return "fan";
         case RT_VARIANT_HYBRID: return "hybrid";
         case RT_VARIANT_SHPOOL: return "shpool";
+        case RT_VARIANT_SHDEFER: return "shdefer";
         default: return "default";
     }
 }
@@ -912,8 +914,9 @@ int resident(K kernel, int device, int cap = 8, size_t dyn_lds = 0, int block = 
 using KFn = void (*)(rtd::KArgs);
 
 // the 4-wave k_persist instantiation of a launch: path buffer in LDS (pbl) or global memory, the spp = 1 build,
-// counters; SHP: the per-wave shadow pool (rt_shpool.hpp), which needs the LDS path buffer
-template <int MAXB, bool SHP>
+// counters; SHP: the per-wave shadow pool (rt_shpool.hpp; 1: one pool per level, 2: one for all levels), which needs
+// the LDS path buffer
+template <int MAXB, int SHP>
 KFn persist4(bool pbl, bool spp1, bool count) {
     using rtd::k_persist;
     if (pbl) {
@@ -932,19 +935,21 @@ KFn persist4(bool pbl, bool spp1, bool count) {
 }
 
 // dynamic LDS of the 4-wave kernels' LDS layout: the wide stack sized to the scene's wide depth, then the path levels
+// (and, for the all-levels pool, each level's hit triangle)
 template <int MAXB>
-size_t pbl_bytes(const rtd::KArgs& A) {
-    return sizeof(int) * 2 * (size_t)A.wcap * rtd::BLOCK + sizeof(float4) * rtd::BLOCK * MAXB;
+size_t pbl_bytes(const rtd::KArgs& A, int shp = 0) {
+    return sizeof(int) * 2 * (size_t)A.wcap * rtd::BLOCK + sizeof(float4) * rtd::BLOCK * MAXB +
+           (shp == 2 ? sizeof(int) * rtd::BLOCK * MAXB : 0);
 }
 // Does that layout fit 4 workgroups per CU for this scene? (the LDS path buffer measured 1.2 % faster than the global
 // slab on dragon, 2.3 % on car_boxed; the shadow pool needs it)
 template <int MAXB>
-bool pbl_fits(const rtd::KArgs& A, int device) {
+bool pbl_fits(const rtd::KArgs& A, int device, int shp = 0) {
     if (!A.gstack || A.wcap <= 0) return false;
     (void)device;
     int per_cu = 0;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persist4<MAXB, false>(true, true, false), rtd::BLOCK,
-                                                        pbl_bytes<MAXB>(A)) == hipSuccess &&
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persist4<MAXB, 0>(true, true, false), rtd::BLOCK,
+                                                        pbl_bytes<MAXB>(A, shp)) == hipSuccess &&
            per_cu >= 4;
 }
 
@@ -954,6 +959,8 @@ bool pbl_fits(const rtd::KArgs& A, int device) {
 //                        when 4 workgroups of that fit a CU, else a global slab;
 //   RT_VARIANT_SHPOOL    PERSIST4 with each bounce level's shadow rays walked as a per-wave pool (rt_shpool.hpp);
 //                        PERSIST4 where the LDS path buffer does not fit;
+//   RT_VARIANT_SHDEFER   PERSIST4 with every level's shadow rays walked as ONE per-wave pool after the closest hits
+//                        (the path buffer plus a hit-triangle array in LDS; else PERSIST4);
 // a tile trace (A.tile_trace: the hybrid launch's measuring frame, PRT_TILE_TRACE) runs the 3-wave build with
 // per-tile timestamps.
 template <int MAXB>
@@ -961,12 +968,16 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
     dyn = 0;
     if (A.tile_trace)
         return count ? rtd::k_persist<MAXB, false, true, true, 3, true, true> : rtd::k_persist<MAXB, false, false, true, 3, true, true>;
-    if (variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL) {
+    if (variant == RT_VARIANT_SHDEFER && pbl_fits<MAXB>(A, device, 2)) {
+        dyn = pbl_bytes<MAXB>(A, 2);
+        return persist4<MAXB, 2>(true, A.spp <= 1, count);
+    }
+    if (variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) {
         const bool pbl = pbl_fits<MAXB>(A, device);
         if (pbl) dyn = pbl_bytes<MAXB>(A);
         // (the bench's batches: the spp = 1 build)
-        return variant == RT_VARIANT_SHPOOL && pbl ? persist4<MAXB, true>(true, A.spp <= 1, count)
-                                                   : persist4<MAXB, false>(pbl, A.spp <= 1, count);
+        return variant == RT_VARIANT_SHPOOL && pbl ? persist4<MAXB, 1>(true, A.spp <= 1, count)
+                                                   : persist4<MAXB, 0>(pbl, A.spp <= 1, count);
     }
     return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true> : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
 }
@@ -1121,7 +1132,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     const bool known = f->variant == RT_VARIANT_DEFAULT || f->variant == RT_VARIANT_PERSIST ||
                        f->variant == RT_VARIANT_PERSIST4 || f->variant == RT_VARIANT_COOP2 ||
                        f->variant == RT_VARIANT_COOP4 || f->variant == RT_VARIANT_FAN ||
-                       f->variant == RT_VARIANT_HYBRID || f->variant == RT_VARIANT_SHPOOL;
+                       f->variant == RT_VARIANT_HYBRID || f->variant == RT_VARIANT_SHPOOL ||
+                       f->variant == RT_VARIANT_SHDEFER;
     if (!known || f->hot_pct < 0 || f->hot_pct > 100 || f->hot_kernel < RT_HOT_COOP4 || f->hot_kernel > RT_HOT_FAN ||
         f->tune < 0 || f->tune > 1 ||
         f->waves_cap < 0 || f->waves_cap > 8 || f->dealing < RT_DEAL_DEFAULT || f->dealing > RT_DEAL_ROW_MAJOR ||
@@ -1306,11 +1318,13 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     // the shadow pool: 1..32 lights (a 32-bit visibility word per pixel) and the LDS path buffer at 4 workgroups per CU
     const bool shp_ok = wide_ok && ctx->n_lights >= 1 && ctx->n_lights <= 32 &&
                         (f->bounces <= 4 ? pbl_fits<4>(A, ctx->device) : pbl_fits<8>(A, ctx->device));
+    const bool shd_ok = shp_ok && (f->bounces <= 4 ? pbl_fits<4>(A, ctx->device, 2) : pbl_fits<8>(A, ctx->device, 2));
     auto usable = [&](int v) {
         if (A.tile_trace) return v == RT_VARIANT_PERSIST;  // (diagnostics: the 3-wave kernel's tile trace)
         if (v == RT_VARIANT_FAN) return fan_ok;
         if (v == RT_VARIANT_COOP2 || v == RT_VARIANT_COOP4) return wide_ok;
         if (v == RT_VARIANT_SHPOOL) return shp_ok;
+        if (v == RT_VARIANT_SHDEFER) return shd_ok;
         if (v == RT_VARIANT_HYBRID) return wide_ok && n_frames == 1 && fs == 0 && f->spp == 1;
         return true;
     };
@@ -1320,13 +1334,18 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     // waves; a single 1-spp frame is tail-bound: the hybrid launch, which measures its candidates on the frames of
     // the shape and keeps the fastest (k_persist where it cannot run).
     const bool pool_rule = shp_ok && ctx->n_lights >= 2;
+    // the pool kernel of the rules: one pool for all levels where its larger LDS path buffer fits (dragon 20-frame
+    // batches 0.655 -> 0.639 ms per frame, single frames 1.145 -> 1.091 ms; SIMD efficiency 0.59 -> 0.68), else one
+    // per level
+    const int pool_v = shd_ok ? RT_VARIANT_SHDEFER : RT_VARIANT_SHPOOL;
     int mode = f->variant;
     if (mode == RT_VARIANT_DEFAULT)
-        mode = (n_frames > 1 || f->spp > 1) ? (pool_rule ? RT_VARIANT_SHPOOL : RT_VARIANT_PERSIST4) : RT_VARIANT_HYBRID;
-    if (mode == RT_VARIANT_SHPOOL && !shp_ok) mode = RT_VARIANT_PERSIST4;  // (no room for the pool: PERSIST4 itself)
+        mode = (n_frames > 1 || f->spp > 1) ? (pool_rule ? pool_v : RT_VARIANT_PERSIST4) : RT_VARIANT_HYBRID;
+    if ((mode == RT_VARIANT_SHPOOL && !shp_ok) || (mode == RT_VARIANT_SHDEFER && !shd_ok))
+        mode = RT_VARIANT_PERSIST4;  // (no room for the pool: PERSIST4 itself)
     if (!usable(mode)) mode = RT_VARIANT_PERSIST;  // (no wide view, or a diagnostics trace)
     // the whole-frame kernel of a single frame while the hybrid launch measures or tries its candidates
-    const int single_rule = pool_rule ? RT_VARIANT_SHPOOL : RT_VARIANT_PERSIST;
+    const int single_rule = pool_rule ? pool_v : RT_VARIANT_PERSIST;
     int cap = f->waves_cap;
     const bool tunable = kernel == RT_KERNEL_FAST && f->tune == 1 && f->variant == RT_VARIANT_DEFAULT && !A.tile_trace;
     rt_ctx::Tune* Tp = nullptr;
@@ -1360,7 +1379,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         T.shift = fs;
         T.dealing = f->dealing;
         T.cap_req = f->waves_cap;
-        const int md[7] = {RT_VARIANT_PERSIST, RT_VARIANT_PERSIST4, RT_VARIANT_PERSIST, RT_VARIANT_SHPOOL,
+        const int md[7] = {RT_VARIANT_PERSIST, RT_VARIANT_PERSIST4, RT_VARIANT_PERSIST, pool_v,
                            RT_VARIANT_COOP4,   RT_VARIANT_COOP2,    RT_VARIANT_FAN};
         const int cp[7] = {0, 0, 2, 0, 0, 0, 0};
         for (int i = 0; i < 7 && T.n < rt_ctx::TUNE_MAX; i++)
@@ -1433,7 +1452,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                                      f->bounces, f->spp, n_frames, f->dealing, f->waves_cap};
         }
         rt_ctx::BatchRule& b = *br;
-        const int cand[2] = {RT_VARIANT_PERSIST4, RT_VARIANT_SHPOOL};
+        const int cand[2] = {RT_VARIANT_PERSIST4, pool_v};
         const int nc = 2;
         int pick = -1;
         if (b.choice < 0) {
@@ -1461,8 +1480,9 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                     for (int c = 1; c < nc; c++)
                         if (ms[c] < ms[b.choice]) b.choice = c;
                     if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1)
-                        std::fprintf(stderr, "[prt batch] %dx%d f%d spp%d: persist4 %.3f ms, shpool %.3f ms -> %s\n",
-                                     f->width, f->n_rows, n_frames, f->spp, ms[0], ms[1], variant_name(cand[b.choice]));
+                        std::fprintf(stderr, "[prt batch] %dx%d f%d spp%d: persist4 %.3f ms, %s %.3f ms -> %s\n",
+                                     f->width, f->n_rows, n_frames, f->spp, ms[0], variant_name(cand[1]), ms[1],
+                                     variant_name(cand[b.choice]));
                 } else if (q != hipErrorNotReady) {
                     return fail(ctx, q, "rt_render: batch rule trials");
                 } else {
@@ -1473,7 +1493,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         if (b.choice >= 0) {
             mode = cand[b.choice];
         } else {
-            mode = pick >= 0 ? cand[pick] : (pool_rule ? RT_VARIANT_SHPOOL : RT_VARIANT_PERSIST4);
+            mode = pick >= 0 ? cand[pick] : (pool_rule ? pool_v : RT_VARIANT_PERSIST4);
             li.trial = 1;
             li.settled = 0;
         }
@@ -1567,6 +1587,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             if (!keep) {
                 h.nc = 0;
                 auto add = [&](int pct, int lanes, bool fan, int cold, bool lpt) {
+                    if (cold == RT_VARIANT_SHPOOL) cold = pool_v;  // (HYBRID_CANDS: "the pool kernel")
                     if (h.nc >= rt_ctx::Hybrid::NCAND || !usable(cold)) return;
                     h.pct[h.nc] = pct;
                     h.lanes[h.nc] = lanes;

@@ -883,7 +883,7 @@ __device__ __forceinline__ v3 primary_dir(const KArgs& A, float fx, float fy) {
 
 // the shadow-pool kernels' pixel (rt_shpool.hpp, RT_VARIANT_SHPOOL): every lane of the wave calls it
 struct UCtr;
-template <int MAXB, bool COUNT, bool SPP1>
+template <int MAXB, bool COUNT, bool SPP1, int SHP>
 __device__ __forceinline__ void render_pixel_shp(const KArgs& A, const Cam& C, int frame, int x, int k, bool valid,
                                                  int* __restrict__ stk, Ctr& c, UCtr& u, int* __restrict__ sstk,
                                                  int wcap);
@@ -990,12 +990,12 @@ __device__ __forceinline__ bool next_item(const KArgs& A, int lane, int& reg, in
 // DYN: the wide walk's stack in dynamic LDS sized to the scene's wide depth (2 * wcap ints per lane instead
 // of STACK = 34) and the binary walks' (rare strict fallbacks) in global memory, so that more workgroups
 // fit a CU's LDS: the kernels with OCC > 4 waves per SIMD.
-template <bool SHP> struct UCtrSel { struct type {}; };
-template <> struct UCtrSel<true> { using type = UCtr; };
-template <bool SHP> using UCtrOf = typename UCtrSel<SHP>::type;
+template <int SHP> struct UCtrSel { using type = UCtr; };
+template <> struct UCtrSel<0> { struct type {}; };
+template <int SHP> using UCtrOf = typename UCtrSel<SHP>::type;
 
 template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int OCC = 3, bool TRACE = false, bool BATCH = false,
-          int PB = 0, bool DYN = false, bool SPP1 = false, bool SHP = false>
+          int PB = 0, bool DYN = false, bool SPP1 = false, int SHP = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(OCC > 0 ? OCC : 1)))
 void k_persist(KArgs A) {
     static_assert(PB != 2 || DYN, "an LDS path buffer lives in the DYN kernels' dynamic LDS");
@@ -1033,8 +1033,8 @@ void k_persist(KArgs A) {
         const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
         if (TRACE) t0 = __builtin_amdgcn_s_memrealtime();
         if constexpr (SHP)
-            render_pixel_shp<MAXB, COUNT, SPP1>(A, cam_of<BATCH>(A, frame), frame, x, k, x < A.W && k < A.n_rows, stk, c,
-                                                u, sstk, wcap);
+            render_pixel_shp<MAXB, COUNT, SPP1, SHP>(A, cam_of<BATCH>(A, frame), frame, x, k, x < A.W && k < A.n_rows,
+                                                     stk, c, u, sstk, wcap);
         else if (x < A.W && k < A.n_rows)
             render_pixel<MAXB, STRICT, COUNT, REG, 1, PB, SPP1>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, 0u, sstk,
                                                                 wcap);

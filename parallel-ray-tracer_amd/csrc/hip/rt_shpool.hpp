@@ -72,30 +72,36 @@ __device__ __forceinline__ void flush_u(const UCtr& u, unsigned long long* g) {
         if (v[i]) atomicAdd(g + at[i], (unsigned long long)v[i]);
 }
 
-// The shadow rays of one bounce level of the wave's paths, walked as a wave-level pool.
-// okm: bit j = this lane's path hit a surface at this level and light j passed the back-face test (dot(L - ip, n)
-// >= 0, the reference's early-out, raytracer.c:66-67; failing lights are not walked). lvl: the wave's 64 path-buffer
-// slots of this level (LDS); the owner lane p has stored its hit point in lvl[p].xyz and 0 in lvl[p].w, and the
-// walkers set bit j of lvl[p].w (as an unsigned) when light j is visible from it along the reference's shadow ray.
-// regroup: idle lanes that trigger a refill (all lanes idle always do). Called by every lane of the wave.
-template <bool COUNT>
-__device__ __forceinline__ void shadow_pool(const DScene& s, unsigned okm, float4* lvl, int* __restrict__ stk,
+// The shadow rays of LV bounce levels of the wave's paths, walked as ONE wave-level pool.
+// okm[l]: bit j = this lane's path hit a surface at level l and light j passed the back-face test (dot(L - ip, n)
+// >= 0, the reference's early-out, raytracer.c:66-67; failing lights are not walked). lvl: the wave's path-buffer
+// slots of those levels (LDS, [level][lane]); the owner lane p has stored its level-l hit point in lvl[64 l + p].xyz
+// and 0 in its .w, and the walkers set bit j of that .w (as an unsigned) when light j is visible from it along the
+// reference's shadow ray. regroup: idle lanes that trigger a refill (all lanes idle always do). Called by every lane
+// of the wave.
+template <bool COUNT, int LV>
+__device__ __forceinline__ void shadow_pool(const DScene& s, const unsigned (&okm)[LV], float4* lvl, int* __restrict__ stk,
                                             int* __restrict__ sstk, int wcap, int regroup, Ctr& c, UCtr& u) {
     const unsigned lane = threadIdx.x & 63u;
     const unsigned long long all = uni64(__ballot(1));
     const int nl = s.n_lights;
     const DWide& W = wide_for(s, true);  // |d| = 1: the unit-direction view
-    // the cursor (wave-uniform): light cj, and the owner lanes whose ray toward cj is still unassigned
-    int cj = -1;
+    // the cursor (wave-uniform): level cl, light cj, and the owner lanes whose ray toward it is still unassigned
+    int cl = 0, cj = -1;
     unsigned long long cm = 0;
-    auto advance = [&]() {  // the next light with owners past the back-face test
-        while (cm == 0 && cj + 1 < nl) {
-            cj = uni(cj + 1);
-            cm = uni64(__ballot((okm >> cj) & 1u));
+    auto advance = [&]() {  // the next (level, light) with owners past the back-face test
+        while (cm == 0 && (cl + 1 < LV || cj + 1 < nl)) {
+            if (cj + 1 < nl) {
+                cj = uni(cj + 1);
+            } else {
+                cj = 0;
+                cl = uni(cl + 1);
+            }
+            cm = uni64(__ballot((get_u<LV>(okm, cl) >> cj) & 1u));
             u.shad += (unsigned)__builtin_popcountll(cm);
         }
     };
-    // this lane's ray (owner lane | light << 8) and its walk state (visible_wide's)
+    // this lane's ray (owner lane | level << 6 | light << 9) and its walk state (visible_wide's)
     bool busy = false;
     int wo = 0;
     v3 o = mk(0.0f, 0.0f, 0.0f), d = o;
@@ -118,7 +124,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, unsigned okm, float
                 const unsigned k = __builtin_amdgcn_mbcnt_hi((unsigned)(req >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((unsigned)req, 0u));
                 if (((req >> lane) & 1ull) && k < nav) {
-                    wo = kth_bit(cm, k) | (cj << 8);
+                    wo = kth_bit(cm, k) | (cl << 6) | (cj << 9);
                     got = true;
                 }
                 if (nreq >= nav) {
@@ -133,8 +139,8 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, unsigned okm, float
             if (got) {
                 // the reference's shadow ray, light_v (raytracer.c:62-99) as path_step forms it, from the owner's hit
                 // point (its path-buffer slot)
-                const v3 ipo = xyz(lvl[wo & 63]);
-                const v3 Lp = xyz(s.lights[2 * (wo >> 8)]);
+                const v3 ipo = xyz(lvl[wo & 511]);  // (64 level + owner)
+                const v3 Lp = xyz(s.lights[2 * (wo >> 9)]);
                 v3 l = sub(Lp, ipo);
                 const float mg = mag(l);
                 l = dvs(l, mg);
@@ -145,7 +151,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, unsigned okm, float
                 if (degenerate(d)) {  // zero direction component: the reference's NaN slabs, walked strictly
                     c.fb++;
                     if (visible_walk<true, COUNT, true>(s.ref, o, d, ld2, sstk ? sstk : stk, c))
-                        atomicOr(reinterpret_cast<unsigned*>(lvl + (wo & 63)) + 3, 1u << ((wo >> 8) & 31));
+                        atomicOr(reinterpret_cast<unsigned*>(lvl + (wo & 511)) + 3, 1u << ((wo >> 9) & 31));
                 } else {
                     p = ray_pre(o, d);
                     oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
@@ -159,7 +165,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, unsigned okm, float
         }
         // walk until the wave is idle, or enough of it to refill while work is left: visible_wide's loop, one
         // ballot per step
-        const bool more = cm != 0 || cj + 1 < nl;
+        const bool more = cm != 0 || cj + 1 < nl || cl + 1 < LV;
         for (;;) {
             if (busy) {  // one step of visible_wide
                 unsigned nh, th, imask, nlf;
@@ -193,7 +199,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, unsigned okm, float
                 if (occ || next < 0) {
                     if (!occ && next == -2) c.err++;
                     if (!occ)  // the owner's visibility bit
-                        atomicOr(reinterpret_cast<unsigned*>(lvl + (wo & 63)) + 3, 1u << ((wo >> 8) & 31));
+                        atomicOr(reinterpret_cast<unsigned*>(lvl + (wo & 511)) + 3, 1u << ((wo >> 9) & 31));
                     busy = false;
                 }
             }
@@ -264,7 +270,8 @@ __device__ __forceinline__ v3 trace_path_shp(const KArgs& A, bool alive, v3 o, v
         if (nh) {
             u.skip += nh * (unsigned)s.n_lights;  // less the rays walked (shadow_pool counts those in u.shad)
             const unsigned sh0 = u.shad;
-            shadow_pool<COUNT>(s, okm, pbw + it * 64, stk, sstk, wcap, A.regroup, c, u);
+            const unsigned okl[1] = {okm};
+            shadow_pool<COUNT, 1>(s, okl, pbw + it * 64, stk, sstk, wcap, A.regroup, c, u);
             u.skip -= u.shad - sh0;
         }
         if (hit >= 0) {  // raytracer.c:144-172 as path_step, the lights' visibility from the pool
@@ -318,12 +325,147 @@ __device__ __forceinline__ v3 trace_path_shp(const KArgs& A, bool alive, v3 o, v
     return fold_pb<MAXB>(s, pb, L, tail);
 }
 
+// trace_path_shp with ONE pool for every level's shadow rays (RT_VARIANT_SHDEFER): a path's closest hits are walked
+// level by level first -- the reflection ray of level i needs level i's hit point and normal, never its shadow rays --
+// and then the shadow rays of all its levels, every pixel's and every light's, form one pool, so a tile pays one
+// pool tail instead of one per level and the few shadow rays of the deep levels fill the lanes together with the
+// others. The levels' colours follow in the reference's order (path_step's expressions, level 0 first, each with its
+// own direction: the primary one, then each level's reflection, recomputed), then the deepest-first fold. The path
+// buffer holds a level's hit point and visibility word (then its colour and material), and a second [level][lane]
+// array its hit triangle (orig | nd << 30, -1: a miss).
+template <int MAXB, bool COUNT>
+__device__ __forceinline__ v3 trace_path_dfr(const KArgs& A, bool alive, v3 o, v3 d, int* __restrict__ stk, Ctr& c,
+                                             UCtr& u, int hpix, int* __restrict__ sstk, int wcap) {
+    extern __shared__ int lds_dyn[];
+    float4* pb0 = (float4*)(lds_dyn + 2 * wcap * BLOCK);
+    const size_t wl = (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
+    float4* pb = pb0 + wl;
+    float4* pbw = pb - (threadIdx.x & 63);  // the wave's slots of level 0
+    int* hid = (int*)(pb0 + (size_t)BLOCK * MAXB) + wl;
+    const DScene& s = A.s;
+    const v3 amb = mk(s.amb_x, s.amb_y, s.amb_z);
+    const v3 d0 = d;
+    unsigned okm[MAXB];
+#pragma unroll
+    for (int k = 0; k < MAXB; k++) okm[k] = 0u;
+    int L = 0;
+    bool tail = false;
+    unsigned nhits = 0;
+    for (int it = 0; it < A.bounces; ++it) {  // the closest hits of every level (raytracer.c:101-147, 163-172)
+        const unsigned na = popc_wave(alive);
+        if (na == 0) break;
+        if (COUNT) c.lvl = (unsigned)it;
+        if (it == 0) u.prim += na;
+        else u.refl += na;
+        bool hitl = false;
+        if (alive) {
+            float best;
+            int nd;
+            const int orig = closest<false, COUNT, true>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0);
+            if (hpix >= 0) {
+                if (it == 0) {
+                    if (A.hit) A.hit[hpix] = orig;
+                    if (A.t) A.t[hpix] = best;
+                }
+                if (A.bounce_hit) A.bounce_hit[(size_t)hpix * A.bounces + it] = orig;
+            }
+            if (orig < 0) {  // raytracer.c:132-135
+                pb[it * 64] = make_float4(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z, __int_as_float(0));
+                hid[it * 64] = -1;
+                L = it + 1;
+                tail = false;
+                alive = false;
+            } else {
+                hitl = true;
+                const v3 ip = add(o, mul(d, best));
+                const float4 sh0 = s.shade[2 * orig], sh1 = s.shade[2 * orig + 1];
+                const int m = __float_as_int(sh0.w);
+                const v3 n = nd ? xyz(sh1) : xyz(sh0);
+                unsigned ok = 0;
+                for (int j = 0; j < s.n_lights; ++j) {  // light_v's back-face test (raytracer.c:66-67)
+                    const v3 tmp2 = sub(xyz(s.lights[2 * j]), ip);
+                    ok |= dot(tmp2, n) < 0 ? 0u : (1u << j);
+                }
+                set_u<MAXB>(okm, it, ok);
+                pb[it * 64] = make_float4(ip.x, ip.y, ip.z, __uint_as_float(0u));
+                hid[it * 64] = orig | (nd ? (1 << 30) : 0);
+                const v3 ns = mul(n, 2.0f * __builtin_fabsf(dot(d, n)));  // (dd = -(-d) = d exactly)
+                const v3 r = normalize(add(d, ns));
+                const v3 kr = xyz(s.mats[3 * m + 2]);
+                if (!(mag(kr) > 0.0f)) {  // raytracer.c:168
+                    L = it + 1;
+                    tail = false;
+                    alive = false;
+                } else if (it + 1 == A.bounces) {  // raytrace(.., BOUNCES) returns {0,0,0}: col += kr * 0
+                    L = it + 1;
+                    tail = true;
+                    alive = false;
+                } else {
+                    o = ip;
+                    d = r;
+                }
+            }
+        }
+        const unsigned nh = popc_wave(hitl);
+        u.hits += nh;
+        nhits += nh;
+    }
+    if (nhits) {  // every level's shadow rays as one pool
+        u.skip += nhits * (unsigned)s.n_lights;
+        const unsigned sh0 = u.shad;
+        shadow_pool<COUNT, MAXB>(s, okm, pbw, stk, sstk, wcap, A.regroup, c, u);
+        u.skip -= u.shad - sh0;
+    }
+    v3 dl = d0;  // level i's direction: the primary one, then each level's reflection
+    for (int it = 0; it < L; ++it) {  // the levels' colours (raytracer.c:144-160 as path_step), in order
+        const int h = hid[it * 64];
+        if (h < 0) break;  // a miss: its colour is in place (and it was the path's last level)
+        const float4 e = pb[it * 64];
+        const v3 ip = xyz(e);
+        const unsigned vis = __float_as_uint(e.w) & get_u<MAXB>(okm, it);
+        const int orig = h & ((1 << 30) - 1);
+        const float4 sh0 = s.shade[2 * orig], sh1 = s.shade[2 * orig + 1];
+        const int m = __float_as_int(sh0.w);
+        const v3 n = (h >> 30) ? xyz(sh1) : xyz(sh0);
+        const v3 kd0 = xyz(s.mats[3 * m + 1]);
+        v3 col = mk(0.0f + kd0.x * amb.x, 0.0f + kd0.y * amb.y, 0.0f + kd0.z * amb.z);
+        const v3 v = mul(dl, -1.0f);
+        for (int j = 0; j < s.n_lights; ++j) {
+            const v3 Lp = xyz(s.lights[2 * j]);
+            v3 l = sub(Lp, ip);
+            float mg = mag(l);
+            l = dvs(l, mg);
+            mg *= mg;
+            const int V = (int)((vis >> j) & 1u);
+            const v3 kl = xyz(s.lights[2 * j + 1]);
+            const v3 ks = xyz(s.mats[3 * m]), kd = xyz(s.mats[3 * m + 1]);
+            const float ndl = dot(n, l);
+            const v3 hv = normalize(add(l, v));
+            const float coeff = fmaxf(0.0f, dot(n, hv));
+            const v3 cr = mk(kd.x * fmaxf(0.0f, ndl) + ks.x * coeff, kd.y * fmaxf(0.0f, ndl) + ks.y * coeff,
+                             kd.z * fmaxf(0.0f, ndl) + ks.z * coeff);
+            const float fV = (float)V;
+            col.x = col.x + fV * kl.x * cr.x / mg;
+            col.y = col.y + fV * kl.y * cr.y / mg;
+            col.z = col.z + fV * kl.z * cr.z / mg;
+        }
+        pb[it * 64] = make_float4(col.x, col.y, col.z, __int_as_float(m));
+        const v3 dd = mul(v, -1.0f);
+        dl = normalize(add(dd, mul(n, 2.0f * __builtin_fabsf(dot(dd, n)))));
+    }
+    return fold_pb<MAXB>(s, pb, L, tail);
+}
+
 // render_pixel (rt_kernels.hpp) for the shadow-pool kernels: called by EVERY lane of the wave (valid = the lane
 // holds a pixel of the frame), so that the path loop and the pool run in uniform control flow
-template <int MAXB, bool COUNT, bool SPP1>
+template <int MAXB, bool COUNT, bool SPP1, int SHP>
 __device__ __forceinline__ void render_pixel_shp(const KArgs& A, const Cam& C, int frame, int x, int k, bool valid,
                                                  int* __restrict__ stk, Ctr& c, UCtr& u, int* __restrict__ sstk,
                                                  int wcap) {
+    auto trace = [&](v3 d, int hp) {
+        if constexpr (SHP == 2) return trace_path_dfr<MAXB, COUNT>(A, valid, C.pos, d, stk, c, u, hp, sstk, wcap);
+        else return trace_path_shp<MAXB, COUNT>(A, valid, C.pos, d, stk, c, u, hp, sstk, wcap);
+    };
     const int y = image_row(A, k, frame);
     valid = valid && y < A.H;  // frame_shift: a rotated rank's compact rows past the image
     u.pix += popc_wave(valid);
@@ -333,8 +475,7 @@ __device__ __forceinline__ void render_pixel_shp(const KArgs& A, const Cam& C, i
         for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
     v3 col;
     if (SPP1 || A.spp <= 1) {
-        col = clamp01(trace_path_shp<MAXB, COUNT>(A, valid, C.pos, primary_dir(C, (float)x, (float)y), stk, c, u,
-                                                  hpix, sstk, wcap));
+        col = clamp01(trace(primary_dir(C, (float)x, (float)y), hpix));
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples; hit / t from the first sample
         const int g = A.spp_grid;
         v3 acc = mk(0.0f, 0.0f, 0.0f);
@@ -342,8 +483,7 @@ __device__ __forceinline__ void render_pixel_shp(const KArgs& A, const Cam& C, i
             for (int si = 0; si < g; ++si) {
                 const float fx = (float)x + ((float)si + 0.5f) / (float)g;
                 const float fy = (float)y + ((float)sj + 0.5f) / (float)g;
-                const v3 cs = clamp01(trace_path_shp<MAXB, COUNT>(A, valid, C.pos, primary_dir(C, fx, fy), stk, c, u,
-                                                                  si == 0 && sj == 0 ? hpix : -1, sstk, wcap));
+                const v3 cs = clamp01(trace(primary_dir(C, fx, fy), si == 0 && sj == 0 ? hpix : -1));
                 acc = add(acc, cs);
             }
         const float nn = (float)(g * g);

@@ -15,7 +15,7 @@ P = ctypes.POINTER
 KERNELS = {"auto": 0, "strict": 1, "fast": 2}
 # rt_frame.variant (launch configurations of the fast kernel, include/rt_hip.h); a variant name is also
 # accepted as `kernel` (kernel="coop4" == kernel="fast", variant="coop4")
-VARIANTS = {"default": 0, "persist": 1, "persist4": 2, "coop2": 4, "coop4": 5, "fan": 7, "hybrid": 11, "shpool": 13}
+VARIANTS = {"default": 0, "persist": 1, "persist4": 2, "coop2": 4, "coop4": 5, "fan": 7, "hybrid": 11, "shpool": 13, "shdefer": 15}
 VARIANT_NAMES = {v: k for k, v in VARIANTS.items()}
 HOT_KERNELS = {"coop4": 0, "coop2": 1, "fan": 2}  # rt_frame.hot_kernel (RT_HOT_*)
 DEALING = {"default": 0, "global": 1, "rows": 2, "columns": 3, "blocks": 4, "row_major": 5}

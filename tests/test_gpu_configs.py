@@ -118,7 +118,7 @@ def test_config_single_frame_vs_reference(name, W, H, tag, kernel):
     assert st["stack_overflows"] == 0
 
 
-@pytest.mark.parametrize("variant", ["default", "persist4", "shpool"])
+@pytest.mark.parametrize("variant", ["default", "persist4", "shpool", "shdefer"])
 @pytest.mark.parametrize("name,W,H,tag", CONFIGS)
 def test_config_bench_batch_vs_reference(name, W, H, tag, variant):
     """bench.py's instantiation (4 frames of its camera path in one rt_render_frames launch, BGRA8 only) against
@@ -139,7 +139,7 @@ def test_config_bench_batch_vs_reference(name, W, H, tag, variant):
         if variant == "default" and r.launch_info()["settled"]:
             break
     if variant == "default":
-        assert r.launch_info()["settled"] and r.launch_info()["variant"] in ("persist4", "shpool"), r.launch_info()
+        assert r.launch_info()["settled"] and r.launch_info()["variant"] in ("persist4", "shpool", "shdefer"), r.launch_info()
     frames = px.cpu().numpy().view(np.uint32)
     r.close()
     ref = np.load(os.path.join(GOLD, f"{name}_{tag}_strict_sample.npz"))

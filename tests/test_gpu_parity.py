@@ -20,8 +20,8 @@ RGB_TOL = 1e-5
 # with its default rule ("fast"), and each variant forced: k_persist at 4 waves/SIMD ("persist4"), k_coop
 # ("coopG": G lanes per ray), k_fan ("fan":
 # 1 + lights lanes per pixel). "shpool": k_persist with each level's shadow rays walked as a per-wave pool
-# (rt_shpool.hpp).
-KERNELS = ["strict", "fast", "persist4", "coop2", "coop4", "fan", "shpool"]
+# (rt_shpool.hpp); "shdefer": one pool for all levels' shadow rays.
+KERNELS = ["strict", "fast", "persist4", "coop2", "coop4", "fan", "shpool", "shdefer"]
 
 
 def select(kernel):
@@ -190,7 +190,7 @@ def test_spp_matches_oracle(dev, scenes, spp, kernel):
     assert out["stats"]["primary"] == 64 * 36 * spp
 
 
-@pytest.mark.parametrize("kernel", ["default", "shpool", "persist4"])
+@pytest.mark.parametrize("kernel", ["default", "shpool", "shdefer", "persist4"])
 @pytest.mark.parametrize("spp", [4, 16])
 def test_spp_of_a_two_light_scene_matches_oracle(dev, spp, kernel):
     """the default rule sends spp > 1 frames of 2+-light scenes through the shadow pool's multi-sample path

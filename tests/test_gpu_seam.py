@@ -98,7 +98,7 @@ def test_single_frame_rule_settles_on_a_moving_camera(dev):
     assert first <= 1 + 3 * 5 + 2, (first, infos[:first + 1])
     assert all(x["settled"] and not x["trial"] for x in infos[first:first + 60]), infos
     assert infos[0]["trial"] == 1 and infos[0]["variant"] == "persist"  # the measuring frame
-    assert infos[-1]["variant"] in ("persist", "shpool", "hybrid")
+    assert infos[-1]["variant"] in ("persist", "shpool", "shdefer", "hybrid")
 
 
 @pytest.mark.parametrize("name", ["dragon", "car_boxed"])
@@ -125,9 +125,9 @@ def test_frame_batches_with_changing_cameras(dev, name):
 
 @pytest.mark.parametrize("name", ["dragon", "two_cars"])
 def test_batch_rule_settles_on_the_faster_kernel(dev, name):
-    """frame batches under the default rule: PERSIST4 and the shadow pool are tried twice each on the first launches
-    of the shape, then the faster renders; launch_info reports the trials and the choice; every launch's frames are
-    the same bits"""
+    """frame batches under the default rule: PERSIST4 and the shadow pool (the all-levels pool where its path buffer
+    fits, as on dragon) are tried twice each on the first launches of the shape, then the faster renders; launch_info
+    reports the trials and the choice; every launch's frames are the same bits"""
     W, H, n = 320, 180, 8
     s = host.Scene.named(name).build_bvh(3)
     cams = [walk(W, H, i) for i in range(n)]
@@ -146,5 +146,6 @@ def test_batch_rule_settles_on_the_faster_kernel(dev, name):
         np.testing.assert_array_equal(got, ref, err_msg=str(k))
     r.close()
     tried = [x["variant"] for x in seen[:4]]
-    assert tried == ["persist4", "shpool"] * 2 and all(x["trial"] for x in seen[:4]), seen
+    pool = "shdefer" if name == "dragon" else tried[1]
+    assert tried == ["persist4", pool] * 2 and pool in ("shpool", "shdefer") and all(x["trial"] for x in seen[:4]), seen
     assert seen[4]["settled"] and all(x["settled"] and x["variant"] == seen[4]["variant"] for x in seen[4:]), seen

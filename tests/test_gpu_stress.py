@@ -23,7 +23,7 @@ from prt import host
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 G = json.load(open(os.path.join(GOLD, "golden.json")))
-KERNELS = ["strict", "fast", "persist4", "coop4", "fan", "shpool"]
+KERNELS = ["strict", "fast", "persist4", "coop4", "fan", "shpool", "shdefer"]
 _SCENES = {}
 
 
@@ -78,7 +78,7 @@ def test_high_triangle_count_small_frames(name, kernel):
     assert md5.hexdigest() == G["standin"][name]["320x180_md5"]
 
 
-@pytest.mark.parametrize("kernel", ["fast", "persist4", "shpool"])
+@pytest.mark.parametrize("kernel", ["fast", "persist4", "shpool", "shdefer"])
 @pytest.mark.parametrize("name", ["dragon", "sportscar", "dragon871k"])
 def test_high_triangle_count_1080p_vs_reference(name, kernel):
     """the whole 1080p frame: every 97th pixel against the reference's values, the frame's md5 against the
