@@ -938,7 +938,7 @@ KFn persist4(bool pbl, bool spp1, bool count) {
 // (and, for the all-levels pool, each level's hit triangle)
 template <int MAXB>
 size_t pbl_bytes(const rtd::KArgs& A, int shp = 0) {
-    return sizeof(int) * 2 * (size_t)A.wcap * rtd::BLOCK + sizeof(float4) * rtd::BLOCK * MAXB +
+    return sizeof(int) * (size_t)rtd::wstack_words(A.wcap, shp > 0) * rtd::BLOCK + sizeof(float4) * rtd::BLOCK * MAXB +
            (shp == 2 ? sizeof(int) * rtd::BLOCK * MAXB : 0);
 }
 // Does that layout fit 4 workgroups per CU for this scene? (the LDS path buffer measured 1.2 % faster than the global
@@ -968,16 +968,18 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
     dyn = 0;
     if (A.tile_trace)
         return count ? rtd::k_persist<MAXB, false, true, true, 3, true, true> : rtd::k_persist<MAXB, false, false, true, 3, true, true>;
-    if (variant == RT_VARIANT_SHDEFER && pbl_fits<MAXB>(A, device, 2)) {
-        dyn = pbl_bytes<MAXB>(A, 2);
-        return persist4<MAXB, 2>(true, A.spp <= 1, count);
+    if (variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) {
+        const int shp = variant == RT_VARIANT_SHDEFER ? 2 : 1;
+        if (pbl_fits<MAXB>(A, device, shp)) {
+            dyn = pbl_bytes<MAXB>(A, shp);
+            return shp == 2 ? persist4<MAXB, 2>(true, A.spp <= 1, count) : persist4<MAXB, 1>(true, A.spp <= 1, count);
+        }
     }
     if (variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) {
         const bool pbl = pbl_fits<MAXB>(A, device);
         if (pbl) dyn = pbl_bytes<MAXB>(A);
         // (the bench's batches: the spp = 1 build)
-        return variant == RT_VARIANT_SHPOOL && pbl ? persist4<MAXB, 1>(true, A.spp <= 1, count)
-                                                   : persist4<MAXB, 0>(pbl, A.spp <= 1, count);
+        return persist4<MAXB, 0>(pbl, A.spp <= 1, count);
     }
     return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true> : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
 }
@@ -1317,7 +1319,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     const int fan_r = ctx->n_lights <= 1 ? 2 : ctx->n_lights <= 3 ? 4 : 8;  // lanes per pixel: 1 + lights
     // the shadow pool: 1..32 lights (a 32-bit visibility word per pixel) and the LDS path buffer at 4 workgroups per CU
     const bool shp_ok = wide_ok && ctx->n_lights >= 1 && ctx->n_lights <= 32 &&
-                        (f->bounces <= 4 ? pbl_fits<4>(A, ctx->device) : pbl_fits<8>(A, ctx->device));
+                        std::max(ctx->wide_n, std::max(ctx->unit_n, ctx->prim_n)) <= rtd::WIDE_MAX_NODES &&  // (packed stack)
+                        (f->bounces <= 4 ? pbl_fits<4>(A, ctx->device, 1) : pbl_fits<8>(A, ctx->device, 1));
     const bool shd_ok = shp_ok && (f->bounces <= 4 ? pbl_fits<4>(A, ctx->device, 2) : pbl_fits<8>(A, ctx->device, 2));
     auto usable = [&](int v) {
         if (A.tile_trace) return v == RT_VARIANT_PERSIST;  // (diagnostics: the 3-wave kernel's tile trace)

@@ -285,7 +285,14 @@ __device__ __forceinline__ bool visible_walk(const DBvh& B, v3 o, v3 d, float ld
 // hit bits) popped child by child in the order k ^ octant(ray) (near first, no sort).
 // Same result semantics as closest_walk<false>: min t over all triangles, boxes pruned at
 // best * PRUNE_SLACK so that exact ties are always met and reported.
-constexpr int WSTACK = 16;  // node-group entries (2 ints) in the STACK-int LDS column; builder depth <= 16
+constexpr int WSTACK = 16;  // node-group entries in the STACK-int LDS column; builder depth <= 16
+// A stack entry is two words (child base; interior mask << 8 | hit bits). PK (the shadow-pool kernels): one word
+// (child base << 8 | hit bits) plus the interior mask as one byte, four entries' bytes to a word after the wcap entry
+// words -- 5 bytes per entry, so that the all-levels pool's path buffer fits 4 workgroups per CU beside the stack of
+// deeper trees (sportscar depth 14, two_cars 12) -- at 4 more VALU per push / pop (PERSIST4 with it: 1.1-1.5 % slower,
+// so only the pool kernels pack). The packed child base has 24 bits: wide trees of at most WIDE_MAX_NODES nodes.
+constexpr int WIDE_MAX_NODES = 1 << 24;
+__host__ __device__ constexpr int wstack_words(int wcap, bool pk) { return pk ? wcap + (wcap + 3) / 4 : 2 * wcap; }
 // A child box left before t = EPS holds no hit: hit_triangle accepts t > EPS only (raytracer.c:56), and the
 // computed far plane lies beyond the true box by the inflation (>= 20x the triangle test's rounding of t), so
 // every triangle point inside has t below the computed exit. Testing the interval from EPS instead of 0 prunes
@@ -399,22 +406,35 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
 // of the stack (pushing / re-pushing the rest). It does not depend on this node's triangle tests, so
 // the walks issue its loads BEFORE those tests and their latency overlaps them. -1: walk done; -2: stack
 // overflow (reported, never silent).
+template <bool PK = false>
 __device__ __forceinline__ int wide_next(unsigned nh, int cb, unsigned imask, unsigned oct, int& sp,
                                          int* __restrict__ stk, int wcap = WSTACK) {
     if (!nh) {
         if (sp == 0) return -1;
         --sp;
-        cb = stk[(2 * sp) * BLOCK];
-        const unsigned bits = (unsigned)stk[(2 * sp + 1) * BLOCK];
-        imask = bits >> 8;
-        nh = bits & 0xFFu;
+        if constexpr (PK) {
+            const unsigned e = (unsigned)stk[sp * BLOCK];
+            cb = (int)(e >> 8);
+            nh = e & 0xFFu;
+            imask = reinterpret_cast<const unsigned char*>(stk + (wcap + (sp >> 2)) * BLOCK)[sp & 3];
+        } else {
+            cb = stk[(2 * sp) * BLOCK];
+            const unsigned bits = (unsigned)stk[(2 * sp + 1) * BLOCK];
+            imask = bits >> 8;
+            nh = bits & 0xFFu;
+        }
     }
     const unsigned slot = (unsigned)__builtin_ctz(nh) ^ oct;
     nh &= nh - 1u;
     if (nh) {
         if (sp >= wcap) return -2;
-        stk[(2 * sp) * BLOCK] = cb;
-        stk[(2 * sp + 1) * BLOCK] = (int)((imask << 8) | nh);
+        if constexpr (PK) {
+            stk[sp * BLOCK] = (int)(((unsigned)cb << 8) | nh);
+            reinterpret_cast<unsigned char*>(stk + (wcap + (sp >> 2)) * BLOCK)[sp & 3] = (unsigned char)imask;
+        } else {
+            stk[(2 * sp) * BLOCK] = cb;
+            stk[(2 * sp + 1) * BLOCK] = (int)((imask << 8) | nh);
+        }
         ++sp;
     }
     return cb + __popc(imask & ((1u << slot) - 1u));
@@ -422,7 +442,7 @@ __device__ __forceinline__ int wide_next(unsigned nh, int cb, unsigned imask, un
 
 // PIPE: software-pipeline the leaf triangles (the next triangle's loads issued before this one's test);
 // pays where registers allow (the split kernels), not in k_persist (spills at its 168-VGPR cap).
-template <bool COUNT, bool PIPE = false>
+template <bool COUNT, bool PIPE = false, bool PK = false>
 __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& best, int& hp, int& nd, bool& tie,
                                              int* __restrict__ stk, Ctr& c, int wcap = WSTACK) {
     const RayPre p = ray_pre(o, d);
@@ -439,7 +459,7 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
             c.nb += 10;
             count_step(c, false);
         }
-        const int next = wide_next(nh, cb, imask, oct, sp, stk, wcap);
+        const int next = wide_next<PK>(nh, cb, imask, oct, sp, stk, wcap);
         // the next node's loads go out before this node's triangle tests, unconditionally (a walk that has ended
         // reloads the root): a load under a branch is copied into the merged register right after it, and that
         // copy waits for the load (dragon 0.712 -> 0.689 ms per frame, sportscar 0.931 -> 0.901, car_boxed 0.870 -> 0.858)
@@ -501,7 +521,7 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
     }
 }
 
-template <bool COUNT, bool PIPE = false>
+template <bool COUNT, bool PIPE = false, bool PK = false>
 __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c,
                                              int wcap = WSTACK) {
     const RayPre p = ray_pre(o, d);
@@ -520,7 +540,7 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
             c.nb += 10;
             count_step(c, true);
         }
-        const int next = wide_next(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
+        const int next = wide_next<PK>(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
         N = wload(W, next >= 0 ? next : 0);  // unconditional (closest_wide)
         if (!PIPE) {
             while (th) {
@@ -585,7 +605,7 @@ __device__ __forceinline__ const DWide& wide_for(const DScene& s, bool unit) {
 // Closest hit with the kernel's policy; returns the ORIGINAL triangle index (-1 = miss).
 // sstk (nullable): the binary walks' stack when the wide walk's `stk` holds only wcap entries (DYN kernels)
 // unit: d has unit length (a reflection ray): the unit-direction view serves the fast walk
-template <bool STRICT, bool COUNT, bool REG = true, bool PIPE = false>
+template <bool STRICT, bool COUNT, bool REG = true, bool PIPE = false, bool PK = false>
 __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best, int& nd, int* __restrict__ stk,
                                        Ctr& c, int* __restrict__ sstk = nullptr, int wcap = WSTACK, bool unit = false) {
     int* __restrict__ bstk = sstk ? sstk : stk;
@@ -596,7 +616,7 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
     if (!STRICT && !degenerate(d)) {
         if (s.wide.nodes) {
             const DWide& W = wide_for(s, unit);
-            closest_wide<COUNT, PIPE>(W, o, d, best, hp, nd, tie, stk, c, wcap);
+            closest_wide<COUNT, PIPE, PK>(W, o, d, best, hp, nd, tie, stk, c, wcap);
             if (!tie) return hp >= 0 ? W.tri_orig[hp] : -1;
         } else {
             closest_walk<false, COUNT, REG>(s.acc, o, d, best, hp, nd, tie, bstk, c);
@@ -818,7 +838,7 @@ __device__ v3 trace_path(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, Ctr&
     float4* pb = nullptr;
     if constexpr (PB == 2) {
         extern __shared__ int lds_dyn[];
-        pb = (float4*)(lds_dyn + 2 * wcap * BLOCK) + (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
+        pb = (float4*)(lds_dyn + wstack_words(wcap, false) * BLOCK) + (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
     } else if constexpr (PB) {  // [wave][level][lane] (persistent grids: a wave's slot is its own for the launch)
         pb = A.pathbuf + ((size_t)(blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6)) * MAXB) * 64 + (threadIdx.x & 63);
     } else {
@@ -987,7 +1007,7 @@ __device__ __forceinline__ bool next_item(const KArgs& A, int lane, int& reg, in
     return false;
 }
 
-// DYN: the wide walk's stack in dynamic LDS sized to the scene's wide depth (2 * wcap ints per lane instead
+// DYN: the wide walk's stack in dynamic LDS sized to the scene's wide depth (wstack_words ints per lane instead
 // of STACK = 34) and the binary walks' (rare strict fallbacks) in global memory, so that more workgroups
 // fit a CU's LDS: the kernels with OCC > 4 waves per SIMD.
 template <int SHP> struct UCtrSel { using type = UCtr; };

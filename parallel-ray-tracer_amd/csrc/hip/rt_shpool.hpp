@@ -177,7 +177,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, const unsigned (&ok
                     c.nb += 10;
                     count_step(c, true);
                 }
-                const int next = wide_next(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
+                const int next = wide_next<true>(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
                 N = wload(W, next >= 0 ? next : 0);  // unconditional (closest_wide)
                 bool occ = false;
                 while (th) {
@@ -221,7 +221,7 @@ template <int MAXB, bool COUNT>
 __device__ __forceinline__ v3 trace_path_shp(const KArgs& A, bool alive, v3 o, v3 d, int* __restrict__ stk, Ctr& c,
                                              UCtr& u, int hpix, int* __restrict__ sstk, int wcap) {
     extern __shared__ int lds_dyn[];
-    float4* pb = (float4*)(lds_dyn + 2 * wcap * BLOCK) + (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
+    float4* pb = (float4*)(lds_dyn + wstack_words(wcap, true) * BLOCK) + (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
     float4* pbw = pb - (threadIdx.x & 63);  // the wave's slots of level 0
     const DScene& s = A.s;
     const v3 amb = mk(s.amb_x, s.amb_y, s.amb_z);
@@ -239,7 +239,7 @@ __device__ __forceinline__ v3 trace_path_shp(const KArgs& A, bool alive, v3 o, v
         if (alive) {  // raytracer.c:101-147 as path_step
             float best;
             int nd;
-            const int orig = closest<false, COUNT, true>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0);
+            const int orig = closest<false, COUNT, true, false, true>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0);
             if (hpix >= 0) {
                 if (it == 0) {
                     if (A.hit) A.hit[hpix] = orig;
@@ -337,7 +337,7 @@ template <int MAXB, bool COUNT>
 __device__ __forceinline__ v3 trace_path_dfr(const KArgs& A, bool alive, v3 o, v3 d, int* __restrict__ stk, Ctr& c,
                                              UCtr& u, int hpix, int* __restrict__ sstk, int wcap) {
     extern __shared__ int lds_dyn[];
-    float4* pb0 = (float4*)(lds_dyn + 2 * wcap * BLOCK);
+    float4* pb0 = (float4*)(lds_dyn + wstack_words(wcap, true) * BLOCK);
     const size_t wl = (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
     float4* pb = pb0 + wl;
     float4* pbw = pb - (threadIdx.x & 63);  // the wave's slots of level 0
@@ -361,7 +361,7 @@ __device__ __forceinline__ v3 trace_path_dfr(const KArgs& A, bool alive, v3 o, v
         if (alive) {
             float best;
             int nd;
-            const int orig = closest<false, COUNT, true>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0);
+            const int orig = closest<false, COUNT, true, false, true>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0);
             if (hpix >= 0) {
                 if (it == 0) {
                     if (A.hit) A.hit[hpix] = orig;

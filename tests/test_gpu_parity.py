@@ -397,7 +397,7 @@ def test_cli_drop_in_writes_the_reference_bmp(tmp_path):
     assert len(list(cache.iterdir())) == 2
 
 
-@pytest.mark.parametrize("name,n_cand", [("sportscar", 6), ("car_boxed", 7), ("dragon", 7)])
+@pytest.mark.parametrize("name,n_cand", [("sportscar", 7), ("car_boxed", 7), ("dragon", 7)])
 def test_autotuned_frames_equal_forced_configuration(dev, name, n_cand, monkeypatch, capfd):
     """rt_render's launch autotuner (rt_frame.tune = 1, rt_hip.hip): the trial frame (every candidate, each
     TUNE_REPS times, into the same outputs) and the frames after the decision are bit-exact to a forced
