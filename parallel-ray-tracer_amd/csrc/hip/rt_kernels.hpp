@@ -312,6 +312,19 @@ __device__ __forceinline__ unsigned first_active_lane() {
     return (unsigned)((threadIdx.x & 63u) == (unsigned)__builtin_ctzll(ex));
 }
 
+// Diagnostics build (PRT_DEFS=-DPRT_DIAG_TRI): the lane-count bins q1 / q2 count the wave iterations of the closest /
+// shadow walks' triangle loops instead (their SIMD efficiency = c.cht / (64 q1), c.sht / (64 q2)).
+#ifdef PRT_DIAG_TRI
+#define PRT_TRI_ITER(c, q) \
+    do {                   \
+        if (COUNT) (c).q += first_active_lane(); \
+    } while (0)
+#else
+#define PRT_TRI_ITER(c, q) \
+    do {                   \
+    } while (0)
+#endif
+
 // k_persist's walks (RT_FLAG_COUNTERS): one wave step, by walk kind and by the number of active lanes
 __device__ __forceinline__ void count_step(Ctr& c, bool shadow) {
     const unsigned long long ex = __builtin_amdgcn_read_exec();
@@ -319,10 +332,12 @@ __device__ __forceinline__ void count_step(Ctr& c, bool shadow) {
     const unsigned b = ((unsigned)__builtin_popcountll(ex) - 1u) >> 4;
     c.ws += f;
     if (shadow) c.wsh += f;
+#ifndef PRT_DIAG_TRI
     c.q1 += b == 0 ? f : 0u;
     c.q2 += b == 1 ? f : 0u;
     c.q3 += b == 2 ? f : 0u;
     c.q4 += b == 3 ? f : 0u;
+#endif
     if (c.hist && f) atomicAdd(c.hist + (shadow ? 16u : 0u) + 4u * (c.lvl < 3u ? c.lvl : 3u) + b, 1u);
 }
 
@@ -466,6 +481,7 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
         N = wload(W, next >= 0 ? next : 0);
         if (!PIPE) {
             while (th) {
+                PRT_TRI_ITER(c, q1);
                 const int i = tb + __builtin_ctz(th);
                 th &= th - 1u;
                 int k;
@@ -544,6 +560,7 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
         N = wload(W, next >= 0 ? next : 0);  // unconditional (closest_wide)
         if (!PIPE) {
             while (th) {
+            PRT_TRI_ITER(c, q2);
                 const int i = tb + __builtin_ctz(th);
                 th &= th - 1u;
                 int k;

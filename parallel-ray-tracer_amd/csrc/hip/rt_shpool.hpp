@@ -72,6 +72,16 @@ __device__ __forceinline__ void flush_u(const UCtr& u, unsigned long long* g) {
         if (v[i]) atomicAdd(g + at[i], (unsigned long long)v[i]);
 }
 
+// Packed triangle tests (TQ, the all-levels pool): a wave step's hit leaf slots hold few triangles per lane and the
+// per-lane loop over them runs as long as the lane with the most (dragon: 2.7 loop rounds per pool step at 10 % of the
+// lanes, PRT_DIAG_TRI). When some lane holds 3 or more, the step's (owner lane, triangle) pairs are written to a
+// wave-private LDS queue instead and tested 64 at a time, each by the lane that reads it, with the owner's ray
+// fetched by `ds_bpermute`; occlusion (the reference's per-triangle test, bvh.c:283-290) and the nearest hit (for the
+// walk's box pruning) go back to the owner's LDS slots. Per wave: TQ_CAP jobs, 64 occlusion flags, 64 nearest hits,
+// the queue's counter.
+constexpr int TQ_CAP = 128;
+constexpr int TQ_OCC = TQ_CAP, TQ_T = TQ_CAP + 64, TQ_CNT = TQ_CAP + 128, TQ_WORDS = TQ_CAP + 132;
+
 // The shadow rays of LV bounce levels of the wave's paths, walked as ONE wave-level pool.
 // okm[l]: bit j = this lane's path hit a surface at level l and light j passed the back-face test (dot(L - ip, n)
 // >= 0, the reference's early-out, raytracer.c:66-67; failing lights are not walked). lvl: the wave's path-buffer
@@ -79,10 +89,16 @@ __device__ __forceinline__ void flush_u(const UCtr& u, unsigned long long* g) {
 // and 0 in its .w, and the walkers set bit j of that .w (as an unsigned) when light j is visible from it along the
 // reference's shadow ray. regroup: idle lanes that trigger a refill (all lanes idle always do). Called by every lane
 // of the wave.
-template <bool COUNT, int LV>
+template <bool COUNT, int LV, bool TQ = false>
 __device__ __forceinline__ void shadow_pool(const DScene& s, const unsigned (&okm)[LV], float4* lvl, int* __restrict__ stk,
-                                            int* __restrict__ sstk, int wcap, int regroup, Ctr& c, UCtr& u) {
+                                            int* __restrict__ sstk, int wcap, int regroup, Ctr& c, UCtr& u,
+                                            int* tq = nullptr) {
     const unsigned lane = threadIdx.x & 63u;
+    if constexpr (TQ) {  // this lane's result slots, the queue's counter
+        tq[TQ_OCC + lane] = 0;
+        tq[TQ_T + lane] = (int)__float_as_uint(FMAX);
+        if (lane == 0u) tq[TQ_CNT] = 0;
+    }
     const unsigned long long all = uni64(__ballot(1));
     const int nl = s.n_lights;
     const DWide& W = wide_for(s, true);  // |d| = 1: the unit-direction view
@@ -167,9 +183,11 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, const unsigned (&ok
         // ballot per step
         const bool more = cm != 0 || cj + 1 < nl || cl + 1 < LV;
         for (;;) {
+            unsigned th = 0u;
+            int tb = 0, next = -1;
             if (busy) {  // one step of visible_wide
-                unsigned nh, th, imask, nlf;
-                int cb, tb;
+                unsigned nh, imask, nlf;
+                int cb;
                 wide_node<COUNT>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nlf, SHADOW_ORDER_XOR);
                 if (COUNT) {
                     c.shi++;
@@ -177,10 +195,56 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, const unsigned (&ok
                     c.nb += 10;
                     count_step(c, true);
                 }
-                const int next = wide_next<true>(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
+                next = wide_next<true>(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
                 N = wload(W, next >= 0 ? next : 0);  // unconditional (closest_wide)
-                bool occ = false;
-                while (th) {
+            }
+            bool occ = false, seq = true;
+            if constexpr (TQ) {
+                const unsigned nt = (unsigned)__builtin_popcount(th);
+                if (uni64(__ballot(nt >= 3u)) != 0ull) {
+                    unsigned* cnt = reinterpret_cast<unsigned*>(tq + TQ_CNT);
+                    unsigned pos = 0u;
+                    if (nt) pos = atomicAdd(cnt, nt);
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    const unsigned T = (unsigned)uni((int)atomicAdd(cnt, 0u));
+                    if (T <= (unsigned)TQ_CAP) {
+                        seq = false;
+                        for (unsigned m = th; m; m &= m - 1u) tq[pos++] = (int)((lane << 26) | (unsigned)(tb + __builtin_ctz(m)));
+                        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                        for (unsigned base = 0u; base < T; base += 64u) {
+                            const unsigned j = base + lane;
+                            const unsigned job = j < T ? (unsigned)tq[j] : lane << 26;
+                            const int ow = (int)(job >> 26);
+                            const v3 oo = mk(__shfl(o.x, ow, 64), __shfl(o.y, ow, 64), __shfl(o.z, ow, 64));
+                            const v3 dd = mk(__shfl(d.x, ow, 64), __shfl(d.y, ow, 64), __shfl(d.z, ow, 64));
+                            const float l2 = __shfl(ld2, ow, 64);
+                            if (j < T) {
+                                PRT_TRI_ITER(c, q2);
+                                int k;
+                                const float tt = hit_triangle(oo, dd, W.tris + 3 * (int)(job & 0x3FFFFFFu), k);
+                                if (COUNT) c.sht++;
+                                if (tt < FMAX) {
+                                    const v3 q = add(oo, mul(dd, tt));
+                                    const v3 oi = sub(oo, q);
+                                    if (l2 > dot(oi, oi)) tq[TQ_OCC + ow] = 1;
+                                    atomicMin(reinterpret_cast<unsigned*>(tq + TQ_T + ow), __float_as_uint(tt));
+                                }
+                            }
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                        if (nt) {
+                            occ = tq[TQ_OCC + lane] != 0;
+                            best = fminf(best, __uint_as_float((unsigned)tq[TQ_T + lane]));
+                            tq[TQ_OCC + lane] = 0;
+                            tq[TQ_T + lane] = (int)__float_as_uint(FMAX);
+                        }
+                    }
+                    if (lane == 0u) *cnt = 0u;
+                }
+            }
+            if (busy) {
+                while (seq && th) {
+                    PRT_TRI_ITER(c, q2);
                     const int i = tb + __builtin_ctz(th);
                     th &= th - 1u;
                     int k;
@@ -413,7 +477,8 @@ __device__ __forceinline__ v3 trace_path_dfr(const KArgs& A, bool alive, v3 o, v
     if (nhits) {  // every level's shadow rays as one pool
         u.skip += nhits * (unsigned)s.n_lights;
         const unsigned sh0 = u.shad;
-        shadow_pool<COUNT, MAXB>(s, okm, pbw, stk, sstk, wcap, A.regroup, c, u);
+        int* tq = (int*)(pb0 + (size_t)BLOCK * MAXB) + BLOCK * MAXB + (threadIdx.x >> 6) * TQ_WORDS;
+        shadow_pool<COUNT, MAXB, true>(s, okm, pbw, stk, sstk, wcap, A.regroup, c, u, tq);
         u.skip -= u.shad - sh0;
     }
     v3 dl = d0;  // level i's direction: the primary one, then each level's reflection
