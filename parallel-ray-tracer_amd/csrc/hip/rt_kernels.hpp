@@ -455,11 +455,85 @@ __device__ __forceinline__ int wide_next(unsigned nh, int cb, unsigned imask, un
     return cb + __popc(imask & ((1u << slot) - 1u));
 }
 
+// A wave's LDS queue of packed triangle tests (TQ; rt_shpool.hpp uses it for the shadow pool): TQ_CAP jobs
+// (owner lane << 26 | triangle), then 128 words of per-owner results, then the queue's counter.
+constexpr int TQ_CAP = 128;
+constexpr int TQ_OCC = TQ_CAP, TQ_T = TQ_CAP + 64, TQ_CNT = TQ_CAP + 128, TQ_WORDS = TQ_CAP + 132;
+constexpr unsigned long long TQ_EMPTY = ~0ull;
+
+// The closest walk's packed triangle tests (TQ): the lanes active in this step test the step's (owner, triangle)
+// pairs, one each (single round: at most as many pairs as active lanes), with the owner's ray fetched by
+// ds_bpermute. The results go back through the owner's LDS slots: the least (t, triangle) key by a 64-bit LDS
+// atomic min, then the winner's side (nd) and a tie flag (another pair with the same t) in one flag word. The owner
+// then applies the sequential loop's rule to the step's minimum m: m < best takes it (tie iff two pairs hit at m),
+// m == best (a hit) marks a tie -- the state the per-lane loop would leave, which is what the strict re-walk of a
+// tie relies on. Returns false when the step's pairs do not fit one round (the caller runs the loop).
+template <bool COUNT>
+__device__ __forceinline__ bool closest_tris_packed(const DWide& W, v3 o, v3 d, unsigned th, int tb, float& best,
+                                                    int& hp, int& nd, bool& tie, int* tq, Ctr& c) {
+    const unsigned lane = threadIdx.x & 63u;
+    const unsigned long long ex = __builtin_amdgcn_read_exec();
+    const unsigned na = (unsigned)__builtin_popcountll(ex);
+    const unsigned rk = __builtin_amdgcn_mbcnt_hi((unsigned)(ex >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ex, 0u));
+    unsigned* cnt = reinterpret_cast<unsigned*>(tq + TQ_CNT);
+    const unsigned nt = (unsigned)__builtin_popcount(th);
+    unsigned pos = 0u;
+    if (nt) pos = atomicAdd(cnt, nt);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const unsigned T = (unsigned)__builtin_amdgcn_readfirstlane((int)atomicAdd(cnt, 0u));
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (rk == 0u) *cnt = 0u;
+    if (T > na) return false;
+    for (unsigned m = th; m; m &= m - 1u) tq[pos++] = (int)((lane << 26) | (unsigned)(tb + __builtin_ctz(m)));
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const bool has = rk < T;
+    const unsigned job = has ? (unsigned)tq[rk] : lane << 26;
+    const int ow = (int)(job >> 26);
+    const v3 oo = mk(__shfl(o.x, ow, 64), __shfl(o.y, ow, 64), __shfl(o.z, ow, 64));
+    const v3 dd = mk(__shfl(d.x, ow, 64), __shfl(d.y, ow, 64), __shfl(d.z, ow, 64));
+    unsigned long long* key = reinterpret_cast<unsigned long long*>(tq + TQ_OCC);
+    unsigned* flag = reinterpret_cast<unsigned*>(tq + 64);  // (the job words 64..127: free in a single round)
+    const unsigned tri = job & 0x3FFFFFFu;
+    float tt = FMAX;
+    int k = 0;
+    if (has) {
+        PRT_TRI_ITER(c, q1);
+        tt = hit_triangle<true>(oo, dd, W.tris + 3 * (int)tri, k);
+        if (COUNT) c.cht++;
+        if (tt < FMAX) atomicMin(key + ow, ((unsigned long long)__float_as_uint(tt) << 32) | tri);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (has && tt < FMAX) {
+        const unsigned long long kw = key[ow];
+        if ((unsigned)(kw >> 32) == __float_as_uint(tt)) atomicOr(flag + ow, (unsigned)kw == tri ? (unsigned)k : 2u);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (nt) {
+        const unsigned long long kw = key[lane];
+        const unsigned fl = flag[lane];
+        key[lane] = TQ_EMPTY;
+        flag[lane] = 0u;
+        const float mt = __uint_as_float((unsigned)(kw >> 32));
+        if (kw != TQ_EMPTY) {
+            if (mt < best) {
+                best = mt;
+                hp = (int)(unsigned)kw;
+                nd = (int)(fl & 1u);
+                tie = (fl & 2u) != 0u;
+            } else if (mt == best) {
+                tie = true;
+            }
+        }
+    }
+    return true;
+}
+
 // PIPE: software-pipeline the leaf triangles (the next triangle's loads issued before this one's test);
 // pays where registers allow (the split kernels), not in k_persist (spills at its 168-VGPR cap).
-template <bool COUNT, bool PIPE = false, bool PK = false>
+// TQ: a step whose lanes hold 3+ triangles tests them packed (closest_tris_packed; tq: the wave's queue).
+template <bool COUNT, bool PIPE = false, bool PK = false, bool TQ = false>
 __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& best, int& hp, int& nd, bool& tie,
-                                             int* __restrict__ stk, Ctr& c, int wcap = WSTACK) {
+                                             int* __restrict__ stk, Ctr& c, int wcap = WSTACK, int* tq = nullptr) {
     const RayPre p = ray_pre(o, d);
     const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
     int sp = 0;
@@ -479,6 +553,11 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
         // reloads the root): a load under a branch is copied into the merged register right after it, and that
         // copy waits for the load (dragon 0.712 -> 0.689 ms per frame, sportscar 0.931 -> 0.901, car_boxed 0.870 -> 0.858)
         N = wload(W, next >= 0 ? next : 0);
+        if constexpr (TQ) {
+            if (__builtin_amdgcn_readfirstlane((int)(__ballot(__builtin_popcount(th) >= 3u) != 0ull)) &&
+                closest_tris_packed<COUNT>(W, o, d, th, tb, best, hp, nd, tie, tq, c))
+                th = 0u;
+        }
         if (!PIPE) {
             while (th) {
                 PRT_TRI_ITER(c, q1);
@@ -622,9 +701,10 @@ __device__ __forceinline__ const DWide& wide_for(const DScene& s, bool unit) {
 // Closest hit with the kernel's policy; returns the ORIGINAL triangle index (-1 = miss).
 // sstk (nullable): the binary walks' stack when the wide walk's `stk` holds only wcap entries (DYN kernels)
 // unit: d has unit length (a reflection ray): the unit-direction view serves the fast walk
-template <bool STRICT, bool COUNT, bool REG = true, bool PIPE = false, bool PK = false>
+template <bool STRICT, bool COUNT, bool REG = true, bool PIPE = false, bool PK = false, bool TQ = false>
 __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best, int& nd, int* __restrict__ stk,
-                                       Ctr& c, int* __restrict__ sstk = nullptr, int wcap = WSTACK, bool unit = false) {
+                                       Ctr& c, int* __restrict__ sstk = nullptr, int wcap = WSTACK, bool unit = false,
+                                       int* tq = nullptr) {
     int* __restrict__ bstk = sstk ? sstk : stk;
     int hp = -1;
     bool tie = false;
@@ -633,7 +713,7 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
     if (!STRICT && !degenerate(d)) {
         if (s.wide.nodes) {
             const DWide& W = wide_for(s, unit);
-            closest_wide<COUNT, PIPE, PK>(W, o, d, best, hp, nd, tie, stk, c, wcap);
+            closest_wide<COUNT, PIPE, PK, TQ>(W, o, d, best, hp, nd, tie, stk, c, wcap, tq);
             if (!tie) return hp >= 0 ? W.tri_orig[hp] : -1;
         } else {
             closest_walk<false, COUNT, REG>(s.acc, o, d, best, hp, nd, tie, bstk, c);

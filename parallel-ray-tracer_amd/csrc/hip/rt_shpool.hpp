@@ -74,13 +74,10 @@ __device__ __forceinline__ void flush_u(const UCtr& u, unsigned long long* g) {
 
 // Packed triangle tests (TQ, the all-levels pool): a wave step's hit leaf slots hold few triangles per lane and the
 // per-lane loop over them runs as long as the lane with the most (dragon: 2.7 loop rounds per pool step at 10 % of the
-// lanes, PRT_DIAG_TRI). When some lane holds 3 or more, the step's (owner lane, triangle) pairs are written to a
-// wave-private LDS queue instead and tested 64 at a time, each by the lane that reads it, with the owner's ray
-// fetched by `ds_bpermute`; occlusion (the reference's per-triangle test, bvh.c:283-290) and the nearest hit (for the
-// walk's box pruning) go back to the owner's LDS slots. Per wave: TQ_CAP jobs, 64 occlusion flags, 64 nearest hits,
-// the queue's counter.
-constexpr int TQ_CAP = 128;
-constexpr int TQ_OCC = TQ_CAP, TQ_T = TQ_CAP + 64, TQ_CNT = TQ_CAP + 128, TQ_WORDS = TQ_CAP + 132;
+// lanes, PRT_DIAG_TRI). When some lane holds 3 or more, the step's (owner lane, triangle) pairs are written to the
+// wave's LDS queue (TQ_*, rt_kernels.hpp) instead and tested 64 at a time, each by the lane that reads it, with the
+// owner's ray fetched by `ds_bpermute`; occlusion (the reference's per-triangle test, bvh.c:283-290) and the nearest
+// hit (for the walk's box pruning) go back to the owner's LDS slots.
 
 // The shadow rays of LV bounce levels of the wave's paths, walked as ONE wave-level pool.
 // okm[l]: bit j = this lane's path hit a surface at level l and light j passed the back-face test (dot(L - ip, n)
@@ -406,6 +403,15 @@ __device__ __forceinline__ v3 trace_path_dfr(const KArgs& A, bool alive, v3 o, v
     float4* pb = pb0 + wl;
     float4* pbw = pb - (threadIdx.x & 63);  // the wave's slots of level 0
     int* hid = (int*)(pb0 + (size_t)BLOCK * MAXB) + wl;
+    // the wave's packed-triangle queue (TQ_*): the closest walks' result slots empty, its counter 0
+    int* tq = (int*)(pb0 + (size_t)BLOCK * MAXB) + BLOCK * MAXB + (threadIdx.x >> 6) * TQ_WORDS;
+    {
+        const unsigned lane = threadIdx.x & 63u;
+        reinterpret_cast<unsigned long long*>(tq + TQ_OCC)[lane] = TQ_EMPTY;
+        tq[64 + lane] = 0;
+        if (lane == 0u) tq[TQ_CNT] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
     const DScene& s = A.s;
     const v3 amb = mk(s.amb_x, s.amb_y, s.amb_z);
     const v3 d0 = d;
@@ -425,7 +431,8 @@ __device__ __forceinline__ v3 trace_path_dfr(const KArgs& A, bool alive, v3 o, v
         if (alive) {
             float best;
             int nd;
-            const int orig = closest<false, COUNT, true, false, true>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0);
+            const int orig =
+                closest<false, COUNT, true, false, true, true>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0, tq);
             if (hpix >= 0) {
                 if (it == 0) {
                     if (A.hit) A.hit[hpix] = orig;
@@ -477,7 +484,6 @@ __device__ __forceinline__ v3 trace_path_dfr(const KArgs& A, bool alive, v3 o, v
     if (nhits) {  // every level's shadow rays as one pool
         u.skip += nhits * (unsigned)s.n_lights;
         const unsigned sh0 = u.shad;
-        int* tq = (int*)(pb0 + (size_t)BLOCK * MAXB) + BLOCK * MAXB + (threadIdx.x >> 6) * TQ_WORDS;
         shadow_pool<COUNT, MAXB, true>(s, okm, pbw, stk, sstk, wcap, A.regroup, c, u, tq);
         u.skip -= u.shad - sh0;
     }
