@@ -939,7 +939,8 @@ KFn persist4(bool pbl, bool spp1, bool count) {
 template <int MAXB>
 size_t pbl_bytes(const rtd::KArgs& A, int shp = 0) {
     return sizeof(int) * (size_t)rtd::wstack_words(A.wcap, shp > 0) * rtd::BLOCK + sizeof(float4) * rtd::BLOCK * MAXB +
-           (shp == 2 ? sizeof(int) * (rtd::BLOCK * MAXB + rtd::BLOCK / 64 * rtd::TQ_WORDS) : 0);
+           (shp == 2 ? sizeof(int) * (rtd::BLOCK * MAXB + rtd::BLOCK / 64 * rtd::TQ_WORDS) : 0) +
+           (shp == 3 ? sizeof(int) * (rtd::BLOCK / 64 * rtd::TQ_WORDS) : 0);
 }
 // Does that layout fit 4 workgroups per CU for this scene? (the LDS path buffer measured 1.2 % faster than the global
 // slab on dragon, 2.3 % on car_boxed; the shadow pool needs it)
@@ -974,6 +975,14 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
             dyn = pbl_bytes<MAXB>(A, shp);
             return shp == 2 ? persist4<MAXB, 2>(true, A.spp <= 1, count) : persist4<MAXB, 1>(true, A.spp <= 1, count);
         }
+    }
+    // PERSIST4 with packed stack entries and packed triangle tests (SHP = 3) where its LDS fits: sportscar 20-frame
+    // batches 0.922 -> 0.895 ms per frame, car_boxed 0.860 -> 0.841 (same box). spp = 1 builds only (the spp > 1
+    // build spills 144 B at the 128-VGPR cap)
+    if ((variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) &&
+        A.spp <= 1 && pbl_fits<MAXB>(A, device, 3)) {
+        dyn = pbl_bytes<MAXB>(A, 3);
+        return persist4<MAXB, 3>(true, A.spp <= 1, count);
     }
     if (variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) {
         const bool pbl = pbl_fits<MAXB>(A, device);
@@ -1321,7 +1330,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     const bool shp_ok = wide_ok && ctx->n_lights >= 1 && ctx->n_lights <= 32 &&
                         std::max(ctx->wide_n, std::max(ctx->unit_n, ctx->prim_n)) <= rtd::WIDE_MAX_NODES &&  // (packed stack)
                         (f->bounces <= 4 ? pbl_fits<4>(A, ctx->device, 1) : pbl_fits<8>(A, ctx->device, 1));
-    const bool shd_ok = shp_ok && (f->bounces <= 4 ? pbl_fits<4>(A, ctx->device, 2) : pbl_fits<8>(A, ctx->device, 2));
+    const bool shd_ok = shp_ok && ctx->n_lights <= 8 && (f->bounces <= 4 ? pbl_fits<4>(A, ctx->device, 2) : pbl_fits<8>(A, ctx->device, 2));
     auto usable = [&](int v) {
         if (A.tile_trace) return v == RT_VARIANT_PERSIST;  // (diagnostics: the 3-wave kernel's tile trace)
         if (v == RT_VARIANT_FAN) return fan_ok;

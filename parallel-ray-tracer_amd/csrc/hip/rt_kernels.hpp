@@ -455,16 +455,31 @@ __device__ __forceinline__ int wide_next(unsigned nh, int cb, unsigned imask, un
     return cb + __popc(imask & ((1u << slot) - 1u));
 }
 
-// A wave's LDS queue of packed triangle tests (TQ; rt_shpool.hpp uses it for the shadow pool): TQ_CAP jobs
-// (owner lane << 26 | triangle), then 128 words of per-owner results, then the queue's counter.
+// A wave's LDS queue of packed triangle tests (TQ): TQ_CAP jobs (owner lane << 26 | triangle), then 128 words of
+// per-owner results, then the queue's counter. Between packed steps the result words, the job words 64..127 (the
+// closest walk's flags) and the counter are 0 (tq_clear): minima are kept complemented, by atomic max.
 constexpr int TQ_CAP = 128;
 constexpr int TQ_OCC = TQ_CAP, TQ_T = TQ_CAP + 64, TQ_CNT = TQ_CAP + 128, TQ_WORDS = TQ_CAP + 132;
-constexpr unsigned long long TQ_EMPTY = ~0ull;
+__device__ __forceinline__ void tq_clear(int* tq) {
+    const unsigned lane = threadIdx.x & 63u;
+    tq[64 + lane] = 0;
+    tq[TQ_OCC + lane] = 0;
+    tq[TQ_T + lane] = 0;
+    if (lane == 0u) tq[TQ_CNT] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+// a step packs its triangle tests when some lane holds at least TQ_MIN of them (the per-lane loop would run that many
+// rounds; a packed round costs about 1.5 of them). Same box, dragon 20-frame batches: TQ_MIN 2 / 3 / 4 = 0.573 /
+// 0.575 / 0.579 ms per frame.
+#ifndef PRT_TQ_MIN
+#define PRT_TQ_MIN 2
+#endif
+constexpr unsigned TQ_MIN = PRT_TQ_MIN;
 
 // The closest walk's packed triangle tests (TQ): the lanes active in this step test the step's (owner, triangle)
 // pairs, one each (single round: at most as many pairs as active lanes), with the owner's ray fetched by
 // ds_bpermute. The results go back through the owner's LDS slots: the least (t, triangle) key by a 64-bit LDS
-// atomic min, then the winner's side (nd) and a tie flag (another pair with the same t) in one flag word. The owner
+// atomic max of its complement, then the winner's side (nd) and a tie flag (another pair with the same t) in one flag word. The owner
 // then applies the sequential loop's rule to the step's minimum m: m < best takes it (tie iff two pairs hit at m),
 // m == best (a hit) marks a tie -- the state the per-lane loop would leave, which is what the strict re-walk of a
 // tie relies on. Returns false when the step's pairs do not fit one round (the caller runs the loop).
@@ -491,7 +506,7 @@ __device__ __forceinline__ bool closest_tris_packed(const DWide& W, v3 o, v3 d, 
     const int ow = (int)(job >> 26);
     const v3 oo = mk(__shfl(o.x, ow, 64), __shfl(o.y, ow, 64), __shfl(o.z, ow, 64));
     const v3 dd = mk(__shfl(d.x, ow, 64), __shfl(d.y, ow, 64), __shfl(d.z, ow, 64));
-    unsigned long long* key = reinterpret_cast<unsigned long long*>(tq + TQ_OCC);
+    unsigned long long* key = reinterpret_cast<unsigned long long*>(tq + TQ_OCC);  // complemented keys, 0 = none
     unsigned* flag = reinterpret_cast<unsigned*>(tq + 64);  // (the job words 64..127: free in a single round)
     const unsigned tri = job & 0x3FFFFFFu;
     float tt = FMAX;
@@ -500,21 +515,22 @@ __device__ __forceinline__ bool closest_tris_packed(const DWide& W, v3 o, v3 d, 
         PRT_TRI_ITER(c, q1);
         tt = hit_triangle<true>(oo, dd, W.tris + 3 * (int)tri, k);
         if (COUNT) c.cht++;
-        if (tt < FMAX) atomicMin(key + ow, ((unsigned long long)__float_as_uint(tt) << 32) | tri);
+        if (tt < FMAX) atomicMax(key + ow, ~(((unsigned long long)__float_as_uint(tt) << 32) | tri));
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (has && tt < FMAX) {
-        const unsigned long long kw = key[ow];
+        const unsigned long long kw = ~key[ow];
         if ((unsigned)(kw >> 32) == __float_as_uint(tt)) atomicOr(flag + ow, (unsigned)kw == tri ? (unsigned)k : 2u);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (nt) {
-        const unsigned long long kw = key[lane];
+        const unsigned long long kc = key[lane];
         const unsigned fl = flag[lane];
-        key[lane] = TQ_EMPTY;
+        key[lane] = 0ull;
         flag[lane] = 0u;
+        const unsigned long long kw = ~kc;
         const float mt = __uint_as_float((unsigned)(kw >> 32));
-        if (kw != TQ_EMPTY) {
+        if (kc != 0ull) {
             if (mt < best) {
                 best = mt;
                 hp = (int)(unsigned)kw;
@@ -524,6 +540,56 @@ __device__ __forceinline__ bool closest_tris_packed(const DWide& W, v3 o, v3 d, 
                 tie = true;
             }
         }
+    }
+    return true;
+}
+
+// The shadow walks' packed triangle tests (TQ), as closest_tris_packed: a pair occludes the owner's ray when its
+// triangle is hit nearer than the light (the reference's per-triangle test, bvh.c:283-290); the nearest hit (for the
+// walk's box pruning) goes back complemented by atomic max.
+template <bool COUNT>
+__device__ __forceinline__ bool shadow_tris_packed(const DWide& W, v3 o, v3 d, float ld2, unsigned th, int tb,
+                                                   float& best, bool& occ, int* tq, Ctr& c) {
+    const unsigned lane = threadIdx.x & 63u;
+    const unsigned long long ex = __builtin_amdgcn_read_exec();
+    const unsigned na = (unsigned)__builtin_popcountll(ex);
+    const unsigned rk = __builtin_amdgcn_mbcnt_hi((unsigned)(ex >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ex, 0u));
+    unsigned* cnt = reinterpret_cast<unsigned*>(tq + TQ_CNT);
+    const unsigned nt = (unsigned)__builtin_popcount(th);
+    unsigned pos = 0u;
+    if (nt) pos = atomicAdd(cnt, nt);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const unsigned T = (unsigned)__builtin_amdgcn_readfirstlane((int)atomicAdd(cnt, 0u));
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (rk == 0u) *cnt = 0u;
+    if (T > na) return false;
+    for (unsigned m = th; m; m &= m - 1u) tq[pos++] = (int)((lane << 26) | (unsigned)(tb + __builtin_ctz(m)));
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const bool has = rk < T;
+    const unsigned job = has ? (unsigned)tq[rk] : lane << 26;
+    const int ow = (int)(job >> 26);
+    const v3 oo = mk(__shfl(o.x, ow, 64), __shfl(o.y, ow, 64), __shfl(o.z, ow, 64));
+    const v3 dd = mk(__shfl(d.x, ow, 64), __shfl(d.y, ow, 64), __shfl(d.z, ow, 64));
+    const float l2 = __shfl(ld2, ow, 64);
+    if (has) {
+        PRT_TRI_ITER(c, q2);
+        int k;
+        const float tt = hit_triangle(oo, dd, W.tris + 3 * (int)(job & 0x3FFFFFFu), k);
+        if (COUNT) c.sht++;
+        if (tt < FMAX) {
+            const v3 q = add(oo, mul(dd, tt));
+            const v3 oi = sub(oo, q);
+            if (l2 > dot(oi, oi)) tq[TQ_OCC + ow] = 1;
+            atomicMax(reinterpret_cast<unsigned*>(tq + TQ_T + ow), ~__float_as_uint(tt));
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (nt) {
+        occ = tq[TQ_OCC + lane] != 0;
+        const unsigned tc = (unsigned)tq[TQ_T + lane];
+        if (tc) best = fminf(best, __uint_as_float(~tc));
+        tq[TQ_OCC + lane] = 0;
+        tq[TQ_T + lane] = 0;
     }
     return true;
 }
@@ -554,7 +620,7 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
         // copy waits for the load (dragon 0.712 -> 0.689 ms per frame, sportscar 0.931 -> 0.901, car_boxed 0.870 -> 0.858)
         N = wload(W, next >= 0 ? next : 0);
         if constexpr (TQ) {
-            if (__builtin_amdgcn_readfirstlane((int)(__ballot(__builtin_popcount(th) >= 3u) != 0ull)) &&
+            if (__builtin_amdgcn_readfirstlane((int)(__ballot(__builtin_popcount(th) >= TQ_MIN) != 0ull)) &&
                 closest_tris_packed<COUNT>(W, o, d, th, tb, best, hp, nd, tie, tq, c))
                 th = 0u;
         }
@@ -616,9 +682,9 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
     }
 }
 
-template <bool COUNT, bool PIPE = false, bool PK = false>
+template <bool COUNT, bool PIPE = false, bool PK = false, bool TQ = false>
 __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c,
-                                             int wcap = WSTACK) {
+                                             int wcap = WSTACK, int* tq = nullptr) {
     const RayPre p = ray_pre(o, d);
     const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
     float best = FMAX;
@@ -637,9 +703,17 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
         }
         const int next = wide_next<PK>(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
         N = wload(W, next >= 0 ? next : 0);  // unconditional (closest_wide)
+        if constexpr (TQ) {
+            bool occ = false;
+            if (__builtin_amdgcn_readfirstlane((int)(__ballot(__builtin_popcount(th) >= TQ_MIN) != 0ull)) &&
+                shadow_tris_packed<COUNT>(W, o, d, ld2, th, tb, best, occ, tq, c)) {
+                if (occ) return false;
+                th = 0u;
+            }
+        }
         if (!PIPE) {
             while (th) {
-            PRT_TRI_ITER(c, q2);
+                PRT_TRI_ITER(c, q2);
                 const int i = tb + __builtin_ctz(th);
                 th &= th - 1u;
                 int k;
@@ -730,12 +804,13 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
     return hp >= 0 ? s.ref.tri_orig[hp] : -1;
 }
 
-template <bool STRICT, bool COUNT, bool REG = true, bool PIPE = false>
+template <bool STRICT, bool COUNT, bool REG = true, bool PIPE = false, bool PK = false, bool TQ = false>
 __device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c,
-                                        int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
+                                        int* __restrict__ sstk = nullptr, int wcap = WSTACK, int* tq = nullptr) {
     int* __restrict__ bstk = sstk ? sstk : stk;
     if (!STRICT && !degenerate(d)) {
-        if (s.wide.nodes) return visible_wide<COUNT, PIPE>(wide_for(s, true), o, d, ld2, stk, c, wcap);  // |d| = 1
+        if (s.wide.nodes)  // |d| = 1
+            return visible_wide<COUNT, PIPE, PK, TQ>(wide_for(s, true), o, d, ld2, stk, c, wcap, tq);
         return visible_walk<false, COUNT, REG>(s.acc, o, d, ld2, bstk, c);
     }
     if (!STRICT) c.fb++;
@@ -786,12 +861,13 @@ __device__ __forceinline__ void seti(int (&a)[MAXB], int i, int v) {
 // PB: the level's colour and material go to this lane's path buffer slot pb[it * 64] instead of the
 // register arrays (cold values: written once per level, read once by the fold), which frees 4 * MAXB
 // registers across the walks for the kernels with the tightest register budget.
-template <int MAXB, bool STRICT, bool COUNT, bool REG, int G = 1, bool PB = false>
+// PK / TQ: packed stack entries and packed triangle tests (the SHP = 3 build of PERSIST4; tq: the wave's queue)
+template <int MAXB, bool STRICT, bool COUNT, bool REG, int G = 1, bool PB = false, bool PK = false, bool TQ = false>
 __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, v3& o, v3& d, v3 (&cols)[MAXB],
                                           int (&mats)[MAXB], int& L, bool& tail, int& hit0, float& t0,
                                           int* __restrict__ bh, int bh_pix, int* __restrict__ stk, Ctr& c,
                                           unsigned q = 0, float4* __restrict__ pb = nullptr,
-                                          int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
+                                          int* __restrict__ sstk = nullptr, int wcap = WSTACK, int* tq = nullptr) {
     const v3 amb = mk(s.amb_x, s.amb_y, s.amb_z);
     float best;
     int nd;
@@ -800,7 +876,7 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
     else c.refl++;
     int orig;
     if constexpr (G > 1) orig = closest_g<G, COUNT>(s, o, d, best, nd, stk, c, q, it > 0);
-    else orig = closest<STRICT, COUNT, REG>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0);  // it > 0: |d| = 1
+    else orig = closest<STRICT, COUNT, REG, false, PK, TQ>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0, tq);  // it > 0: |d| = 1
     if (it == 0) {
         hit0 = orig;
         t0 = best;
@@ -838,7 +914,7 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
         } else {
             c.shad++;
             if constexpr (G > 1) V = visible_g<G, COUNT>(s, ip, l, ld2, stk, c, q) ? 1 : 0;
-            else V = visible<STRICT, COUNT, REG>(s, ip, l, ld2, stk, c, sstk, wcap) ? 1 : 0;
+            else V = visible<STRICT, COUNT, REG, false, PK, TQ>(s, ip, l, ld2, stk, c, sstk, wcap, tq) ? 1 : 0;
         }
         const v3 kl = xyz(s.lights[2 * j + 1]);
         const v3 ks = xyz(s.mats[3 * m]), kd = xyz(s.mats[3 * m + 1]);
@@ -927,15 +1003,19 @@ __device__ __forceinline__ v3 fold_pb(const DScene& s, const float4* __restrict_
 
 // PB: 0 = levels in registers, 1 = path buffer in global memory (A.pathbuf), 2 = path buffer in dynamic LDS
 // after the DYN wide stack (2 * wcap ints per lane): [wave][level][lane] float4, the L2 left to the scene
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0>
+// (PK / TQ: after the path buffer, the waves' packed-triangle queues)
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0, bool PK = false, bool TQ = false>
 __device__ v3 trace_path(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, Ctr& c, int& hit0, float& t0, int bh_pix,
                          unsigned q = 0, int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
     v3 cols[MAXB];
     int mats[MAXB];
     float4* pb = nullptr;
+    int* tq = nullptr;
     if constexpr (PB == 2) {
         extern __shared__ int lds_dyn[];
-        pb = (float4*)(lds_dyn + wstack_words(wcap, false) * BLOCK) + (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
+        float4* pb0 = (float4*)(lds_dyn + wstack_words(wcap, PK) * BLOCK);
+        pb = pb0 + (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
+        if constexpr (TQ) tq = (int*)(pb0 + (size_t)BLOCK * MAXB) + (threadIdx.x >> 6) * TQ_WORDS;
     } else if constexpr (PB) {  // [wave][level][lane] (persistent grids: a wave's slot is its own for the launch)
         pb = A.pathbuf + ((size_t)(blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6)) * MAXB) * 64 + (threadIdx.x & 63);
     } else {
@@ -948,8 +1028,8 @@ __device__ v3 trace_path(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, Ctr&
     int L = 0;
     bool tail = false;
     for (int it = 0; it < A.bounces; ++it) {
-        if (path_step<MAXB, STRICT, COUNT, REG, G, PB != 0>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0, t0,
-                                                       A.bounce_hit, bh_pix, stk, c, q, pb, sstk, wcap))
+        if (path_step<MAXB, STRICT, COUNT, REG, G, PB != 0, PK, TQ>(A.s, A.bounces, it, o, d, cols, mats, L, tail, hit0,
+                                                                t0, A.bounce_hit, bh_pix, stk, c, q, pb, sstk, wcap, tq))
             break;
     }
     if constexpr (PB != 0) return fold_pb<MAXB>(A.s, pb, L, tail);
@@ -1008,7 +1088,8 @@ __device__ __forceinline__ void flush_u(const UCtr& u, unsigned long long* g);
 
 // Pixel (x, compact row k) of frame `frame` of the launch (outputs at frame * frame_px).
 // SPP1: a build for spp = 1 only (the stratified-sample loop compiled out, fewer live values around the path)
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0, bool SPP1 = false>
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0, bool SPP1 = false,
+          bool TQ = false>
 __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int frame, int x, int k,
                                              int* __restrict__ stk, Ctr& c, unsigned q = 0,
                                              int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
@@ -1021,8 +1102,8 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
     if (A.bounce_hit)
         for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
     if (SPP1 || A.spp <= 1) {
-        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB>(A, C.pos, primary_dir(C, (float)x, (float)y),
-                                                                      stk, c, hit0, t0, (int)o, q, sstk, wcap));
+        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB, TQ, TQ>(A, C.pos, primary_dir(C, (float)x, (float)y),
+                                                                          stk, c, hit0, t0, (int)o, q, sstk, wcap));
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples
         const int g = A.spp_grid;
         v3 acc = mk(0.0f, 0.0f, 0.0f);
@@ -1033,7 +1114,7 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
                 int h;
                 float tt;
                 v3 cs;
-                cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB>(
+                cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB, TQ, TQ>(
                         A, C.pos, primary_dir(C, fx, fy), stk, c, h, tt, si == 0 && sj == 0 ? (int)o : -1, q, sstk, wcap));
                 acc = add(acc, cs);
                 if (si == 0 && sj == 0) {
@@ -1109,6 +1190,7 @@ __device__ __forceinline__ bool next_item(const KArgs& A, int lane, int& reg, in
 // fit a CU's LDS: the kernels with OCC > 4 waves per SIMD.
 template <int SHP> struct UCtrSel { using type = UCtr; };
 template <> struct UCtrSel<0> { struct type {}; };
+template <> struct UCtrSel<3> { struct type {}; };
 template <int SHP> using UCtrOf = typename UCtrSel<SHP>::type;
 
 template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int OCC = 3, bool TRACE = false, bool BATCH = false,
@@ -1117,6 +1199,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
 void k_persist(KArgs A) {
     static_assert(PB != 2 || DYN, "an LDS path buffer lives in the DYN kernels' dynamic LDS");
     static_assert(!SHP || PB == 2, "the shadow pool hands its rays over through the LDS path buffer");
+    // SHP = 3: no pool; PERSIST4 with packed stack entries and packed triangle tests (queues after the path buffer)
     int* stk;
     int* sstk = nullptr;
     int wcap = WSTACK;
@@ -1137,6 +1220,11 @@ void k_persist(KArgs A) {
         __syncthreads();
     }
     UCtrOf<SHP> u = {};  // SHP: the wave-uniform ray counts (rt_shpool.hpp)
+    if constexpr (SHP == 3) {  // the wave's packed-triangle queue starts clear
+        extern __shared__ int lds_dyn[];
+        tq_clear((int*)((float4*)(lds_dyn + wstack_words(wcap, true) * BLOCK) + (size_t)BLOCK * MAXB) +
+                 (threadIdx.x >> 6) * TQ_WORDS);
+    }
     // frame batches: dealt item t = (tile t / n_frames of the dealing order, frame t % n_frames), so the
     // expensive (central) tiles of every frame of the batch start first
     int reg = 0;
@@ -1149,12 +1237,12 @@ void k_persist(KArgs A) {
         unsigned long long t0 = 0;
         const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
         if (TRACE) t0 = __builtin_amdgcn_s_memrealtime();
-        if constexpr (SHP)
+        if constexpr (SHP == 1 || SHP == 2)
             render_pixel_shp<MAXB, COUNT, SPP1, SHP>(A, cam_of<BATCH>(A, frame), frame, x, k, x < A.W && k < A.n_rows,
                                                      stk, c, u, sstk, wcap);
         else if (x < A.W && k < A.n_rows)
-            render_pixel<MAXB, STRICT, COUNT, REG, 1, PB, SPP1>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, 0u, sstk,
-                                                                wcap);
+            render_pixel<MAXB, STRICT, COUNT, REG, 1, PB, SPP1, SHP == 3>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c,
+                                                                          0u, sstk, wcap);
         if (TRACE) {  // {begin, end, wave | fallbacks << 32, wave steps | lane node visits << 32} (COUNT)
             const unsigned fb = wave_sum(c.fb - fb0), ws = wave_sum(c.ws - ws0), nv = wave_sum(c.chi + c.shi - nd0);
             if (lane == 0) {
@@ -1166,7 +1254,7 @@ void k_persist(KArgs A) {
         }
     }
     flush<COUNT>(c, A.counters);
-    if constexpr (SHP) flush_u(u, A.counters);
+    if constexpr (SHP == 1 || SHP == 2) flush_u(u, A.counters);
     if constexpr (COUNT) {  // every wave of the workgroup leaves the tile loop and reaches this point
         __syncthreads();
         if (threadIdx.x < 32 && c.hist[threadIdx.x]) atomicAdd(A.counters + C_HIST + threadIdx.x, (unsigned long long)c.hist[threadIdx.x]);

@@ -13,6 +13,8 @@
 // depend on which lane walks it or when, and the owner folds the lights' Lambert/Blinn terms in the reference's
 // order once all of its level's rays have returned (trace_path_shp).
 #pragma once
+#include <type_traits>
+
 #include "rt_kernels.hpp"
 
 namespace rtd {
@@ -80,22 +82,18 @@ __device__ __forceinline__ void flush_u(const UCtr& u, unsigned long long* g) {
 // hit (for the walk's box pruning) go back to the owner's LDS slots.
 
 // The shadow rays of LV bounce levels of the wave's paths, walked as ONE wave-level pool.
-// okm[l]: bit j = this lane's path hit a surface at level l and light j passed the back-face test (dot(L - ip, n)
+// okm(l): bit j = this lane's path hit a surface at level l and light j passed the back-face test (dot(L - ip, n)
 // >= 0, the reference's early-out, raytracer.c:66-67; failing lights are not walked). lvl: the wave's path-buffer
 // slots of those levels (LDS, [level][lane]); the owner lane p has stored its level-l hit point in lvl[64 l + p].xyz
 // and 0 in its .w, and the walkers set bit j of that .w (as an unsigned) when light j is visible from it along the
 // reference's shadow ray. regroup: idle lanes that trigger a refill (all lanes idle always do). Called by every lane
 // of the wave.
-template <bool COUNT, int LV, bool TQ = false>
-__device__ __forceinline__ void shadow_pool(const DScene& s, const unsigned (&okm)[LV], float4* lvl, int* __restrict__ stk,
+template <bool COUNT, int LV, bool TQ = false, class OKM>
+__device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lvl, int* __restrict__ stk,
                                             int* __restrict__ sstk, int wcap, int regroup, Ctr& c, UCtr& u,
                                             int* tq = nullptr) {
     const unsigned lane = threadIdx.x & 63u;
-    if constexpr (TQ) {  // this lane's result slots, the queue's counter
-        tq[TQ_OCC + lane] = 0;
-        tq[TQ_T + lane] = (int)__float_as_uint(FMAX);
-        if (lane == 0u) tq[TQ_CNT] = 0;
-    }
+    // (TQ: the queue's result slots are clear, tq_clear)
     const unsigned long long all = uni64(__ballot(1));
     const int nl = s.n_lights;
     const DWide& W = wide_for(s, true);  // |d| = 1: the unit-direction view
@@ -110,7 +108,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, const unsigned (&ok
                 cj = 0;
                 cl = uni(cl + 1);
             }
-            cm = uni64(__ballot((get_u<LV>(okm, cl) >> cj) & 1u));
+            cm = uni64(__ballot((okm(cl) >> cj) & 1u));
             u.shad += (unsigned)__builtin_popcountll(cm);
         }
     };
@@ -198,7 +196,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, const unsigned (&ok
             bool occ = false, seq = true;
             if constexpr (TQ) {
                 const unsigned nt = (unsigned)__builtin_popcount(th);
-                if (uni64(__ballot(nt >= 3u)) != 0ull) {
+                if (uni64(__ballot(nt >= TQ_MIN)) != 0ull) {
                     unsigned* cnt = reinterpret_cast<unsigned*>(tq + TQ_CNT);
                     unsigned pos = 0u;
                     if (nt) pos = atomicAdd(cnt, nt);
@@ -224,16 +222,17 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, const unsigned (&ok
                                     const v3 q = add(oo, mul(dd, tt));
                                     const v3 oi = sub(oo, q);
                                     if (l2 > dot(oi, oi)) tq[TQ_OCC + ow] = 1;
-                                    atomicMin(reinterpret_cast<unsigned*>(tq + TQ_T + ow), __float_as_uint(tt));
+                                    atomicMax(reinterpret_cast<unsigned*>(tq + TQ_T + ow), ~__float_as_uint(tt));
                                 }
                             }
                         }
                         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                         if (nt) {
                             occ = tq[TQ_OCC + lane] != 0;
-                            best = fminf(best, __uint_as_float((unsigned)tq[TQ_T + lane]));
+                            const unsigned tc = (unsigned)tq[TQ_T + lane];
+                            if (tc) best = fminf(best, __uint_as_float(~tc));
                             tq[TQ_OCC + lane] = 0;
-                            tq[TQ_T + lane] = (int)__float_as_uint(FMAX);
+                            tq[TQ_T + lane] = 0;
                         }
                     }
                     if (lane == 0u) *cnt = 0u;
@@ -268,6 +267,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, const unsigned (&ok
             if (id2 == all || (more && __builtin_popcountll(id2) >= regroup)) break;
         }
     }
+    if constexpr (TQ) tq_clear(tq);  // (the pool's jobs 64..127 overwrote the closest walk's flag words)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
@@ -331,8 +331,7 @@ __device__ __forceinline__ v3 trace_path_shp(const KArgs& A, bool alive, v3 o, v
         if (nh) {
             u.skip += nh * (unsigned)s.n_lights;  // less the rays walked (shadow_pool counts those in u.shad)
             const unsigned sh0 = u.shad;
-            const unsigned okl[1] = {okm};
-            shadow_pool<COUNT, 1>(s, okl, pbw + it * 64, stk, sstk, wcap, A.regroup, c, u);
+            shadow_pool<COUNT, 1>(s, [&](int) { return okm; }, pbw + it * 64, stk, sstk, wcap, A.regroup, c, u);
             u.skip -= u.shad - sh0;
         }
         if (hit >= 0) {  // raytracer.c:144-172 as path_step, the lights' visibility from the pool
@@ -405,19 +404,13 @@ __device__ __forceinline__ v3 trace_path_dfr(const KArgs& A, bool alive, v3 o, v
     int* hid = (int*)(pb0 + (size_t)BLOCK * MAXB) + wl;
     // the wave's packed-triangle queue (TQ_*): the closest walks' result slots empty, its counter 0
     int* tq = (int*)(pb0 + (size_t)BLOCK * MAXB) + BLOCK * MAXB + (threadIdx.x >> 6) * TQ_WORDS;
-    {
-        const unsigned lane = threadIdx.x & 63u;
-        reinterpret_cast<unsigned long long*>(tq + TQ_OCC)[lane] = TQ_EMPTY;
-        tq[64 + lane] = 0;
-        if (lane == 0u) tq[TQ_CNT] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    }
+    tq_clear(tq);
     const DScene& s = A.s;
     const v3 amb = mk(s.amb_x, s.amb_y, s.amb_z);
     const v3 d0 = d;
-    unsigned okm[MAXB];
-#pragma unroll
-    for (int k = 0; k < MAXB; k++) okm[k] = 0u;
+    // the levels' back-face masks, 8 bits per level (1..8 lights: the rule's shd_ok) in one or two registers
+    using OkT = typename std::conditional<MAXB <= 4, unsigned, unsigned long long>::type;
+    OkT okm = 0;
     int L = 0;
     bool tail = false;
     unsigned nhits = 0;
@@ -440,8 +433,7 @@ __device__ __forceinline__ v3 trace_path_dfr(const KArgs& A, bool alive, v3 o, v
                 }
                 if (A.bounce_hit) A.bounce_hit[(size_t)hpix * A.bounces + it] = orig;
             }
-            if (orig < 0) {  // raytracer.c:132-135
-                pb[it * 64] = make_float4(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z, __int_as_float(0));
+            if (orig < 0) {  // raytracer.c:132-135 (the colour is written by the shading loop below)
                 hid[it * 64] = -1;
                 L = it + 1;
                 tail = false;
@@ -457,7 +449,7 @@ __device__ __forceinline__ v3 trace_path_dfr(const KArgs& A, bool alive, v3 o, v
                     const v3 tmp2 = sub(xyz(s.lights[2 * j]), ip);
                     ok |= dot(tmp2, n) < 0 ? 0u : (1u << j);
                 }
-                set_u<MAXB>(okm, it, ok);
+                okm |= (OkT)ok << (8 * it);
                 pb[it * 64] = make_float4(ip.x, ip.y, ip.z, __uint_as_float(0u));
                 hid[it * 64] = orig | (nd ? (1 << 30) : 0);
                 const v3 ns = mul(n, 2.0f * __builtin_fabsf(dot(d, n)));  // (dd = -(-d) = d exactly)
@@ -484,16 +476,20 @@ __device__ __forceinline__ v3 trace_path_dfr(const KArgs& A, bool alive, v3 o, v
     if (nhits) {  // every level's shadow rays as one pool
         u.skip += nhits * (unsigned)s.n_lights;
         const unsigned sh0 = u.shad;
-        shadow_pool<COUNT, MAXB, true>(s, okm, pbw, stk, sstk, wcap, A.regroup, c, u, tq);
+        shadow_pool<COUNT, MAXB, true>(s, [&](int l) { return (unsigned)(okm >> (8 * l)) & 0xFFu; }, pbw, stk, sstk, wcap,
+                                       A.regroup, c, u, tq);
         u.skip -= u.shad - sh0;
     }
     v3 dl = d0;  // level i's direction: the primary one, then each level's reflection
     for (int it = 0; it < L; ++it) {  // the levels' colours (raytracer.c:144-160 as path_step), in order
         const int h = hid[it * 64];
-        if (h < 0) break;  // a miss: its colour is in place (and it was the path's last level)
+        if (h < 0) {  // a miss (the path's last level): the background
+            pb[it * 64] = make_float4(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z, __int_as_float(0));
+            break;
+        }
         const float4 e = pb[it * 64];
         const v3 ip = xyz(e);
-        const unsigned vis = __float_as_uint(e.w) & get_u<MAXB>(okm, it);
+        const unsigned vis = __float_as_uint(e.w) & ((unsigned)(okm >> (8 * it)) & 0xFFu);
         const int orig = h & ((1 << 30) - 1);
         const float4 sh0 = s.shade[2 * orig], sh1 = s.shade[2 * orig + 1];
         const int m = __float_as_int(sh0.w);
