@@ -964,6 +964,9 @@ bool pbl_fits(const rtd::KArgs& A, int device, int shp = 0) {
 //                        (the path buffer plus a hit-triangle array in LDS; else PERSIST4);
 // a tile trace (A.tile_trace: the hybrid launch's measuring frame, PRT_TILE_TRACE) runs the 3-wave build with
 // per-tile timestamps.
+#ifndef PRT_P4TQ_SPP
+#define PRT_P4TQ_SPP 0  // (A/B builds: the packed PERSIST4 build for spp > 1 too)
+#endif
 template <int MAXB>
 KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, size_t& dyn) {
     dyn = 0;
@@ -980,7 +983,7 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
     // batches 0.922 -> 0.895 ms per frame, car_boxed 0.860 -> 0.841 (same box). spp = 1 builds only (the spp > 1
     // build spills 144 B at the 128-VGPR cap)
     if ((variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) &&
-        A.spp <= 1 && pbl_fits<MAXB>(A, device, 3)) {
+        (A.spp <= 1 || PRT_P4TQ_SPP) && pbl_fits<MAXB>(A, device, 3)) {
         dyn = pbl_bytes<MAXB>(A, 3);
         return persist4<MAXB, 3>(true, A.spp <= 1, count);
     }
