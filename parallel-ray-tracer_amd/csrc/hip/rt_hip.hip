@@ -964,6 +964,9 @@ bool pbl_fits(const rtd::KArgs& A, int device, int shp = 0) {
 //                        (the path buffer plus a hit-triangle array in LDS; else PERSIST4);
 // a tile trace (A.tile_trace: the hybrid launch's measuring frame, PRT_TILE_TRACE) runs the 3-wave build with
 // per-tile timestamps.
+#ifndef PRT_P3_TQ
+#define PRT_P3_TQ 0  // (A/B builds: the 3-wave k_persist's spp = 1 build, 1; with packed triangle tests, 2)
+#endif
 #ifndef PRT_P4TQ_SPP
 #define PRT_P4TQ_SPP 0  // (A/B builds: the packed PERSIST4 build for spp > 1 too)
 #endif
@@ -993,6 +996,15 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
         // (the bench's batches: the spp = 1 build)
         return persist4<MAXB, 0>(pbl, A.spp <= 1, count);
     }
+#if PRT_P3_TQ == 2
+    if (A.spp <= 1)
+        return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true, 0, false, true, 3>
+                     : rtd::k_persist<MAXB, false, false, true, 3, false, true, 0, false, true, 3>;
+#elif PRT_P3_TQ == 1
+    if (A.spp <= 1)
+        return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true, 0, false, true>
+                     : rtd::k_persist<MAXB, false, false, true, 3, false, true, 0, false, true>;
+#endif
     return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true> : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
 }
 

@@ -460,6 +460,11 @@ __device__ __forceinline__ int wide_next(unsigned nh, int cb, unsigned imask, un
 // closest walk's flags) and the counter are 0 (tq_clear): minima are kept complemented, by atomic max.
 constexpr int TQ_CAP = 128;
 constexpr int TQ_OCC = TQ_CAP, TQ_T = TQ_CAP + 64, TQ_CNT = TQ_CAP + 128, TQ_WORDS = TQ_CAP + 132;
+// the waves' queues of a kernel without dynamic LDS (the 3-wave k_persist): a static array
+__device__ __forceinline__ int* tq_static() {
+    __shared__ int q[BLOCK / 64 * TQ_WORDS];
+    return q + (threadIdx.x >> 6) * TQ_WORDS;
+}
 __device__ __forceinline__ void tq_clear(int* tq) {
     const unsigned lane = threadIdx.x & 63u;
     tq[64 + lane] = 0;
@@ -1016,6 +1021,8 @@ __device__ v3 trace_path(const KArgs& A, v3 o, v3 d, int* __restrict__ stk, Ctr&
         float4* pb0 = (float4*)(lds_dyn + wstack_words(wcap, PK) * BLOCK);
         pb = pb0 + (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
         if constexpr (TQ) tq = (int*)(pb0 + (size_t)BLOCK * MAXB) + (threadIdx.x >> 6) * TQ_WORDS;
+    } else if constexpr (TQ) {  // (PB 0 / 1: the kernel's static queues)
+        tq = tq_static();
     } else if constexpr (PB) {  // [wave][level][lane] (persistent grids: a wave's slot is its own for the launch)
         pb = A.pathbuf + ((size_t)(blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6)) * MAXB) * 64 + (threadIdx.x & 63);
     } else {
@@ -1089,7 +1096,7 @@ __device__ __forceinline__ void flush_u(const UCtr& u, unsigned long long* g);
 // Pixel (x, compact row k) of frame `frame` of the launch (outputs at frame * frame_px).
 // SPP1: a build for spp = 1 only (the stratified-sample loop compiled out, fewer live values around the path)
 template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0, bool SPP1 = false,
-          bool TQ = false>
+          bool TQ = false, bool PK = TQ>
 __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int frame, int x, int k,
                                              int* __restrict__ stk, Ctr& c, unsigned q = 0,
                                              int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
@@ -1102,7 +1109,7 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
     if (A.bounce_hit)
         for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
     if (SPP1 || A.spp <= 1) {
-        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB, TQ, TQ>(A, C.pos, primary_dir(C, (float)x, (float)y),
+        col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB, PK, TQ>(A, C.pos, primary_dir(C, (float)x, (float)y),
                                                                           stk, c, hit0, t0, (int)o, q, sstk, wcap));
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples
         const int g = A.spp_grid;
@@ -1114,7 +1121,7 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
                 int h;
                 float tt;
                 v3 cs;
-                cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB, TQ, TQ>(
+                cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB, PK, TQ>(
                         A, C.pos, primary_dir(C, fx, fy), stk, c, h, tt, si == 0 && sj == 0 ? (int)o : -1, q, sstk, wcap));
                 acc = add(acc, cs);
                 if (si == 0 && sj == 0) {
@@ -1198,8 +1205,9 @@ template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int OCC = 3, bool 
 __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_per_eu(OCC > 0 ? OCC : 1)))
 void k_persist(KArgs A) {
     static_assert(PB != 2 || DYN, "an LDS path buffer lives in the DYN kernels' dynamic LDS");
-    static_assert(!SHP || PB == 2, "the shadow pool hands its rays over through the LDS path buffer");
-    // SHP = 3: no pool; PERSIST4 with packed stack entries and packed triangle tests (queues after the path buffer)
+    static_assert(SHP == 0 || SHP == 3 || PB == 2, "the shadow pool hands its rays over through the LDS path buffer");
+    // SHP = 3: no pool; packed triangle tests (queues after the LDS path buffer with packed stack entries in the DYN
+    // kernels, a static array in the others)
     int* stk;
     int* sstk = nullptr;
     int wcap = WSTACK;
@@ -1221,9 +1229,13 @@ void k_persist(KArgs A) {
     }
     UCtrOf<SHP> u = {};  // SHP: the wave-uniform ray counts (rt_shpool.hpp)
     if constexpr (SHP == 3) {  // the wave's packed-triangle queue starts clear
-        extern __shared__ int lds_dyn[];
-        tq_clear((int*)((float4*)(lds_dyn + wstack_words(wcap, true) * BLOCK) + (size_t)BLOCK * MAXB) +
-                 (threadIdx.x >> 6) * TQ_WORDS);
+        if constexpr (DYN) {
+            extern __shared__ int lds_dyn[];
+            tq_clear((int*)((float4*)(lds_dyn + wstack_words(wcap, true) * BLOCK) + (size_t)BLOCK * MAXB) +
+                     (threadIdx.x >> 6) * TQ_WORDS);
+        } else {
+            tq_clear(tq_static());
+        }
     }
     // frame batches: dealt item t = (tile t / n_frames of the dealing order, frame t % n_frames), so the
     // expensive (central) tiles of every frame of the batch start first
@@ -1241,8 +1253,8 @@ void k_persist(KArgs A) {
             render_pixel_shp<MAXB, COUNT, SPP1, SHP>(A, cam_of<BATCH>(A, frame), frame, x, k, x < A.W && k < A.n_rows,
                                                      stk, c, u, sstk, wcap);
         else if (x < A.W && k < A.n_rows)
-            render_pixel<MAXB, STRICT, COUNT, REG, 1, PB, SPP1, SHP == 3>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c,
-                                                                          0u, sstk, wcap);
+            render_pixel<MAXB, STRICT, COUNT, REG, 1, PB, SPP1, SHP == 3, SHP == 3 && DYN>(
+                A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, 0u, sstk, wcap);
         if (TRACE) {  // {begin, end, wave | fallbacks << 32, wave steps | lane node visits << 32} (COUNT)
             const unsigned fb = wave_sum(c.fb - fb0), ws = wave_sum(c.ws - ws0), nv = wave_sum(c.chi + c.shi - nd0);
             if (lane == 0) {

@@ -267,6 +267,21 @@ def test_standin_scenes_vs_reference_fixture(dev, name):
         assert md5.hexdigest() == G["standin"][name]["320x180_md5"], k
 
 
+@pytest.mark.parametrize("name", ["car_only", "dragon"])
+def test_exact_ties_everywhere_match_strict(dev, name):
+    """every triangle twice: every closest hit is an exact tie, which the fast walks must detect -- through the
+    packed triangle tests' tie flags too (shdefer, persist4) -- and resolve by the strict re-walk, so the frame equals
+    the strict kernel's (the reference's first-found rule, bvh.c:331) bit for bit; occlusion is unchanged"""
+    base = host.Scene.named(name)
+    s = host.Scene(np.concatenate([base.triangles, base.triangles]), base.lights).build_bvh(3)
+    ref = render(dev, s, 96, 54, "strict")
+    for k in ("fast", "persist4", "shpool", "shdefer", "coop4"):
+        out = render(dev, s, 96, 54, k, counters=True)
+        np.testing.assert_array_equal(out["hit"], ref["hit"], err_msg=k)
+        assert same_bits(out["t"], ref["t"]) and same_bits(out["rgb"], ref["rgb"]), k
+        assert out["stats"]["fallbacks"] > 0, k
+
+
 _ORACLE_FRAMES = {}
 
 
