@@ -955,21 +955,16 @@ bool pbl_fits(const rtd::KArgs& A, int device, int shp = 0) {
 }
 
 // k_persist (the persistent one-lane-per-path kernel) in configuration `variant`, and its dynamic LDS:
-//   RT_VARIANT_PERSIST   <= 168 VGPRs (3 waves per SIMD), path levels in registers;
+//   RT_VARIANT_PERSIST   <= 168 VGPRs (3 waves per SIMD), path levels in registers (spp = 1: packed triangle tests);
 //   RT_VARIANT_PERSIST4  <= 128 VGPRs (4 waves per SIMD), path levels in a path buffer: in LDS after the wide stack
-//                        when 4 workgroups of that fit a CU, else a global slab;
+//                        (packed stack entries and triangle tests, SHP = 3) when 4 workgroups of that fit a CU, else
+//                        a global slab;
 //   RT_VARIANT_SHPOOL    PERSIST4 with each bounce level's shadow rays walked as a per-wave pool (rt_shpool.hpp);
 //                        PERSIST4 where the LDS path buffer does not fit;
 //   RT_VARIANT_SHDEFER   PERSIST4 with every level's shadow rays walked as ONE per-wave pool after the closest hits
 //                        (the path buffer plus a hit-triangle array in LDS; else PERSIST4);
 // a tile trace (A.tile_trace: the hybrid launch's measuring frame, PRT_TILE_TRACE) runs the 3-wave build with
 // per-tile timestamps.
-#ifndef PRT_P3_TQ
-#define PRT_P3_TQ 0  // (A/B builds: the 3-wave k_persist's spp = 1 build, 1; with packed triangle tests, 2)
-#endif
-#ifndef PRT_P4TQ_SPP
-#define PRT_P4TQ_SPP 0  // (A/B builds: the packed PERSIST4 build for spp > 1 too)
-#endif
 template <int MAXB>
 KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, size_t& dyn) {
     dyn = 0;
@@ -983,10 +978,10 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
         }
     }
     // PERSIST4 with packed stack entries and packed triangle tests (SHP = 3) where its LDS fits: sportscar 20-frame
-    // batches 0.922 -> 0.895 ms per frame, car_boxed 0.860 -> 0.841 (same box). spp = 1 builds only (the spp > 1
-    // build spills 144 B at the 128-VGPR cap)
+    // batches 0.922 -> 0.895 ms per frame, car_boxed 0.860 -> 0.841; car_boxed 4K at 64 spp 194.3 -> 191.6 ms per
+    // frame although that build spills 144 B (same box)
     if ((variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) &&
-        (A.spp <= 1 || PRT_P4TQ_SPP) && pbl_fits<MAXB>(A, device, 3)) {
+        pbl_fits<MAXB>(A, device, 3)) {
         dyn = pbl_bytes<MAXB>(A, 3);
         return persist4<MAXB, 3>(true, A.spp <= 1, count);
     }
@@ -996,15 +991,12 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
         // (the bench's batches: the spp = 1 build)
         return persist4<MAXB, 0>(pbl, A.spp <= 1, count);
     }
-#if PRT_P3_TQ == 2
+    // the 3-wave kernel's spp = 1 build with packed triangle tests (queues in static LDS): same box, single frames
+    // dragon 1.27 -> 1.16 ms, sportscar 2.40 -> 2.29, car_boxed 1.96 -> 1.84; the default rule's single frames (its
+    // cold tiles) sportscar 1.708 -> 1.671, car_boxed 1.210 -> 1.183
     if (A.spp <= 1)
         return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true, 0, false, true, 3>
                      : rtd::k_persist<MAXB, false, false, true, 3, false, true, 0, false, true, 3>;
-#elif PRT_P3_TQ == 1
-    if (A.spp <= 1)
-        return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true, 0, false, true>
-                     : rtd::k_persist<MAXB, false, false, true, 3, false, true, 0, false, true>;
-#endif
     return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true> : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
 }
 
