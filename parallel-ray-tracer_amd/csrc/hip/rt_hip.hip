@@ -940,7 +940,7 @@ template <int MAXB>
 size_t pbl_bytes(const rtd::KArgs& A, int shp = 0) {
     return sizeof(int) * (size_t)rtd::wstack_words(A.wcap, shp > 0) * rtd::BLOCK + sizeof(float4) * rtd::BLOCK * MAXB +
            (shp == 2 ? sizeof(int) * (rtd::BLOCK * MAXB + rtd::BLOCK / 64 * rtd::TQ_WORDS) : 0) +
-           (shp == 3 ? sizeof(int) * (rtd::BLOCK / 64 * rtd::TQ_WORDS) : 0);
+           (shp == 1 || shp == 3 ? sizeof(int) * (rtd::BLOCK / 64 * rtd::TQ_WORDS) : 0);
 }
 // Does that layout fit 4 workgroups per CU for this scene? (the LDS path buffer measured 1.2 % faster than the global
 // slab on dragon, 2.3 % on car_boxed; the shadow pool needs it)

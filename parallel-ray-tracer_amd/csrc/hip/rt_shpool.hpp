@@ -282,8 +282,12 @@ template <int MAXB, bool COUNT>
 __device__ __forceinline__ v3 trace_path_shp(const KArgs& A, bool alive, v3 o, v3 d, int* __restrict__ stk, Ctr& c,
                                              UCtr& u, int hpix, int* __restrict__ sstk, int wcap) {
     extern __shared__ int lds_dyn[];
-    float4* pb = (float4*)(lds_dyn + wstack_words(wcap, true) * BLOCK) + (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
+    float4* pb0 = (float4*)(lds_dyn + wstack_words(wcap, true) * BLOCK);
+    float4* pb = pb0 + (size_t)((threadIdx.x >> 6) * MAXB) * 64 + (threadIdx.x & 63);
     float4* pbw = pb - (threadIdx.x & 63);  // the wave's slots of level 0
+    // the wave's packed-triangle queue (TQ_*) after the path buffer, clear
+    int* tq = (int*)(pb0 + (size_t)BLOCK * MAXB) + (threadIdx.x >> 6) * TQ_WORDS;
+    tq_clear(tq);
     const DScene& s = A.s;
     const v3 amb = mk(s.amb_x, s.amb_y, s.amb_z);
     int L = 0;
@@ -300,7 +304,7 @@ __device__ __forceinline__ v3 trace_path_shp(const KArgs& A, bool alive, v3 o, v
         if (alive) {  // raytracer.c:101-147 as path_step
             float best;
             int nd;
-            const int orig = closest<false, COUNT, true, false, true>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0);
+            const int orig = closest<false, COUNT, true, false, true, true>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0, tq);
             if (hpix >= 0) {
                 if (it == 0) {
                     if (A.hit) A.hit[hpix] = orig;
@@ -331,7 +335,8 @@ __device__ __forceinline__ v3 trace_path_shp(const KArgs& A, bool alive, v3 o, v
         if (nh) {
             u.skip += nh * (unsigned)s.n_lights;  // less the rays walked (shadow_pool counts those in u.shad)
             const unsigned sh0 = u.shad;
-            shadow_pool<COUNT, 1>(s, [&](int) { return okm; }, pbw + it * 64, stk, sstk, wcap, A.regroup, c, u);
+            shadow_pool<COUNT, 1, true>(s, [&](int) { return okm; }, pbw + it * 64, stk, sstk, wcap, A.regroup, c, u,
+                                        tq);
             u.skip -= u.shad - sh0;
         }
         if (hit >= 0) {  // raytracer.c:144-172 as path_step, the lights' visibility from the pool
