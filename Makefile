@@ -15,7 +15,7 @@ HOST_FLAGS := -O2 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -Wall -Wextr
 HIP_FLAGS  := -O3 -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math $(PRT_DEFS) \
               -fhip-fp32-correctly-rounded-divide-sqrt -fPIC -Wall -Iinclude -I$(CSRC)
 
-.PHONY: all host hip cli oracle clean
+.PHONY: all host hip cli oracle clean asan
 
 all: host hip cli oracle
 
@@ -54,3 +54,20 @@ RCP_CHECK := tools/rcp/rcp_exhaustive
 hip: $(RCP_CHECK)
 $(RCP_CHECK): tools/rcp/rcp_exhaustive.hip $(CSRC)/hip/rt_device.hpp
 	$(HIPCC) $(HIP_FLAGS) -o $@ $<
+
+# Sanitizer build of the host library (SURVEY §5 "race detection / sanitizers"): librt_host.so -- the OBJ/MTL parser
+# restating cpu/src/triangle.c:26-126, the BVH builders, the wide collapse (rt_wide.cpp), the scene cache -- with
+# AddressSanitizer + UndefinedBehaviorSanitizer (any report is fatal), then the host-side tests against it
+# (prt._lib loads it through PRT_LIB_DIR; libasan is preloaded ahead of whatever LD_PRELOAD already holds, as ASan
+# must come first). Build container only (CPU; no GPU code is involved).
+ASAN_DIR   := build/asan
+ASAN_FLAGS := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all
+$(ASAN_DIR)/librt_host.so: $(HOST_SRCS) include/rt_host.h include/rt_types.h
+	@mkdir -p $(ASAN_DIR)
+	g++ $(HOST_FLAGS) $(ASAN_FLAGS) -shared -o $@ $(HOST_SRCS)
+
+asan: $(ASAN_DIR)/librt_host.so oracle
+	PRT_LIB_DIR=$(CURDIR)/$(ASAN_DIR) ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:abort_on_error=1 \
+	UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
+	LD_PRELOAD="$$(g++ -print-file-name=libasan.so)$${LD_PRELOAD:+:$$LD_PRELOAD}" \
+	python3 -m pytest -q -m "not gpu" -p no:cacheprovider tests/test_host.py tests/test_oracle.py

@@ -37,6 +37,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mrays/sec (primary+secondary) on dragon at 1920×1080, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+N_SIMD = 1024  # 256 CUs x 4 SIMDs
 
 
 def alg_bytes(st, pixels, n_lights, px_bytes=12):
@@ -54,7 +55,7 @@ def pmc_key(args, frames, world):
     """profiles/pmc_traffic.json key of one bench configuration (tools/pmc_traffic.py takes it from the bench line):
     every argument that changes what the profiled launches run"""
     a = args
-    return (f"{a.scene}_{a.width}x{a.height}_spp{a.spp}_b{a.bounces}_{a.kernel}_{a.variant}{'_tune' if a.tune else ''}_"
+    return (f"{a.scene}_{a.width}x{a.height}_spp{a.spp}_b{a.bounces}_{a.kernel}_{a.variant}_"
             f"{a.bvh}_{a.accel}_r{a.ploc_radius}_{a.output}_o{a.orbit:g}_rb{a.row_block}_s{a.streams}"
             f"{'_norot' if a.no_rotate else ''}_f{frames}_n{world}")
 
@@ -212,11 +213,6 @@ def main():
     ap.add_argument("--output", choices=("bgra8", "rgb"), default="bgra8",
                     help="what each frame's kernel writes and the gather moves: bgra8 = the BMP writer's quantised "
                          "pixel (rt_outputs.bgra, 4 B), rgb = the f32 vec_t pixel (12 B)")
-    ap.add_argument("--tune", action="store_true",
-                    help="rt_frame.tune = 1 for the batches: each context times the candidate launch configurations "
-                         "(default: the library's rule for batches, the 4-wave persistent kernel, which the tuner "
-                         "picks on every BASELINE configuration at N = 1 but not reliably per rank at N = 8, where "
-                         "its trials mislead it)")
     ap.add_argument("--variant", default="default", help="rt_frame.variant of the batches (prt.device.VARIANTS)")
     ap.add_argument("--no-rotate", action="store_true",
                     help="N > 1: keep each rank on its own block residue in every frame (default: frame f of rank "
@@ -255,6 +251,10 @@ def main():
                          "torch: torch.distributed.gather of the compact blocks (prt.dist.FrameGather); auto: native "
                          "on RCCL, torch on gloo (the one-GPU rehearsal: RCCL refuses two ranks on one device)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--timeout", type=float, default=240.0,
+                    help="N > 1: seconds any rank may wait on a collective (the process group's timeout, the native "
+                         "gather's bounded waits) and, x 2.5, on the whole run (a watchdog prints every thread's stack and "
+                         "exits non-zero): a first multi-GPU run that deadlocks fails loudly instead of hanging")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -265,6 +265,9 @@ def main():
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:  # watchdog: a deadlock anywhere in a multi-rank run ends it with stacks and a non-zero status
+        import faulthandler
+        faulthandler.dump_traceback_later(2.5 * args.timeout + 60, exit=True)
     rank = int(os.environ.get("RANK", "0"))
     if args.gpus != world:  # never a silent one-GPU run labelled N
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
@@ -277,12 +280,15 @@ def main():
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
 
+        tmo = datetime.timedelta(seconds=args.timeout)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
 
     from prt import device, host
     from prt.dist import FrameGather, NativeGather
@@ -350,7 +356,7 @@ def main():
         err = ""
         try:
             ng = NativeGather(rends, H, W, 1 if bgra else 3, rank, world, dist, like=fg.blocks[0], frames=F, block=B,
-                              rotate=not args.no_rotate)
+                              rotate=not args.no_rotate, timeout=args.timeout)
         except Exception as e:  # e.g. RCCL not loadable: every rank sees the same
             err = repr(e)
         errs = [err]
@@ -369,7 +375,8 @@ def main():
     n_r = my_rows[2]
     launch_no = [0]
     latest = [0, 0, 0]  # (block, frames, context) of the latest launch
-    variant = [args.variant]  # N > 1: the rule's choice, agreed over the ranks after setup
+    # N > 1: the rule's choice for each launch size (frames per launch), agreed over the ranks after setup
+    variant = {}
 
     def launch(nf):
         b = launch_no[0] % 2
@@ -378,14 +385,14 @@ def main():
         latest[:] = [b, nf, c]
         if gmode == "native":  # render, then the gather on the context's stream (ordered after the render)
             rends[c].render_frames(path(nf), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
-                                   kernel=args.kernel, variant=variant[0], tune=args.tune, **out(ng.target(c)[:nf]))
+                                   kernel=args.kernel, variant=variant.get(nf, args.variant), **out(ng.target(c)[:nf]))
             ng.gather(c, nf)
             return
         with torch.cuda.stream(streams[c]):  # block b is rendered by context c on its stream
             if fg.pending(b):
                 fg.finish(b)
             rends[c].render_frames(path(nf), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
-                                   kernel=args.kernel, variant=variant[0], tune=args.tune, **out(fg.target(b)))
+                                   kernel=args.kernel, variant=variant.get(nf, args.variant), **out(fg.target(b)))
             fg.start(b)
 
     def drain():
@@ -397,7 +404,7 @@ def main():
                     fg.finish(b)
 
     # setup, like the upload: the library's default rule measures its candidates on the first launches of a shape
-    # (PERSIST4 vs the shadow pool, rt_get_launch_info: trial / settled; with --tune the autotuner's trial launch), so
+    # (PERSIST4 vs the shadow pool, rt_get_launch_info: trial / settled), so
     # each batch size of the plan runs here until every context has settled, then `warmup` frames run untimed.
     rays_of = {}  # this rank's rays of a launch of nf frames (the same camera path every launch: deterministic)
     for nf in sorted(set(plan)):
@@ -412,15 +419,15 @@ def main():
                     settled = [all(every)]
                 if settled[0]:
                     break
-        if dist and variant[0] == "default" and not args.tune:
+        if dist and args.variant == "default":
             # every rank measured the rule's candidates on its own row set; small, noisy launches may choose
             # differently, and a rank on the slower kernel would set the pace: every rank takes the choice most
-            # contexts made (ties: rank 0's), explicitly
+            # contexts made for this launch size (ties: rank 0's), explicitly
             mine = [r.launch_info()["variant"] for r in rends]
             every = [None] * world
             dist.all_gather_object(every, mine)
             votes = [v for vs in every for v in vs]
-            variant[0] = max(dict.fromkeys(votes), key=votes.count)
+            variant[nf] = max(dict.fromkeys(votes), key=votes.count)
             for _ in range(n_streams):
                 launch(nf)
         rays_of[nf] = rends[(launch_no[0] - 1) % n_streams].stats()["rays"]
@@ -461,6 +468,8 @@ def main():
         timed.append((launch_no[0] % n_streams, nf))
         launch(nf)
     drain()
+    if ng:  # bounded: a gather whose peer never came aborts the communicator and raises instead of hanging below
+        ng.wait()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -496,10 +505,14 @@ def main():
     rays_frame = rays_total / K
 
     # algorithmic bytes of this rank's full-batch launch: one extra untimed launch with traversal counters
+    # (the timed launches' own configuration; a hybrid single frame's counters are its whole-frame kernel's, or
+    # k_persist's when hot tiles went to k_coop: the counting launch never measures or tries)
+    cv = timed_launch["variant"] if args.kernel != "strict" else args.variant
+    if cv == "hybrid":
+        cv = timed_launch["cold_variant"] if not timed_launch["hot_pct"] else "persist"
     rc = device.Renderer(local, counters=True, stream=stream)
     rc.upload(scene, accel=args.accel, ploc_radius=args.ploc_radius)
-    rc.render_frames(path(F), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
-                     kernel=args.kernel, variant=timed_launch["variant"] if args.kernel != "strict" else args.variant,
+    rc.render_frames(path(F), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp, kernel=args.kernel, variant=cv,
                      **out(fg.target(0)))
     stc = rc.stats()
     rc.close()
@@ -510,26 +523,33 @@ def main():
     # Single-frame latency of this rank's rows: the drop-in seam as the reference drives it (cpu/src/main.c:171-185,
     # gpu/src/main.cu:110-115: one render_frame per iteration, each waited for) with the library's default rule.
     # RT_VARIANT_HYBRID measures and tries its candidates on the first frames of a shape (rt_get_launch_info: trial /
-    # settled); the latency is the median HIP-event time of 9 frames after the rule has settled. Measured for the
-    # reference's fixed camera (frame_latency_ms) and for a walkthrough (every frame's camera moved: the rule is keyed
-    # by the frame's shape, so a moving camera settles the same way).
+    # settled); the latency is the median HIP-event time of the frames after the rule has settled -- 72 of them for the
+    # fixed camera, so that one periodic tile-list refresh (a settled measuring frame every 64 frames, `refresh`) is
+    # among them and its cost is reported too. Measured for the reference's fixed camera (frame_latency_ms), for a
+    # walkthrough (every frame's camera moved: the rule is keyed by the frame's shape, so a moving camera settles the
+    # same way), and for the fixed camera at the walkthrough's middle measured camera (fixed_at_walk_ms: the walk's
+    # cameras see more of the reflective knot, so the walk is compared with a fixed camera where the walk is).
     px_out = out(fg.target(0)[0] if F > 1 else fg.target(0))
 
-    def seam(cam_of, tune=False, n_after=9, limit=80):
+    def seam(cam_of, n_after=9, limit=120):
         rl = device.Renderer(local, stream=stream)
         rl.upload(scene, accel=args.accel, ploc_radius=args.ploc_radius)
-        ts, n, info = [], 0, {}
+        ts, idx, refresh, n, info = [], [], [], 0, {}
         while n < limit and len(ts) < n_after:
-            rl.render(cam_of(n), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp, kernel=args.kernel,
-                      tune=tune, **px_out)
+            rl.render(cam_of(n), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp, kernel=args.kernel, **px_out)
             ms = rl.sync()
-            n += 1
             info = rl.launch_info()
             if info["settled"]:
                 ts.append(ms)
+                idx.append(n)
+                if info["refresh"]:
+                    refresh.append(ms)
+            n += 1
         rl.close()
-        ts.sort()
-        return (ts[len(ts) // 2] if ts else float("nan")), n - len(ts), info
+        srt = sorted(ts)
+        return {"median": srt[len(srt) // 2] if ts else float("nan"), "mean": sum(ts) / len(ts) if ts else float("nan"),
+                "settle": n - len(ts), "info": info, "mid_camera": idx[len(idx) // 2] if idx else 0,
+                "refresh_ms": refresh, "frames": len(ts)}
 
     def walk(i):
         c = host.camera(W, H)
@@ -537,9 +557,15 @@ def main():
         c.ul.x += i * args.orbit
         return c
     nan = float("nan")
-    lat_default, settle_frames, seam_info = seam(lambda i: cam) if not args.no_latency else (nan, None, None)
-    lat_walk, settle_walk, _ = seam(walk) if not args.no_latency else (nan, None, None)
-    lat_tuned, _, _ = seam(lambda i: cam, tune=True) if not args.no_latency else (nan, None, None)
+    if not args.no_latency:
+        sd = seam(lambda i: cam, n_after=72)
+        sw = seam(walk)
+        sf = seam(lambda i, k=sw["mid_camera"]: walk(k))
+    else:
+        sd = sw = sf = {"median": nan, "mean": nan, "settle": None, "info": None, "mid_camera": None, "refresh_ms": [],
+                        "frames": 0}
+    lat_default, settle_frames, seam_info = sd["median"], sd["settle"], sd["info"]
+    lat_walk, settle_walk = sw["median"], sw["settle"]
     lat = torch.tensor([lat_default], dtype=torch.float64, device="cuda")
     if dist:
         dist.all_reduce(lat, op=dist.ReduceOp.MAX)
@@ -560,18 +586,36 @@ def main():
                 else:
                     pmc_stale = {"source": ent.get("source"), "reason": "measured on another librt_hip.so build"}
         traffic = pmc.get("hbm_bytes_per_launch")
-        achieved = bytes_launch / (k_avg_ms / 1e3) / 1e9
+        alg_gbs = bytes_launch / (k_avg_ms / 1e3) / 1e9  # algorithmic bytes per second (served by L1/L2/MALL)
         valu = pmc.get("valu_issue_frac")
+        insts = pmc.get("sq_insts_valu_per_launch")
+        # The roofline the line reports is the one that binds (verdict r4 item 7). With the scene cache-resident, HBM
+        # carries a few % of the algorithmic bytes and binds nothing; the kernel is bound by VALU issue and dependent
+        # loads. Its measured roofline is then the issue of USEFUL wave-VALU instructions (SQ_INSTS_VALU x SIMD
+        # efficiency: the share of lanes doing node work) against the SIMDs' issue peak, one wave64 fp32 instruction per
+        # 2 cycles per SIMD at the clock the PMC pass measured (GRBM_GUI_ACTIVE over the trace's launch time):
+        # frac = issue_frac = valu_issue_frac x simd_efficiency.
+        roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None}
         if traffic is None:
             bound_measured, limiter = None, "unmeasured: no PMC profile of this configuration and build (tools/profile.sh)"
         elif traffic < 0.05 * bytes_launch and valu is not None:
-            bound_measured = "latency/VALU"
+            bound_measured = "issue"
             limiter = (f"dependent-load latency and VALU issue: HBM traffic is {traffic / bytes_launch:.1%} of the "
                        "algorithmic bytes (the scene is L2/MALL-resident), VALU issues "
                        f"{valu:.0%} of the cycles, of which {simd_eff:.0%} of the lanes do node work")
+            if insts and pmc.get("trace_avg_ms"):
+                cycles = insts * 2 / (N_SIMD * valu)  # GRBM_GUI_ACTIVE / 8 XCDs per launch (PMC pass)
+                clk_hz = cycles / (pmc["trace_avg_ms"] / 1e3)
+                peak_i = N_SIMD * clk_hz / 2 / 1e9
+                ach_i = insts * simd_eff / (k_avg_ms / 1e3) / 1e9
+                roof = {"bound": "issue", "achieved": ach_i, "peak": peak_i, "unit": "G useful wave-VALU instr/s",
+                        "frac": ach_i / peak_i, "clock_mhz_measured": clk_hz / 1e6}
         else:
             bound_measured = "hbm" if traffic / (k_avg_ms / 1e3) / 1e9 > 0.5 * HBM_PEAK_GBS else "mixed"
             limiter = "see DESIGN.md §5"
+            hbm_gbs = traffic / (k_avg_ms / 1e3) / 1e9
+            roof = {"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": hbm_gbs / HBM_PEAK_GBS}
         result = {
             "metric": METRIC,
             "value": rays_total / elapsed / 1e6,
@@ -597,19 +641,28 @@ def main():
                        "launch": timed_launch, "accel_built": info["accel_built"], "accel_build_ms": info["build_ms"],
                        "wide_depth": info["wide_depth"]},
             "frame_latency_ms": lat.item() if not args.no_latency else None,
-            "frame_latency_detail": {"default_rule_ms": lat_default, "walkthrough_ms": lat_walk, "tuned_ms": lat_tuned,
+            "frame_latency_detail": {"default_rule_ms": lat_default, "default_rule_mean_ms": sd["mean"],
+                                     "refresh_frame_ms": sd["refresh_ms"], "walkthrough_ms": lat_walk,
+                                     "fixed_at_walk_ms": sf["median"], "walk_mid_camera": sw["mid_camera"],
                                      "settle_frames": settle_frames, "settle_frames_walkthrough": settle_walk,
                                      "choice": seam_info,
                                      "rule": "frame_latency_ms = the default rule (rt_render with rt_frame's launch fields "
                                              "zeroed, render + sync per frame as the reference's loop): median HIP-event "
-                                             "time of 9 frames after rt_get_launch_info reports the rule settled (its "
-                                             "measuring and trial frames excluded), fixed reference camera; "
-                                             "walkthrough_ms: the same with the camera moved every frame; tuned_ms: "
-                                             "rt_frame.tune = 1, the same way"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                                             "time of the 72 frames after rt_get_launch_info reports the rule settled (its "
+                                             "measuring and trial frames excluded; its periodic tile-list refresh, one "
+                                             "settled measuring frame per 64, included: refresh_frame_ms, and in "
+                                             "default_rule_mean_ms), fixed reference camera; walkthrough_ms: the median of 9 "
+                                             "settled frames with the camera moved every frame; fixed_at_walk_ms: the fixed "
+                                             "camera placed at the walkthrough's middle measured camera (walk_mid_camera)"},
+            "roofline": {**roof, "traffic": traffic,
                          "kernel_ms": k_avg_ms, "alg_bytes_per_launch": bytes_launch, "frames_per_launch": F,
-                         "achieved_steady": bytes_launch / F * K / elapsed / 1e9, "streams": n_streams,
+                         # the algorithmic bytes per second and against the HBM peak: not a bound (the
+                         # records come from L1/L2/MALL; it exceeds 1 on scenes with more bytes per ray)
+                         "alg_byte_achieved": alg_gbs, "alg_byte_frac": alg_gbs / HBM_PEAK_GBS,
+                         "alg_byte_achieved_steady": bytes_launch / F * K / elapsed / 1e9, "streams": n_streams,
+                         # L1 -> L2 read bytes per second (PMC TCP_TCC_READ_REQ x 64 B): the cache side that serves them
+                         "l2_read_gbs": (pmc["l2_read_bytes_per_launch"] / (k_avg_ms / 1e3) / 1e9
+                                         if pmc.get("l2_read_bytes_per_launch") else None),
                          # the same launch priced with SURVEY §8d's formula (reference record sizes): comparable
                          # with BASELINE.md's 3.45 / 6.3 Grays/s roofline-equivalent rates
                          "survey_bytes_per_launch": survey_launch,
@@ -654,11 +707,13 @@ def main():
                          "pmc_trace_avg_ms": pmc.get("trace_avg_ms"),
                          # what binds the kernel, measured (the contract's `bound` names the priced roofline)
                          "bound_measured": bound_measured, "limiter": limiter,
-                         "note": "achieved / frac: algorithmic bytes (the node / triangle / shading records the kernel "
-                                 "reads, DESIGN.md §5) of one launch / its HIP-event duration. They are served by L1/L2/"
-                                 "MALL, not HBM, so frac is not a bound: it exceeds 1 on scenes with more bytes per ray "
-                                 "(car_boxed, 64 spp). hbm_frac_measured is the HBM share (2 x FETCH_SIZE + WRITE_SIZE, "
-                                 "PMC); issue_frac = valu_issue_frac x simd_efficiency is the measured bound"},
+                         "note": "bound / achieved / peak / frac: the roofline that binds, from this build's PMC "
+                                 "passes (profiles/pmc_traffic.json): with HBM traffic under 5 % of the algorithmic bytes, "
+                                 "'issue' = useful wave-VALU instructions (SQ_INSTS_VALU x simd_efficiency) per second "
+                                 "against the SIMDs' issue peak at the measured clock, so frac = issue_frac; else HBM "
+                                 "traffic against 8 TB/s. alg_byte_*: algorithmic bytes (DESIGN.md §5) per HIP-event "
+                                 "launch time, served by L1/L2/MALL (not a bound). hbm_frac_measured = (2 x FETCH_SIZE + "
+                                 "WRITE_SIZE) / time / peak"},
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = args.cpu_threads or min(16, usable_cpus())

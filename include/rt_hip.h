@@ -14,7 +14,7 @@
  * The per-pixel hot path (ray generation, BVH traversal, ray-triangle intersection, Lambert/Blinn
  * shading with shadow rays, the BOUNCES reflection loop, clamp) runs in ONE HIP kernel per frame
  * (or per batch of frames, rt_render_frames). Every launch configuration is chosen through the
- * arguments below (rt_frame.variant / tune / waves_cap / dealing / regroup); the library reads no
+ * arguments below (rt_frame.variant / waves_cap / dealing / regroup / hot_pct); the library reads no
  * environment variable on the render path except two diagnostics (PRT_TILE_TRACE, PRT_TUNE_LOG).
  */
 #ifndef RT_HIP_H
@@ -97,25 +97,27 @@ enum {
 /* rt_frame.variant: launch configuration of RT_KERNEL_FAST */
 enum {
     RT_VARIANT_DEFAULT = 0,  /* the library's rule, measured per frame shape: frame batches and spp > 1 try
-                                RT_VARIANT_PERSIST4 and RT_VARIANT_SHPOOL on their first launches and keep the faster
-                                (RT_VARIANT_PERSIST4 where the pool's LDS path buffer does not fit); single 1-spp frames run RT_VARIANT_HYBRID (RT_VARIANT_PERSIST where it cannot
-                                run); with rt_frame.tune = 1 the autotuner's candidates instead (rt_get_launch_info) */
+                                RT_VARIANT_PERSIST4 and the pool kernel -- RT_VARIANT_SHDEFER where its LDS path buffer
+                                fits, else RT_VARIANT_SHPOOL -- three times each on their first launches and keep the
+                                faster by the median (RT_VARIANT_PERSIST4 alone where no pool fits); single 1-spp frames
+                                run RT_VARIANT_HYBRID (RT_VARIANT_PERSIST where it cannot run); rt_get_launch_info */
     RT_VARIANT_PERSIST = 1,  /* k_persist: one lane per pixel path, walks in lockstep, 3 waves per SIMD */
     RT_VARIANT_PERSIST4 = 2, /* k_persist at 4 waves per SIMD (path levels in LDS) */
     /* 3: the split pipeline (closest chains / shadow batches / resolve), measured slower, removed in round 4: refused */
     RT_VARIANT_COOP2 = 4,    /* k_coop: 2 lanes per ray (shorter chains for small row sets) */
     RT_VARIANT_COOP4 = 5,    /* k_coop: 4 lanes per ray */
     /* 6: k_coop with 8 lanes per ray, 3x slower, removed in round 4: refused */
-    RT_VARIANT_FAN = 7,      /* k_fan: 1 + lights lanes per pixel (shadow fan-out; 1..7 lights) */
+    /* 7: k_fan (1 + lights lanes per pixel, shadow fan-out), never chosen by a rule nor won a trial, removed in
+       round 5: refused */
     /* 8, 9: k_chain (each lane's walks back to back), measured slower and removed in round 2: refused */
     /* 10: k_pool (tile-local LDS ray queues behind workgroup barriers), measured slower, removed in round 4: refused */
     RT_VARIANT_HYBRID = 11,  /* single 1-spp frames: the tiles a measuring frame of the same SHAPE found costliest through
                                 k_coop (2 or 4 lanes per ray) on a second stream while k_persist or the shadow pool renders
                                 the rest. The first frame of a shape measures (k_persist with per-tile times), the next
-                                ones try the candidates -- including the whole-frame kernels -- twice each, and the fastest
-                                renders from then on; every 64 frames a measuring frame renews the tile lists for a moving
-                                camera. Nothing waits on the host: measurements and trials are read by event queries
-                                (rt_frame.hot_pct > 0: that threshold and rt_frame.hot_kernel, no trials) */
+                                ones try the candidates -- including the whole-frame kernels -- three times each, and the
+                                best median renders from then on; every 64 frames a measuring frame renews the tile lists
+                                for a moving camera. Nothing waits on the host: measurements and trials are read by event
+                                queries (rt_frame.hot_pct > 0: that threshold and rt_frame.hot_kernel, no trials) */
     /* 12: k_relay (1 + lights waves per tile, LDS hand-off), measured slower, removed in round 4: refused */
     RT_VARIANT_SHPOOL = 13,  /* k_persist at 4 waves per SIMD with each bounce level's shadow rays (every pixel's, every
                                 light's) walked as ONE per-wave pool: a lane whose walk ends takes the next unassigned ray,
@@ -132,9 +134,8 @@ enum {
 /* rt_frame.hot_kernel: the kernel RT_VARIANT_HYBRID sends the hot tiles to when rt_frame.hot_pct > 0 */
 enum {
     RT_HOT_COOP4 = 0, /* k_coop, 4 lanes per ray */
-    RT_HOT_COOP2 = 1, /* k_coop, 2 lanes per ray */
-    RT_HOT_FAN = 2    /* k_fan, 1 + lights lanes per pixel */
-    /* 3: k_relay, removed in round 4: refused */
+    RT_HOT_COOP2 = 1  /* k_coop, 2 lanes per ray */
+    /* 2: k_fan, removed in round 5; 3: k_relay, removed in round 4: refused */
 };
 
 /* rt_frame.dealing: order in which persistent waves take their tiles (k_persist 8x8, k_pool 16x16) */
@@ -165,9 +166,9 @@ typedef struct rt_frame {
                       * even out; compact rows whose image row falls at or past height are skipped. */
     /* launch configuration (RT_KERNEL_FAST; all zero = the library's defaults) */
     int variant;   /* RT_VARIANT_* */
-    int tune;      /* 1 (with RT_VARIANT_DEFAULT): the first frame of each (scene upload, frame shape) runs every
-                      candidate variant three times into the same outputs, the next frame of that shape reads their
-                      HIP-event times and the fastest renders from then on; 0: the default rule, no trial launches */
+    int tune;      /* 0 or 1, both the default rule (which measures its candidates itself). Until round 4, 1 selected
+                      a separate autotuner whose candidates left out the hybrid launch; it was slower than the default
+                      rule on every BASELINE scene and was removed. Other values are refused. */
     int waves_cap; /* persistent grids: at most this many workgroups (4 waves each) per CU; 0 = occupancy limit */
     int dealing;   /* RT_DEAL_* */
     int regroup;   /* RT_VARIANT_SHPOOL: idle lanes of a wave that trigger a refill from the pool; 0 = 16 */
@@ -234,21 +235,26 @@ int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_frame* frame, const rt
  * stats of the call are the batch's sums. rt_gather / rt_download_bmp need a single-frame render. */
 int rt_render_frames(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_frame* frame,
                      const rt_outputs* out);
-/* What the last rt_render / rt_render_frames ran (no synchronisation): the default rule and rt_frame.tune resolve
- * RT_VARIANT_DEFAULT per shape, trying candidates on the first frames of a shape. A caller timing the drop-in seam
- * skips frames until `settled` (the reference's own loop needs no such thing: every frame is bit-exact either way). */
+/* What the last rt_render / rt_render_frames ran (no synchronisation): the default rule resolves RT_VARIANT_DEFAULT per
+ * shape, trying candidates on the first frames of a shape. A caller timing the drop-in seam skips frames until
+ * `settled` (the reference's own loop needs no such thing: every frame is bit-exact either way). */
 typedef struct rt_launch_info {
     int variant;      /* RT_VARIANT_* the last render ran (0 for RT_KERNEL_STRICT) */
     int hot_pct;      /* RT_VARIANT_HYBRID with hot tiles: the threshold, else 0 */
     int hot_lanes;    /* its lanes per ray (k_coop) or per pixel (k_fan) */
     int cold_variant; /* its kernel of the cold tiles (RT_VARIANT_PERSIST or RT_VARIANT_SHPOOL) */
-    int trial;        /* 1: a measuring or trial frame of the default rule (or rt_frame.tune) */
-    int settled;      /* 1: the configuration of this shape is decided; no trial frames follow */
+    int trial;        /* 1: a measuring or trial frame of the default rule */
+    int settled;      /* 1: the configuration of this shape is decided: no trial frames follow (the hybrid rule's
+                         periodic list refresh, every 64 frames of a shape, is reported by `refresh`) */
+    int refresh;      /* 1: a decided hybrid shape's measuring frame that renews its tile lists (k_persist with per-tile
+                         times; part of the rule's steady cost, settled = 1) */
 } rt_launch_info;
 int rt_get_launch_info(rt_ctx* ctx, rt_launch_info* info);
-/* load_from_gpu(): copies the last frame's compact rows to host (synchronous); nullable args */
+/* load_from_gpu(): copies the last frame's compact rows to host (synchronous); nullable args. RT_E_KERNEL when the
+ * render reported a traversal-stack overflow (its frame is not valid). */
 int rt_download(rt_ctx* ctx, float* h_rgb, int* h_hit);
-/* waits for the stream; kernel_ms (nullable) = the last render's kernel time from HIP events */
+/* waits for the stream; kernel_ms (nullable) = the last render's kernel time from HIP events; RT_E_KERNEL when the
+ * last render reported a traversal-stack overflow */
 int rt_sync(rt_ctx* ctx, float* kernel_ms);
 /* per-launch kernel times (HIP events recorded on the context stream around each kernel) of the last
  * n launches (n <= 64), oldest first; synchronises; returns the number written or < 0 */
@@ -280,11 +286,14 @@ int rt_gather_to(rt_ctx* const* ctxs, int n, int root, void* d_dst);
  * x 3 floats or x 1 uint32; a device pointer on the root's device) or, with d_dst NULL, into the root
  * context's own buffer, which then is its last render (rt_download / rt_download_bmp). Collective: every rank
  * calls it. Asynchronous on the streams. Hit indices are not gathered (rt_gather does).
- * Across processes the ranks exchange their 64-B row-set descriptors (one ncclAllGather, a host wait) only when
- * a rank's own part changes -- the first gather, and a new frame shape or row set, which changes every rank's
- * part at once -- and the root checks that exchange's layout partitions each frame and, on the layout's first
- * gather, that every pixel of the gathered frames arrived (one host wait per layout); later gathers of the same
- * layout neither exchange nor wait. */
+ * Across processes the ranks exchange their 64-B row-set descriptors (one ncclAllGather, a host wait) only on what
+ * every rank sees the same way: the first gather, a new frame size, frame count or pixel kind (fields every rank of
+ * a valid layout shares), or rt_comm_relayout called by every rank. A rank whose own rows change without one of
+ * those is refused (RT_E_ARG) before any collective call. The root checks each exchanged layout partitions every
+ * frame and, on the layout's first gather, that every pixel of the gathered frames arrived (one host wait per
+ * layout); later gathers of the same layout neither exchange nor wait. Every host wait on a collective is bounded
+ * (rt_comm_set_timeout, default 120 s): a peer that never joins turns into RT_E_TIMEOUT and an aborted communicator
+ * (ncclCommAbort), never a hang. */
 typedef struct rt_comm rt_comm;
 #define RT_COMM_ID_BYTES 128 /* sizeof(ncclUniqueId) */
 typedef struct rt_comm_info {
@@ -301,6 +310,15 @@ int rt_comm_gather(rt_comm* comm, int root, void* d_dst);
  * context the communicator was built with); multi-process communicators only. Successive gathers of one
  * communicator run in their call order, whatever streams their contexts use. */
 int rt_comm_gather_from(rt_comm* comm, rt_ctx* src, int root, void* d_dst);
+/* Collective: every rank calls it before the same gather, which then exchanges the row sets again (a rank's rows
+ * may change there). */
+int rt_comm_relayout(rt_comm* comm);
+/* The deadline of every host wait on a collective of this communicator (seconds > 0; default 120). */
+int rt_comm_set_timeout(rt_comm* comm, double seconds);
+/* Waits, bounded by that deadline, until the communicator's last gather has run on the device: RT_OK, or
+ * RT_E_TIMEOUT with the communicator aborted (a peer never joined). For a caller that would otherwise block in a
+ * device synchronisation behind a collective that cannot complete. */
+int rt_comm_wait(rt_comm* comm);
 int rt_comm_get_info(rt_comm* comm, rt_comm_info* info);
 const char* rt_comm_last_error(rt_comm* comm);
 void rt_comm_destroy(rt_comm* comm);

@@ -58,7 +58,9 @@ enum {
     RT_E_HIP = -4,      /* HIP runtime error (see rt_last_error) */
     RT_E_STATE = -5,    /* call out of order (e.g. render before upload) */
     RT_E_NODEVICE = -6, /* no GPU visible */
-    RT_E_EMPTY = -7     /* no triangles: "no triangles, cannot build bvh." (bvh.c:361-364) */
+    RT_E_EMPTY = -7,    /* no triangles: "no triangles, cannot build bvh." (bvh.c:361-364) */
+    RT_E_KERNEL = -8,   /* a kernel reported an error: a traversal stack overflowed (the frame is not trustworthy) */
+    RT_E_TIMEOUT = -9   /* a collective did not complete within its deadline (the communicator is aborted) */
 };
 
 #ifdef __cplusplus

@@ -2,11 +2,10 @@
 //
 //   raytracer [threads] [ntris] [--scene NAME] [--assets DIR] [--width W] [--height H]
 //             [--bounces B] [--iterations K] [--warmup W] [--bvh-heuristic H] [--seed S]
-//             [--gpus N] [--gather auto|rccl|peer] [--spp S] [--kernel fast|strict|VARIANT] [--tune]
+//             [--gpus N] [--gather auto|rccl|peer] [--spp S] [--kernel fast|strict|VARIANT]
 //             [--out FILE.bmp] [--cache DIR]
-//   VARIANT: persist, persist4, coop2, coop4, fan, hybrid, shpool, shdefer (rt_frame.variant; the fast
-//   kernel's launch configurations, all rendering the same bits); --tune: measure the candidates on the
-//   first frame and keep the fastest (rt_frame.tune)
+//   VARIANT: persist, persist4, coop2, coop4, hybrid, shpool, shdefer (rt_frame.variant; the fast
+//   kernel's launch configurations, all rendering the same bits; default: the library's measured rule)
 //
 // Positional arguments and defaults are the reference's (options.h: 1920x1080, car_boxed, BOUNCES 4,
 // ITERATIONS 1, BVH_HEURISTIC 3, SEED 1; main.c:97-131: `threads` in 1..63, `ntris` = random mode).
@@ -36,7 +35,7 @@ struct Args {
     int threads = 1;
     long ntris = -1;
     std::string scene = "car_boxed", assets = "../assets", out, kernel = "fast", cache, gather = "auto";
-    int W = 1920, H = 1080, bounces = 4, iterations = 1, warmup = 0, heuristic = 3, gpus = 1, spp = 1, tune = 0;
+    int W = 1920, H = 1080, bounces = 4, iterations = 1, warmup = 0, heuristic = 3, gpus = 1, spp = 1;
     unsigned seed = 1;
 };
 
@@ -66,7 +65,6 @@ Args parse(int argc, char** argv) {
         else if (s == "--gpus") a.gpus = std::atoi(val().c_str());
         else if (s == "--spp") a.spp = std::atoi(val().c_str());
         else if (s == "--kernel") a.kernel = val();
-        else if (s == "--tune") a.tune = 1;
         else if (s == "--out") a.out = val();
         else if (s == "--gather") a.gather = val();
         else if (s == "--cache") a.cache = val();
@@ -163,7 +161,7 @@ int main(int argc, char** argv) {
         const char* name;
         int variant;
     } variants[] = {{"fast", RT_VARIANT_DEFAULT}, {"persist", RT_VARIANT_PERSIST}, {"persist4", RT_VARIANT_PERSIST4},
-                    {"coop2", RT_VARIANT_COOP2},  {"coop4", RT_VARIANT_COOP4},     {"fan", RT_VARIANT_FAN},
+                    {"coop2", RT_VARIANT_COOP2},  {"coop4", RT_VARIANT_COOP4},
                     {"hybrid", RT_VARIANT_HYBRID}, {"shpool", RT_VARIANT_SHPOOL}, {"shdefer", RT_VARIANT_SHDEFER}};
     int kern = a.kernel == "strict" ? RT_KERNEL_STRICT : -1, variant = RT_VARIANT_DEFAULT;
     for (const auto& v : variants)
@@ -198,7 +196,6 @@ int main(int argc, char** argv) {
                 for (int j = g; j < nb; j += G) nr += std::min(B, a.H - j * B);
                 rt_frame f{a.W, a.H, g * B, G * B, nr, a.bounces, a.spp, kern, B};
                 f.variant = variant;
-                f.tune = a.tune;
                 int s = rt_render(ctx[g], &cam, &f, nullptr);
                 if (s == RT_OK) s = rt_sync(ctx[g], nullptr);
                 status[g] = s;

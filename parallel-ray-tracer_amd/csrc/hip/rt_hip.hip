@@ -22,9 +22,9 @@
 #include "rt_kernels.hpp"
 #include "rt_shpool.hpp"
 #include "rt_coop.hpp"
-#include "rt_fan.hpp"
 #include "rt_output.hpp"
 #include "rt_build.hpp"
+#include "rt_comm_logic.hpp"
 
 #include <chrono>
 #include <hipcub/hipcub.hpp>
@@ -76,6 +76,9 @@ struct rt_ctx {
     float4* d_mats = nullptr;
     float4* d_lights = nullptr;
     int n_lights = 0, n_tris = 0;
+    // the packed builds' bounds: 5-byte stack entries hold a 24-bit child base (rtd::WIDE_MAX_NODES wide nodes per
+    // view), packed triangle-test jobs a 26-bit triangle (rtd::TQ_MAX_TRIS); larger scenes run the unpacked builds
+    bool pk_ok = true, tq_ok = true;
     float amb[3] = {0.5f, 0.5f, 0.5f};
     bool has_scene = false;
     rt_scene_info info{};  // what the last upload built (rt_get_scene_info)
@@ -114,6 +117,7 @@ struct rt_ctx {
     unsigned* d_full_bgra = nullptr;  // gathered BGRA8 frames (rt_gather / rt_comm_gather of bgra renders)
     size_t full_bgra_cap = 0;
     unsigned long long* d_counters = nullptr;  // rtd::NCOUNT
+    unsigned long long* h_err = nullptr;       // pinned: the last render's error counter (rtd::C_ERR), read by rt_sync / rt_download
     std::unordered_map<long long, int*> orders;  // tile dealing orders (rt_frame.dealing), per tx x ty tile grid
     unsigned int* d_work = nullptr;
     static constexpr int NEV = 64;  // ring of per-launch event pairs (rt_kernel_times)
@@ -123,33 +127,20 @@ struct rt_ctx {
     hipEvent_t copy_ev = nullptr;             // rt_gather: this (source) context's peer copies issued
     long long launches = 0;
     bool rendered = false;
-    // launch autotuning of RT_KERNEL_FAST (rt_render): the candidate configurations are timed on the
-    // first frame of a (scene upload, frame shape) and the fastest one renders the frames after it
-    static constexpr int TUNE_MAX = 10, TUNE_REPS = 3;
-    struct Tune {
-        long long scene = -1;
-        int W = 0, rows = 0, bounces = 0, spp = 0, frames = 0;
-        int off = 0, stride = 0, block = 0, shift = 0, dealing = 0, cap_req = 0;  // the rest of the frame shape
-        int n = 0, choice = -1;  // candidates; the chosen one (-1: not decided yet)
-        bool pending = false;    // trial launches enqueued, timings not read yet
-        int mode[TUNE_MAX] = {};  // RT_VARIANT_*
-        int cap[TUNE_MAX] = {};
-        float ms[TUNE_MAX] = {};
-        hipEvent_t e0[TUNE_MAX * TUNE_REPS] = {}, e1[TUNE_MAX * TUNE_REPS] = {};
-    };
     // the default rule of frame batches and spp > 1 (PERSIST4 or SHPOOL), measured per shape (render_batch)
     struct BatchRule {
         long long scene = -1;
         int W = 0, rows = 0, off = 0, stride = 0, block = 0, shift = 0, bounces = 0, spp = 0, frames = 0, dealing = 0,
             cap_req = 0;
-        static constexpr int ROUNDS = 2;
-        long long launch[2][ROUNDS] = {{-1, -1}, {-1, -1}};
+        // trials per candidate: 3, decided by the minimum -- or, for launches longer than LONG_MS, the median (the
+        // 64-spp configuration's 190-ms launches of one kernel ranged 186-199 ms on one box; the minimum of two trials
+        // picked either kernel)
+        static constexpr int ROUNDS = 3;
+        static constexpr float LONG_MS = 50.0f;
+        long long launch[2][ROUNDS] = {{-1, -1, -1}, {-1, -1, -1}};
         int choice = -1;
     };
     std::vector<BatchRule> brules;
-    // one tuning state per (scene upload, frame shape: width, rows, their offset / stride / block / shift,
-    // bounces, spp, frames, dealing, waves cap): a context that alternates frame shapes keeps every decision
-    std::vector<Tune> tunes;
     long long scene_gen = 0;  // bumped by every upload
     // RT_VARIANT_HYBRID (single 1-spp frames), keyed by the frame's SHAPE: the per-tile times of a measuring k_persist
     // frame, the candidates' tile lists they give (the hot kernel's tiles of the costliest 8x8 tiles; the rest for the
@@ -163,11 +154,11 @@ struct rt_ctx {
         static constexpr int ROUNDS = 3;    // trials per candidate, chosen by their median (single frames are noisy, and
                                             // some two-stream launches bimodal)
         static constexpr int REFRESH = 64;  // frames of a shape between measuring frames once it is decided
-        // candidates: hot threshold (0 = the cold kernel over the whole frame), lanes per ray, k_fan or k_coop for
-        // the hot tiles, the cold tiles' kernel (RT_VARIANT_PERSIST / SHPOOL); their lists at d_lists + at[c]
+        // candidates: hot threshold (0 = the cold kernel over the whole frame), lanes per ray of k_coop for the hot
+        // tiles, the cold tiles' kernel (RT_VARIANT_PERSIST / SHPOOL); their lists at d_lists + at[c]
         int nc = 0, choice = -1;
         int pct[NCAND] = {}, lanes[NCAND] = {}, cold[NCAND] = {}, n_hot[NCAND] = {}, n_cold[NCAND] = {};
-        bool fan[NCAND] = {}, lpt[NCAND] = {};
+        bool lpt[NCAND] = {};
         size_t at[NCAND] = {};
         long long launch[NCAND][ROUNDS] = {};
         float ms[NCAND] = {};
@@ -188,7 +179,8 @@ namespace {
 // RT_VARIANT_HYBRID candidates: pct = 0: the cold kernel over the whole frame; else the 8x8 tiles slower than pct % of the
 // slowest tile of the measuring frame go to k_coop with `lanes` lanes per ray while the cold kernel renders the rest
 // (each candidate is tried ROUNDS times; hybrid_pick). Measured: car_boxed hot > 45 % k_coop<4>,
-// sportscar hot > 60 % k_coop<2> / <4>, dragon the whole-frame kernels; k_fan and k_relay hot tiles never won.
+// sportscar hot > 60 % k_coop<2> / <4>, dragon the whole-frame kernels; k_fan and k_relay hot tiles never won
+// (both removed).
 // lpt: the cold tiles dealt costliest first by the measuring frame's per-tile times (longest processing time first,
 // the classic makespan heuristic: a single frame ends with its slowest tile) instead of centre-out; with pct = 0 the
 // whole frame that way.
@@ -204,10 +196,10 @@ struct HotCand {
 constexpr HotCand HYBRID_CANDS[] = {{0, 0, RT_VARIANT_SHPOOL, true},   {0, 0, RT_VARIANT_PERSIST, true},
                                     {45, 4, RT_VARIANT_PERSIST, true}, {60, 4, RT_VARIANT_PERSIST, false},
                                     {60, 2, RT_VARIANT_PERSIST, false}};
-// pixel tile of a group kernel (rtd::GTile): k_coop<2> / k_fan<2> 8x4, k_coop<4> / k_fan<4> 4x4, k_fan<8> 4x2
+// pixel tile of a group kernel (rtd::GTile): k_coop<2> 8x4, k_coop<4> 4x4
 inline void hot_tile(int g, int& tw, int& th) {
     tw = g == 2 ? 8 : 4;
-    th = g == 8 ? 2 : 4;
+    th = 4;
 }
 
 const char* variant_name(int v) {
@@ -216,7 +208,6 @@ const char* variant_name(int v) {
         case RT_VARIANT_PERSIST4: return "persist4";
         case RT_VARIANT_COOP2: return "coop2";
         case RT_VARIANT_COOP4: return "coop4";
-        case RT_VARIANT_FAN: return "fan";
         case RT_VARIANT_HYBRID: return "hybrid";
         case RT_VARIANT_SHPOOL: return "shpool";
         case RT_VARIANT_SHDEFER: return "shdefer";
@@ -411,6 +402,7 @@ extern "C" int rt_create(const rt_opts* opts, rt_ctx** out) {
     if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_counters, sizeof(unsigned long long) * rtd::NCOUNT);
     if (e == hipSuccess) e = hipMalloc((void**)&ctx->d_work, 1024);
     if (e == hipSuccess) e = hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&ctx->h_err, sizeof(unsigned long long), hipHostMallocDefault);
     if (e != hipSuccess) {
         rt_destroy(ctx);
         return RT_E_HIP;
@@ -864,6 +856,8 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     ctx->prim_tris_n = prim_nodes.empty() ? 0 : prim_tris_n;
     ctx->n_lights = sc->n_lights;
     ctx->n_tris = n;
+    ctx->pk_ok = std::max(ctx->wide_n, std::max(ctx->unit_n, ctx->prim_n)) <= rtd::WIDE_MAX_NODES;
+    ctx->tq_ok = n < rtd::TQ_MAX_TRIS;
     ctx->amb[0] = sc->amb.x;
     ctx->amb[1] = sc->amb.y;
     ctx->amb[2] = sc->amb.z;
@@ -966,11 +960,11 @@ bool pbl_fits(const rtd::KArgs& A, int device, int shp = 0) {
 // a tile trace (A.tile_trace: the hybrid launch's measuring frame, PRT_TILE_TRACE) runs the 3-wave build with
 // per-tile timestamps.
 template <int MAXB>
-KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, size_t& dyn) {
+KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, size_t& dyn, bool pk_ok, bool tq_ok) {
     dyn = 0;
     if (A.tile_trace)
         return count ? rtd::k_persist<MAXB, false, true, true, 3, true, true> : rtd::k_persist<MAXB, false, false, true, 3, true, true>;
-    if (variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) {
+    if ((variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) && pk_ok && tq_ok) {
         const int shp = variant == RT_VARIANT_SHDEFER ? 2 : 1;
         if (pbl_fits<MAXB>(A, device, shp)) {
             dyn = pbl_bytes<MAXB>(A, shp);
@@ -980,8 +974,8 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
     // PERSIST4 with packed stack entries and packed triangle tests (SHP = 3) where its LDS fits: sportscar 20-frame
     // batches 0.922 -> 0.895 ms per frame, car_boxed 0.860 -> 0.841; car_boxed 4K at 64 spp 194.3 -> 191.6 ms per
     // frame although that build spills 144 B (same box)
-    if ((variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) &&
-        pbl_fits<MAXB>(A, device, 3)) {
+    if ((variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) && pk_ok &&
+        tq_ok && pbl_fits<MAXB>(A, device, 3)) {
         dyn = pbl_bytes<MAXB>(A, 3);
         return persist4<MAXB, 3>(true, A.spp <= 1, count);
     }
@@ -994,7 +988,7 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
     // the 3-wave kernel's spp = 1 build with packed triangle tests (queues in static LDS): same box, single frames
     // dragon 1.27 -> 1.16 ms, sportscar 2.40 -> 2.29, car_boxed 1.96 -> 1.84; the default rule's single frames (its
     // cold tiles) sportscar 1.708 -> 1.671, car_boxed 1.210 -> 1.183
-    if (A.spp <= 1)
+    if (A.spp <= 1 && tq_ok)
         return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true, 0, false, true, 3>
                      : rtd::k_persist<MAXB, false, false, true, 3, false, true, 0, false, true, 3>;
     return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true> : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
@@ -1002,23 +996,16 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
 
 // `cap`: workgroups per CU at most (0: the occupancy limit); the grid never exceeds the tiles / 4.
 template <int MAXB>
-void launch_paths(const rtd::KArgs& A, int variant, bool count, int device, hipStream_t s, int cap) {
+void launch_paths(const rtd::KArgs& A, int variant, bool count, int device, hipStream_t s, int cap, bool pk_ok,
+                  bool tq_ok) {
     size_t dyn = 0;
-    const KFn k = persist_kernel<MAXB>(A, variant, count, device, dyn);
+    const KFn k = persist_kernel<MAXB>(A, variant, count, device, dyn, pk_ok, tq_ok);
     const int blocks = std::max(1, std::min(resident(k, device, cap > 0 ? cap : 8, dyn), (A.n_tiles * A.n_frames + 3) / 4));
     k<<<blocks, rtd::BLOCK, dyn, s>>>(A);
 }
 
 rtd::DBvh dview(const DevView& v) { return rtd::DBvh{v.nodes, v.leaves, v.tris, v.orig, v.root}; }
 
-// k_fan (rt_fan.hpp): R lanes per pixel (closest chain + R - 1 shadow lanes), 64 / R-pixel tiles
-template <int MAXB>
-KFn fan_kernel(int R, bool count) {
-    using rtd::k_fan;
-    if (R == 2) return count ? k_fan<MAXB, true, 2, 3, false, true> : k_fan<MAXB, false, 2, 3, false, true>;
-    if (R == 8) return count ? k_fan<MAXB, true, 8, 3, false, true> : k_fan<MAXB, false, 8, 3, false, true>;
-    return count ? k_fan<MAXB, true, 4, 3, false, true> : k_fan<MAXB, false, 4, 3, false, true>;
-}
 // k_coop (rt_coop.hpp): G = 2 or 4 lanes per ray; one wave per tile of 64 / G pixels
 template <int MAXB>
 KFn coop_kernel(int G, bool count) {
@@ -1028,8 +1015,8 @@ KFn coop_kernel(int G, bool count) {
 }
 // never more workgroups than tiles / 4
 template <int MAXB>
-int launch_group(const rtd::KArgs& A, bool fan, int g, bool count, int device, hipStream_t s, int cap) {
-    const KFn k = fan ? fan_kernel<MAXB>(g, count) : coop_kernel<MAXB>(g, count);
+int launch_group(const rtd::KArgs& A, int g, bool count, int device, hipStream_t s, int cap) {
+    const KFn k = coop_kernel<MAXB>(g, count);
     const int blocks = std::max(1, std::min(resident(k, device, cap), (A.n_tiles * A.n_frames + 3) / 4));
     k<<<blocks, rtd::BLOCK, 0, s>>>(A);
     return RT_OK;
@@ -1145,14 +1132,13 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     while (g * g < f->spp) g++;
     if (f->spp < 1 || g * g != f->spp || g > 16) return arg_err(ctx, "rt_render: spp must be a square 1..256");
     if (f->kernel < RT_KERNEL_AUTO || f->kernel > RT_KERNEL_FAST) return arg_err(ctx, "rt_render: bad kernel");
-    // (variants 3, 6, 8, 9, 10, 12 -- the split pipeline, k_coop<8>, k_chain, k_pool, k_relay -- measured slower
-    // than k_persist and were removed: refused)
+    // (variants 3, 6, 7, 8, 9, 10, 12, 14 -- the split pipeline, k_coop<8>, k_fan, k_chain, k_pool, k_relay, k_stream
+    // -- measured slower than k_persist and were removed: refused)
     const bool known = f->variant == RT_VARIANT_DEFAULT || f->variant == RT_VARIANT_PERSIST ||
                        f->variant == RT_VARIANT_PERSIST4 || f->variant == RT_VARIANT_COOP2 ||
-                       f->variant == RT_VARIANT_COOP4 || f->variant == RT_VARIANT_FAN ||
-                       f->variant == RT_VARIANT_HYBRID || f->variant == RT_VARIANT_SHPOOL ||
-                       f->variant == RT_VARIANT_SHDEFER;
-    if (!known || f->hot_pct < 0 || f->hot_pct > 100 || f->hot_kernel < RT_HOT_COOP4 || f->hot_kernel > RT_HOT_FAN ||
+                       f->variant == RT_VARIANT_COOP4 || f->variant == RT_VARIANT_HYBRID ||
+                       f->variant == RT_VARIANT_SHPOOL || f->variant == RT_VARIANT_SHDEFER;
+    if (!known || f->hot_pct < 0 || f->hot_pct > 100 || f->hot_kernel < RT_HOT_COOP4 || f->hot_kernel > RT_HOT_COOP2 ||
         f->tune < 0 || f->tune > 1 ||
         f->waves_cap < 0 || f->waves_cap > 8 || f->dealing < RT_DEAL_DEFAULT || f->dealing > RT_DEAL_ROW_MAJOR ||
         f->regroup < 0 || f->regroup > 64)
@@ -1328,19 +1314,14 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     //   SHPOOL              k_persist at 4 waves with each level's shadow rays walked as a per-wave pool;
     //   COOP2/4             k_coop (rt_coop.hpp): G lanes per ray, 64/G-pixel tiles — shorter chains per tile,
     //                       which is what a frame split over many GPUs (few tiles per wave) is bound by;
-    //   FAN                 k_fan (rt_fan.hpp): 1 + lights lanes per pixel;
     //   HYBRID              single frames: the costliest tiles through k_coop on a second stream (§3e).
     const bool wide_ok = kernel == RT_KERNEL_FAST && ctx->wide_n > 0;
-    const bool fan_ok = wide_ok && ctx->n_lights >= 1 && ctx->n_lights <= 7;
-    const int fan_r = ctx->n_lights <= 1 ? 2 : ctx->n_lights <= 3 ? 4 : 8;  // lanes per pixel: 1 + lights
     // the shadow pool: 1..32 lights (a 32-bit visibility word per pixel) and the LDS path buffer at 4 workgroups per CU
-    const bool shp_ok = wide_ok && ctx->n_lights >= 1 && ctx->n_lights <= 32 &&
-                        std::max(ctx->wide_n, std::max(ctx->unit_n, ctx->prim_n)) <= rtd::WIDE_MAX_NODES &&  // (packed stack)
+    const bool shp_ok = wide_ok && ctx->n_lights >= 1 && ctx->n_lights <= 32 && ctx->pk_ok && ctx->tq_ok &&
                         (f->bounces <= 4 ? pbl_fits<4>(A, ctx->device, 1) : pbl_fits<8>(A, ctx->device, 1));
     const bool shd_ok = shp_ok && ctx->n_lights <= 8 && (f->bounces <= 4 ? pbl_fits<4>(A, ctx->device, 2) : pbl_fits<8>(A, ctx->device, 2));
     auto usable = [&](int v) {
         if (A.tile_trace) return v == RT_VARIANT_PERSIST;  // (diagnostics: the 3-wave kernel's tile trace)
-        if (v == RT_VARIANT_FAN) return fan_ok;
         if (v == RT_VARIANT_COOP2 || v == RT_VARIANT_COOP4) return wide_ok;
         if (v == RT_VARIANT_SHPOOL) return shp_ok;
         if (v == RT_VARIANT_SHDEFER) return shd_ok;
@@ -1365,97 +1346,15 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     if (!usable(mode)) mode = RT_VARIANT_PERSIST;  // (no wide view, or a diagnostics trace)
     // the whole-frame kernel of a single frame while the hybrid launch measures or tries its candidates
     const int single_rule = pool_rule ? pool_v : RT_VARIANT_PERSIST;
-    int cap = f->waves_cap;
-    const bool tunable = kernel == RT_KERNEL_FAST && f->tune == 1 && f->variant == RT_VARIANT_DEFAULT && !A.tile_trace;
-    rt_ctx::Tune* Tp = nullptr;
-    auto same_shape = [&](const rt_ctx::Tune& t) {
-        return t.scene == ctx->scene_gen && t.W == f->width && t.rows == f->n_rows && t.bounces == f->bounces &&
-               t.spp == f->spp && t.frames == n_frames && t.off == f->row_offset && t.stride == f->row_stride &&
-               t.block == rb && t.shift == fs && t.dealing == f->dealing && t.cap_req == f->waves_cap;
-    };
-    for (auto& t : ctx->tunes)
-        if (same_shape(t)) Tp = &t;
-    if (!Tp && tunable) {
-        if (ctx->tunes.size() >= 16) {  // bounded: drop the oldest decision (its events with it)
-            for (int i = 0; i < rt_ctx::TUNE_MAX * rt_ctx::TUNE_REPS; i++) {
-                if (ctx->tunes.front().e0[i]) HIPC(hipEventDestroy(ctx->tunes.front().e0[i]));
-                if (ctx->tunes.front().e1[i]) HIPC(hipEventDestroy(ctx->tunes.front().e1[i]));
-            }
-            ctx->tunes.erase(ctx->tunes.begin());
-        }
-        ctx->tunes.emplace_back();
-        Tp = &ctx->tunes.back();
-        rt_ctx::Tune& T = *Tp;
-        T.scene = ctx->scene_gen;
-        T.W = f->width;
-        T.rows = f->n_rows;
-        T.bounces = f->bounces;
-        T.spp = f->spp;
-        T.frames = n_frames;
-        T.off = f->row_offset;
-        T.stride = f->row_stride;
-        T.block = rb;
-        T.shift = fs;
-        T.dealing = f->dealing;
-        T.cap_req = f->waves_cap;
-        const int md[7] = {RT_VARIANT_PERSIST, RT_VARIANT_PERSIST4, RT_VARIANT_PERSIST, pool_v,
-                           RT_VARIANT_COOP4,   RT_VARIANT_COOP2,    RT_VARIANT_FAN};
-        const int cp[7] = {0, 0, 2, 0, 0, 0, 0};
-        for (int i = 0; i < 7 && T.n < rt_ctx::TUNE_MAX; i++)
-            if (usable(md[i])) {
-                T.mode[T.n] = md[i];
-                T.cap[T.n] = f->waves_cap > 0 ? f->waves_cap : cp[i];
-                T.n++;
-            }
-    }
-    bool trial = false;
-    if (tunable) {
-        rt_ctx::Tune& T = *Tp;
-        if (T.pending) {  // the trials' timings: read once, without waiting while they run
-            const hipError_t q = hipEventQuery(T.e1[T.n * rt_ctx::TUNE_REPS - 1]);
-            if (q == hipSuccess) {
-                int best = 0;
-                for (int c = 0; c < T.n; c++) {
-                    float m = 1e30f;
-                    for (int r = 0; r < rt_ctx::TUNE_REPS; r++) {
-                        float ms = 0.0f;
-                        HIPC(hipEventElapsedTime(&ms, T.e0[r * T.n + c], T.e1[r * T.n + c]));
-                        m = std::min(m, ms);
-                    }
-                    T.ms[c] = m;
-                    if (m < T.ms[best]) best = c;
-                }
-                T.choice = best;
-                T.pending = false;
-                if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1) {
-                    std::fprintf(stderr, "[prt tune] %dx%d b%d spp%d f%d:", T.W, T.rows, T.bounces, T.spp, T.frames);
-                    for (int c = 0; c < T.n; c++)
-                        std::fprintf(stderr, " %s/%d %.3f ms", variant_name(T.mode[c]), T.cap[c], T.ms[c]);
-                    std::fprintf(stderr, " -> %d\n", best);
-                }
-            } else if (q != hipErrorNotReady) {
-                return fail(ctx, q, "rt_render: tuning trials");
-            } else {
-                (void)hipGetLastError();  // not an error: the trials are still running
-            }
-        } else if (T.choice < 0) {
-            trial = !count;  // counters would add up over the trial launches: such a frame keeps the default
-        }
-        if (T.choice >= 0) {
-            mode = T.mode[T.choice];
-            cap = T.cap[T.choice];
-        }
-    }
+    const int cap = f->waves_cap;
     rt_launch_info li{};  // what this render runs (rt_get_launch_info)
     li.settled = 1;
-    li.trial = trial || (Tp && tunable && Tp->choice < 0) ? 1 : 0;
-    if (li.trial) li.settled = 0;
     // The default rule for frame batches and spp > 1 where the shadow pool can run: measured, not guessed. Whether the
     // pool pays depends on the scene (dragon 20-frame batches 0.708 -> 0.666 ms per frame; two_cars 4K 1.881 vs 1.917,
     // car_boxed 0.868 vs 0.902), so the first launches of a shape try PERSIST4 and SHPOOL ROUNDS times each (their own
     // HIP events, read by a query once the last has run) and the faster per frame renders from then on. A context with
     // traversal counters never tries (the counters of a trial would be another kernel's): it keeps the static rule.
-    if (f->variant == RT_VARIANT_DEFAULT && !tunable && kernel == RT_KERNEL_FAST && !A.tile_trace && !count &&
+    if (f->variant == RT_VARIANT_DEFAULT && kernel == RT_KERNEL_FAST && !A.tile_trace && !count &&
         (n_frames > 1 || f->spp > 1) && shp_ok) {
         rt_ctx::BatchRule* br = nullptr;
         for (auto& b : ctx->brules)
@@ -1488,13 +1387,16 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 const hipError_t q = hipEventQuery(ctx->ev1s[last % rt_ctx::NEV]);
                 if (q == hipSuccess) {
                     float ms[2] = {1e30f, 1e30f};
-                    for (int c = 0; c < nc; c++)
-                        for (int r = 0; r < rt_ctx::BatchRule::ROUNDS; r++) {
+                    constexpr int R = rt_ctx::BatchRule::ROUNDS;
+                    for (int c = 0; c < nc; c++) {
+                        float t[R];
+                        for (int r = 0; r < R; r++) {
                             const int sl = (int)(b.launch[c][r] % rt_ctx::NEV);
-                            float t = 0.0f;
-                            HIPC(hipEventElapsedTime(&t, ctx->ev0s[sl], ctx->ev1s[sl]));
-                            ms[c] = std::min(ms[c], t);
+                            HIPC(hipEventElapsedTime(&t[r], ctx->ev0s[sl], ctx->ev1s[sl]));
                         }
+                        std::sort(t, t + R);
+                        ms[c] = t[R / 2] > rt_ctx::BatchRule::LONG_MS ? t[R / 2] : t[0];
+                    }
                     b.choice = 0;
                     for (int c = 1; c < nc; c++)
                         if (ms[c] < ms[b.choice]) b.choice = c;
@@ -1551,8 +1453,11 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&h.s2, hipStreamNonBlocking);
             if (e != hipSuccess) return err(e, "rt_render: hybrid events / stream");
         }
-        li.settled = 0;
-        li.trial = 1;
+        // a decided shape's frames -- its periodic refresh (a measuring frame, li.refresh) and the frames while that
+        // measurement is in flight included -- are the rule's steady state (settled); a new shape's are trials
+        const bool decided = same && h.choice >= 0;
+        li.settled = decided ? 1 : 0;
+        li.trial = decided ? 0 : 1;
         if (!same) {  // a new shape: measure it, once an earlier measurement in flight has landed in h_tr
             if (h.state == 1) {
                 bool done = false;
@@ -1605,20 +1510,18 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             const bool keep = h.choice >= 0;  // a refresh: new lists, the same candidates and choice
             if (!keep) {
                 h.nc = 0;
-                auto add = [&](int pct, int lanes, bool fan, int cold, bool lpt) {
+                auto add = [&](int pct, int lanes, int cold, bool lpt) {
                     if (cold == RT_VARIANT_SHPOOL) cold = pool_v;  // (HYBRID_CANDS: "the pool kernel")
                     if (h.nc >= rt_ctx::Hybrid::NCAND || !usable(cold)) return;
                     h.pct[h.nc] = pct;
                     h.lanes[h.nc] = lanes;
-                    h.fan[h.nc] = fan;
                     h.lpt[h.nc] = lpt;
                     h.cold[h.nc++] = cold;
                 };
                 if (f->hot_pct > 0) {
-                    const bool fan = f->hot_kernel == RT_HOT_FAN && fan_ok;
-                    add(f->hot_pct, fan ? fan_r : f->hot_kernel == RT_HOT_COOP2 ? 2 : 4, fan, RT_VARIANT_PERSIST, false);
+                    add(f->hot_pct, f->hot_kernel == RT_HOT_COOP2 ? 2 : 4, RT_VARIANT_PERSIST, false);
                 } else {
-                    for (const HotCand& hc : HYBRID_CANDS) add(hc.pct, hc.lanes, false, hc.cold, hc.lpt);
+                    for (const HotCand& hc : HYBRID_CANDS) add(hc.pct, hc.lanes, hc.cold, hc.lpt);
                 }
             }
             std::vector<int> lists;
@@ -1721,8 +1624,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         if (const char* l = std::getenv("PRT_TUNE_LOG"); l && std::atoi(l) == 1) {
             std::fprintf(stderr, "[prt hybrid] %dx%d b%d:", f->width, f->n_rows, f->bounces);
             for (int c = 0; c < h.nc; c++)
-                std::fprintf(stderr, " %s%d/%s%d/%s%s %.3f ms", h.pct[c] ? "hot>" : "whole", h.pct[c],
-                             h.fan[c] ? "fan" : "coop", h.lanes[c], variant_name(h.cold[c]), h.lpt[c] ? "/lpt" : "", h.ms[c]);
+                std::fprintf(stderr, " %s%d/coop%d/%s%s %.3f ms", h.pct[c] ? "hot>" : "whole", h.pct[c], h.lanes[c],
+                             variant_name(h.cold[c]), h.lpt[c] ? "/lpt" : "", h.ms[c]);
             std::fprintf(stderr, " -> %d\n", best);
         }
         li.settled = 1;
@@ -1743,17 +1646,17 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             k<<<grid, rtd::BLOCK, 0, ctx->stream>>>(A);
             return RT_OK;
         }
-        if (md == RT_VARIANT_FAN || md == RT_VARIANT_COOP2 || md == RT_VARIANT_COOP4) {
+        if (md == RT_VARIANT_COOP2 || md == RT_VARIANT_COOP4) {
             rtd::KArgs B = A;
-            const int gr = md == RT_VARIANT_FAN ? fan_r : md == RT_VARIANT_COOP2 ? 2 : 4;
+            const int gr = md == RT_VARIANT_COOP2 ? 2 : 4;
             int tw, th;
             hot_tile(gr, tw, th);  // rtd::GTile<gr>
             B.tiles_x = (f->width + tw - 1) / tw;
             const int ty = (f->n_rows + th - 1) / th;
             B.n_tiles = B.tiles_x * ty;
             if (int rc = order_for(B.tiles_x, ty, B.tile_order)) return rc;
-            return f->bounces <= 4 ? launch_group<4>(B, md == RT_VARIANT_FAN, gr, count, ctx->device, ctx->stream, cp)
-                                   : launch_group<8>(B, md == RT_VARIANT_FAN, gr, count, ctx->device, ctx->stream, cp);
+            return f->bounces <= 4 ? launch_group<4>(B, gr, count, ctx->device, ctx->stream, cp)
+                                   : launch_group<8>(B, gr, count, ctx->device, ctx->stream, cp);
         }
         rtd::KArgs P = A;
         if (region_off) {
@@ -1775,11 +1678,12 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             rt_ctx::Hybrid& h = ctx->hy;
             if (pk.kind == 0) {  // measuring frame: k_persist with per-tile times, copied to the host behind it
                 li.variant = RT_VARIANT_PERSIST;
-                li.trial = 1;
-                li.settled = 0;
+                li.refresh = h.choice >= 0 ? 1 : 0;  // a decided shape's periodic list refresh (settled)
+                li.trial = li.refresh ? 0 : 1;
+                li.settled = li.refresh;
                 P.tile_trace = h.d_tr;
-                if (f->bounces <= 4) launch_paths<4>(P, RT_VARIANT_PERSIST, count, ctx->device, ctx->stream, cp);
-                else launch_paths<8>(P, RT_VARIANT_PERSIST, count, ctx->device, ctx->stream, cp);
+                if (f->bounces <= 4) launch_paths<4>(P, RT_VARIANT_PERSIST, count, ctx->device, ctx->stream, cp, ctx->pk_ok, ctx->tq_ok);
+                else launch_paths<8>(P, RT_VARIANT_PERSIST, count, ctx->device, ctx->stream, cp, ctx->pk_ok, ctx->tq_ok);
                 HIPC(hipGetLastError());
                 HIPC(hipMemcpyAsync(h.h_tr, h.d_tr, sizeof(unsigned long long) * 4 * h.n_tiles, hipMemcpyDeviceToHost,
                                     ctx->stream));
@@ -1790,28 +1694,11 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             md = pk.c;  // a whole-frame kernel: chosen, tried, or while the measurement / trials are on their way
             li.variant = md;
         }
-        if (f->bounces <= 4) launch_paths<4>(P, md, count, ctx->device, ctx->stream, cp);
-        else launch_paths<8>(P, md, count, ctx->device, ctx->stream, cp);
+        if (f->bounces <= 4) launch_paths<4>(P, md, count, ctx->device, ctx->stream, cp, ctx->pk_ok, ctx->tq_ok);
+        else launch_paths<8>(P, md, count, ctx->device, ctx->stream, cp, ctx->pk_ok, ctx->tq_ok);
         return RT_OK;
     };
-    if (trial) {
-        rt_ctx::Tune& T = *Tp;
-        const int nt = T.n * rt_ctx::TUNE_REPS;
-        for (int i = 0; i < nt; i++) {
-            if (!T.e0[i]) HIPC(hipEventCreate(&T.e0[i]));
-            if (!T.e1[i]) HIPC(hipEventCreate(&T.e1[i]));
-        }
-        for (int i = 0; i < nt; i++) {
-            const int c = i % T.n;
-            if (i == nt - 1) HIPC(hipEventRecord(ctx->ev0, ctx->stream));
-            HIPC(hipEventRecord(T.e0[i], ctx->stream));
-            const int rc = dispatch(T.mode[c], T.cap[c]);
-            if (rc) return rc;
-            HIPC(hipGetLastError());
-            HIPC(hipEventRecord(T.e1[i], ctx->stream));
-        }
-        T.pending = true;
-    } else {
+    {
         HIPC(hipEventRecord(ctx->ev0, ctx->stream));
         const int rc = dispatch(mode, cap);
         if (rc) return rc;
@@ -1866,10 +1753,28 @@ extern "C" int rt_get_launch_info(rt_ctx* ctx, rt_launch_info* info) {
     return RT_OK;
 }
 
+namespace {
+// Waits for the context stream; with a render behind it, reads that render's error counter (rtd::C_ERR: a traversal
+// stack overflowed, rt_kernels.hpp) in the same wait, so that a frame computed with a truncated walk never passes as
+// good: RT_E_KERNEL.
+int sync_checked(rt_ctx* ctx, const char* who) {
+    if (ctx->rendered)
+        HIPC(hipMemcpyAsync(ctx->h_err, ctx->d_counters + rtd::C_ERR, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                            ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    if (ctx->rendered && *ctx->h_err) {
+        ctx->err = std::string(who) + ": the render's traversal stack overflowed " + std::to_string(*ctx->h_err) +
+                   " times (BVH deeper than the walks' stacks): the frame is not valid";
+        return RT_E_KERNEL;
+    }
+    return RT_OK;
+}
+}  // namespace
+
 extern "C" int rt_sync(rt_ctx* ctx, float* kernel_ms) {
     if (!ctx) return RT_E_ARG;
     HIPC(hipSetDevice(ctx->device));
-    HIPC(hipStreamSynchronize(ctx->stream));
+    if (int rc = sync_checked(ctx, "rt_sync")) return rc;
     if (kernel_ms) {
         *kernel_ms = 0.0f;
         if (ctx->rendered) HIPC(hipEventElapsedTime(kernel_ms, ctx->ev0, ctx->ev1));
@@ -1897,7 +1802,7 @@ extern "C" int rt_download(rt_ctx* ctx, float* h_rgb, int* h_hit) {
         return RT_E_STATE;
     }
     HIPC(hipSetDevice(ctx->device));
-    HIPC(hipStreamSynchronize(ctx->stream));
+    if (int rc = sync_checked(ctx, "rt_download")) return rc;
     if (h_rgb && !ctx->last_rgb) {
         ctx->err = "rt_download: last frame was rendered to a bgra output only";
         return RT_E_STATE;
@@ -1928,7 +1833,7 @@ int grow(rt_ctx* ctx, T** p, size_t& cap, size_t n) {
 }  // namespace
 
 namespace {
-// RT_VARIANT_HYBRID, one frame: the hot tiles (ctx->hy lists) through k_coop / k_fan on the context's second stream
+// RT_VARIANT_HYBRID, one frame: the hot tiles (ctx->hy lists) through k_coop on the context's second stream
 // while the cold kernel (k_persist, or the shadow pool) renders the cold 8x8 tiles on the context stream; both
 // persistent grids together fill the chip (the hot grid is sized to start every hot tile at once, at most half the
 // chip), and the context stream waits for both.
@@ -1938,7 +1843,7 @@ int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c) {
     const int n_hot = h.n_hot[c], n_cold = h.n_cold[c];
     int* lists = h.d_lists + h.at[c];
     const int g = h.lanes[c];
-    const KFn kc = h.fan[c] ? fan_kernel<MAXB>(g, count) : coop_kernel<MAXB>(g, count);
+    const KFn kc = coop_kernel<MAXB>(g, count);
     int tw, th;
     hot_tile(g, tw, th);
     rtd::KArgs B = A;  // the hot kernel's tiles, dealt hottest first from their own work counter
@@ -1952,7 +1857,7 @@ int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c) {
     P.region_off = h.cold_regions ? lists + n_hot : nullptr;
     P.tile_order = lists + n_hot + (h.cold_regions ? 9 : 0);
     size_t dyn = 0;
-    const KFn kp = persist_kernel<MAXB>(P, h.cold[c], count, ctx->device, dyn);
+    const KFn kp = persist_kernel<MAXB>(P, h.cold[c], count, ctx->device, dyn, ctx->pk_ok, ctx->tq_ok);
     const int rp = resident(kp, ctx->device, 8, dyn);
     const int rcp = resident(kc, ctx->device);
     const int nc = n_hot > 0 ? std::max(1, std::min((n_hot + 3) / 4, rcp / 2)) : 0;
@@ -1975,15 +1880,10 @@ int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c) {
 }  // namespace
 
 namespace {
-// One rank's part of a gathered frame batch: its last render's compact rows (rt_frame) and payload. 16 ints:
-// the descriptor the RCCL ranks of different processes exchange (rt_comm_gather).
-struct Part {
-    int W, H, frames, rows, off, stride, block, shift;
-    int words;  // 32-bit words per pixel: 1 = BGRA8 (rt_outputs.bgra), 3 = f32 rgb
-    int hit;    // 1: the render wrote hit indices too
-    int pad[6];
-};
-static_assert(sizeof(Part) == 64, "descriptor size");
+// a rank's part of a gathered frame batch, the layout checks (rt_comm_logic.hpp: host-only, unit-tested with g++)
+using rtc::check_parts;
+using rtc::Part;
+using rtc::part_px;
 
 Part part_of(const rt_ctx* c) {
     Part p{};
@@ -2000,37 +1900,6 @@ Part part_of(const rt_ctx* c) {
     return p;
 }
 const void* payload_of(const rt_ctx* c) { return c->last_bgra ? (const void*)c->last_bgra : (const void*)c->last_rgb; }
-size_t part_px(const Part& p) { return (size_t)p.frames * p.rows * p.W; }
-
-// "" when the parts' rows partition every frame of the batch (rows a rotated rank renders past the image are
-// skipped), else what is wrong
-std::string check_parts(const std::vector<Part>& ps) {
-    for (const Part& p : ps)
-        if (p.W <= 0 || p.H <= 0) return "a rank has not rendered";
-    const Part& a = ps[0];
-    std::vector<char> cover((size_t)a.H);
-    for (const Part& p : ps) {
-        if (p.W != a.W || p.H != a.H) return "frame sizes differ";
-        if (p.frames != a.frames) return "frame counts differ";
-        if (p.words != a.words) return "outputs differ (bgra vs rgb)";
-        if (p.rows < 0 || p.stride < 1 || p.block < 1) return "bad row set";
-    }
-    for (int f = 0; f < a.frames; f++) {
-        std::fill(cover.begin(), cover.end(), 0);
-        for (const Part& p : ps) {
-            const long long start = p.shift ? (p.off + (long long)f * p.shift) % p.stride : p.off;
-            for (int k = 0; k < p.rows; k++) {
-                const long long y = start + (long long)(k / p.block) * p.stride + k % p.block;
-                if (y >= a.H && p.shift) continue;
-                if (y < 0 || y >= a.H || cover[y]) return "row sets do not partition the frame";
-                cover[y] = 1;
-            }
-        }
-        for (char v : cover)
-            if (!v) return "row sets do not cover the frame";
-    }
-    return "";
-}
 
 // compact part -> full frames on stream s (root's device)
 int unshuffle(rt_ctx* ctx, const void* src, void* dst, const Part& p, int words, hipStream_t s) {
@@ -2158,8 +2027,8 @@ struct rt_comm {
     int nranks = 0, rank0 = 0;
     bool multi = false;  // rt_comm_init_rank: one rank of a multi-process job (row sets exchanged over RCCL)
     // multi-process: the layout -- every rank's descriptor as last exchanged (ncclAllGather), and this rank's part
-    // at that exchange. A gather exchanges again only when this rank's part differs from it (a new frame shape or row
-    // set; every rank's part changes with a layout, so the ranks exchange together).
+    // at that exchange. A gather exchanges again only on what every rank sees the same way (rtc::layout_step: the
+    // first gather, a new frame size / count / pixel kind, or rt_comm_relayout on every rank).
     std::vector<Part> layout;
     Part mine{};
     bool have_layout = false;
@@ -2169,6 +2038,8 @@ struct rt_comm {
     hipStream_t side = nullptr;  // the exchange's stream: the host waits for the exchange only, not for renders
     hipEvent_t done = nullptr;   // after the last send / recv group: the next operation on the communicator waits
     bool issued = false;
+    bool aborted = false;     // a collective missed its deadline: the communicator was aborted (ncclCommAbort)
+    double timeout_s = 120.0;  // host waits on a collective (rt_comm_set_timeout)
     rt_comm_info info{};
     std::string err;
 };
@@ -2184,6 +2055,7 @@ struct Rccl {
     ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
     ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
     ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
@@ -2210,6 +2082,7 @@ Rccl& rccl() {
     sym(R.CommInitAll, "ncclCommInitAll");
     sym(R.CommInitRank, "ncclCommInitRank");
     sym(R.CommDestroy, "ncclCommDestroy");
+    sym(R.CommAbort, "ncclCommAbort");
     sym(R.AllGather, "ncclAllGather");
     sym(R.Send, "ncclSend");
     sym(R.Recv, "ncclRecv");
@@ -2236,6 +2109,46 @@ int comm_arg(rt_comm* cm, const std::string& what) {
         ncclResult_t r_ = (call);                         \
         if (r_ != ncclSuccess) return comm_fail(cm, r_, #call); \
     } while (0)
+
+// A collective that misses its deadline: every RCCL communicator of `cm` is aborted (its kernels stop waiting for
+// the missing peer, so the streams drain), and the communicator refuses further gathers.
+int comm_abort(rt_comm* cm, const std::string& what) {
+    for (size_t l = 0; l < cm->comms.size(); l++)
+        if (cm->comms[l]) {
+            (void)hipSetDevice(cm->devices[l]);
+            (void)rccl().CommAbort(cm->comms[l]);
+            cm->comms[l] = nullptr;
+        }
+    cm->aborted = true;
+    cm->err = what;
+    for (rt_ctx* c : cm->ctxs) c->err = what;
+    return RT_E_TIMEOUT;
+}
+// A host wait on work behind a collective (a stream or an event), bounded by the communicator's timeout
+// (rtc::bounded_wait): RT_E_TIMEOUT and an aborted communicator instead of a hang when a peer never arrives.
+template <class Q>
+int comm_wait(rt_comm* cm, Q query_hip, const char* what) {
+    int err = 0;
+    const rtc::Wait w = rtc::bounded_wait(
+        [&]() -> int {
+            const hipError_t e = query_hip();
+            if (e == hipSuccess) return 0;
+            if (e == hipErrorNotReady) {
+                (void)hipGetLastError();  // not an error: still running
+                return 1;
+            }
+            return -(int)e;
+        },
+        cm->timeout_s, err);
+    if (w == rtc::Wait::Done) return RT_OK;
+    if (w == rtc::Wait::Error) {
+        cm->err = std::string(what) + ": " + hipGetErrorString((hipError_t)(-err));
+        for (rt_ctx* c : cm->ctxs) c->err = cm->err;
+        return RT_E_HIP;
+    }
+    return comm_abort(cm, std::string(what) + ": no completion within " + std::to_string(cm->timeout_s) +
+                              " s (a peer rank never joined the collective); the communicator is aborted");
+}
 }  // namespace
 
 extern "C" int rt_comm_get_id(unsigned char* id) {
@@ -2328,17 +2241,23 @@ namespace {
 int comm_gather_multi(rt_comm* cm, rt_ctx* src, int root, void* d_dst) {
     rt_ctx* ctx = src;
     HIPC(hipSetDevice(ctx->device));
+    if (cm->aborted) return comm_arg(cm, "rt_comm_gather: the communicator was aborted (" + cm->err + ")");
     // this rank's part; a rank whose context has not rendered still takes part (W = 0), so that every rank fails
     // together in check_parts instead of the others waiting in the collective for it
     const Part mine = ctx->rendered ? part_of(ctx) : Part{};
-    const bool fresh = !cm->have_layout || std::memcmp(&mine, &cm->mine, sizeof mine) != 0;
+    const rtc::Step step = rtc::layout_step(mine, cm->mine, cm->have_layout);
+    if (step == rtc::Step::RowsChanged)  // (refused before any collective call: the peers' next wait times out)
+        return comm_arg(cm, "rt_comm_gather: this rank's rows changed without a layout change every rank sees "
+                            "(frame size, frame count, pixel kind): call rt_comm_relayout on every rank first");
+    const bool fresh = step == rtc::Step::Exchange;
     if (fresh) {  // a new layout: exchange the 64-B descriptors (ncclAllGather) and check that they partition the frames
         cm->h_desc[cm->nranks] = mine;
         if (cm->issued) HIPC(hipStreamWaitEvent(cm->side, cm->done, 0));
         HIPC(hipMemcpyAsync(cm->d_desc + cm->nranks, cm->h_desc + cm->nranks, sizeof(Part), hipMemcpyHostToDevice, cm->side));
         NCCLC(rccl().AllGather(cm->d_desc + cm->nranks, cm->d_desc, sizeof(Part) / 4, ncclInt32, cm->comms[0], cm->side));
         HIPC(hipMemcpyAsync(cm->h_desc, cm->d_desc, sizeof(Part) * cm->nranks, hipMemcpyDeviceToHost, cm->side));
-        HIPC(hipStreamSynchronize(cm->side));
+        if (int rc = comm_wait(cm, [&] { return hipStreamQuery(cm->side); }, "rt_comm_gather: row-set exchange"))
+            return rc;
         cm->info.exchanges++;
         cm->layout.assign(cm->h_desc, cm->h_desc + cm->nranks);
         cm->have_layout = false;
@@ -2394,7 +2313,8 @@ int comm_gather_multi(rt_comm* cm, rt_ctx* src, int root, void* d_dst) {
         rtd::k_count_unwritten<<<grid, 256, 0, ctx->stream>>>((const unsigned*)dst, full_px, words, cm->d_count);
         HIPC(hipGetLastError());
         HIPC(hipMemcpyAsync(&left, cm->d_count, sizeof left, hipMemcpyDeviceToHost, ctx->stream));
-        HIPC(hipStreamSynchronize(ctx->stream));
+        if (int rc2 = comm_wait(cm, [&] { return hipStreamQuery(ctx->stream); }, "rt_comm_gather: coverage check"))
+            return rc2;
         cm->info.checked++;
         if (left)  // (the layout stays: every rank keeps the same view of it, so the next gathers stay matched)
             return comm_arg(cm, "rt_comm_gather: the gathered frames miss " + std::to_string(left) + " pixels");
@@ -2465,6 +2385,26 @@ extern "C" int rt_comm_gather_from(rt_comm* cm, rt_ctx* src, int root, void* d_d
 
 extern "C" int rt_comm_gather(rt_comm* cm, int root, void* d_dst) { return rt_comm_gather_from(cm, nullptr, root, d_dst); }
 
+extern "C" int rt_comm_relayout(rt_comm* cm) {
+    if (!cm) return RT_E_ARG;
+    cm->have_layout = false;  // the next gather exchanges (every rank calls this before the same gather)
+    return RT_OK;
+}
+
+extern "C" int rt_comm_set_timeout(rt_comm* cm, double seconds) {
+    if (!cm || !(seconds > 0.0)) return RT_E_ARG;
+    cm->timeout_s = seconds;
+    return RT_OK;
+}
+
+extern "C" int rt_comm_wait(rt_comm* cm) {
+    if (!cm) return RT_E_ARG;
+    if (cm->aborted) return RT_E_TIMEOUT;
+    if (!cm->issued || !cm->done) return RT_OK;
+    (void)hipSetDevice(cm->devices[0]);
+    return comm_wait(cm, [&] { return hipEventQuery(cm->done); }, "rt_comm_wait: the last gather");
+}
+
 extern "C" int rt_comm_get_info(rt_comm* cm, rt_comm_info* info) {
     if (!cm || !info) return RT_E_ARG;
     *info = cm->info;
@@ -2476,16 +2416,15 @@ extern "C" const char* rt_comm_last_error(rt_comm* cm) { return cm ? cm->err.c_s
 extern "C" void rt_comm_destroy(rt_comm* cm) {
     if (!cm) return;
     // (the contexts may be gone already: only the communicator's own devices, events and streams are touched)
-    if (cm->issued && cm->done) {  // the last send / recv group (any context's stream) has run
-        (void)hipSetDevice(cm->devices[0]);
-        (void)hipEventSynchronize(cm->done);
-    }
+    // the last send / recv group (any context's stream) has run -- or its peers never came and the bounded wait
+    // aborted the communicator (comm_abort): nothing left to wait for
+    if (cm->issued && cm->done && !cm->aborted) (void)rt_comm_wait(cm);
     for (size_t l = 0; l < cm->comms.size(); l++) {
         (void)hipSetDevice(cm->devices[l]);
-        if (!cm->multi) (void)hipDeviceSynchronize();  // (one process: the groups ran on the contexts' streams)
+        if (!cm->multi && !cm->aborted) (void)hipDeviceSynchronize();  // (one process: the groups ran on the contexts' streams)
         if (cm->comms[l]) (void)rccl().CommDestroy(cm->comms[l]);
     }
-    if (cm->side) (void)hipStreamSynchronize(cm->side);
+    if (cm->side && !cm->aborted) (void)hipStreamSynchronize(cm->side);
     if (cm->d_desc) (void)hipFree(cm->d_desc);
     if (cm->d_count) (void)hipFree(cm->d_count);
     if (cm->h_desc) (void)hipHostFree(cm->h_desc);
@@ -2518,8 +2457,7 @@ extern "C" int rt_download_bmp(rt_ctx* ctx, unsigned char* h_bmp, size_t cap) {
     HIPC(hipGetLastError());
     if (rth_bmp_header(W, H, h_bmp) != RT_OK) return arg_err(ctx, "rt_download_bmp: bad frame size");
     HIPC(hipMemcpyAsync(h_bmp + 54, ctx->d_bmp, 4 * px, hipMemcpyDeviceToHost, ctx->stream));
-    HIPC(hipStreamSynchronize(ctx->stream));
-    return RT_OK;
+    return sync_checked(ctx, "rt_download_bmp");
 }
 
 extern "C" int rt_get_stats(rt_ctx* ctx, rt_stats* st) {
@@ -2553,8 +2491,8 @@ extern "C" int rt_get_stats(rt_ctx* ctx, rt_stats* st) {
     std::memcpy(st->steps_hist, c + rtd::C_HIST, sizeof st->steps_hist);
     static_assert(sizeof st->steps_hist == 32 * sizeof(unsigned long long), "histogram slots");
     if (c[rtd::C_ERR]) {
-        ctx->err = "traversal stack overflow: BVH deeper than 32 levels";
-        return RT_E_STATE;
+        ctx->err = "rt_get_stats: the render's traversal stack overflowed (BVH deeper than the walks' stacks)";
+        return RT_E_KERNEL;
     }
     return RT_OK;
 }
@@ -2574,6 +2512,7 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     if (ctx->d_gstack) (void)hipFree(ctx->d_gstack);
     if (ctx->h_cams) (void)hipHostFree(ctx->h_cams);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->h_err) (void)hipHostFree(ctx->h_err);
     for (auto& o : ctx->orders) (void)hipFree(o.second);
     for (void* p : {(void*)ctx->d_full, (void*)ctx->d_full_hit, (void*)ctx->d_stage, (void*)ctx->d_bmp,
                     (void*)ctx->d_full_bgra})
@@ -2583,11 +2522,6 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
         if (ctx->ev0s[i]) (void)hipEventDestroy(ctx->ev0s[i]);
         if (ctx->ev1s[i]) (void)hipEventDestroy(ctx->ev1s[i]);
     }
-    for (auto& t : ctx->tunes)
-        for (int i = 0; i < rt_ctx::TUNE_MAX * rt_ctx::TUNE_REPS; i++) {
-            if (t.e0[i]) (void)hipEventDestroy(t.e0[i]);
-            if (t.e1[i]) (void)hipEventDestroy(t.e1[i]);
-        }
     if (ctx->hy.s2) (void)hipStreamSynchronize(ctx->hy.s2);
     if (ctx->hy.d_tr) (void)hipFree(ctx->hy.d_tr);
     if (ctx->hy.h_tr) (void)hipHostFree(ctx->hy.h_tr);

@@ -289,8 +289,10 @@ constexpr int WSTACK = 16;  // node-group entries in the STACK-int LDS column; b
 // A stack entry is two words (child base; interior mask << 8 | hit bits). PK (the shadow-pool kernels): one word
 // (child base << 8 | hit bits) plus the interior mask as one byte, four entries' bytes to a word after the wcap entry
 // words -- 5 bytes per entry, so that the all-levels pool's path buffer fits 4 workgroups per CU beside the stack of
-// deeper trees (sportscar depth 14, two_cars 12) -- at 4 more VALU per push / pop (PERSIST4 with it: 1.1-1.5 % slower,
-// so only the pool kernels pack). The packed child base has 24 bits: wide trees of at most WIDE_MAX_NODES nodes.
+// deeper trees (sportscar depth 14, two_cars 12) -- at 4 more VALU per push / pop. The pool kernels pack, and so does
+// PERSIST4's SHP = 3 build (packed stack entries plus packed triangle tests, which together win). The packed child
+// base has 24 bits: wide trees of at most WIDE_MAX_NODES nodes; the host (rt_hip.hip persist_kernel, shp_ok) runs the
+// unpacked builds for larger trees.
 constexpr int WIDE_MAX_NODES = 1 << 24;
 __host__ __device__ constexpr int wstack_words(int wcap, bool pk) { return pk ? wcap + (wcap + 3) / 4 : 2 * wcap; }
 // A child box left before t = EPS holds no hit: hit_triangle accepts t > EPS only (raytracer.c:56), and the
@@ -458,7 +460,11 @@ __device__ __forceinline__ int wide_next(unsigned nh, int cb, unsigned imask, un
 // A wave's LDS queue of packed triangle tests (TQ): TQ_CAP jobs (owner lane << 26 | triangle), then 128 words of
 // per-owner results, then the queue's counter. Between packed steps the result words, the job words 64..127 (the
 // closest walk's flags) and the counter are 0 (tq_clear): minima are kept complemented, by atomic max.
+// A job's triangle (a position in the view's leaf-ordered triangles) has 26 bits: the TQ builds serve scenes of fewer
+// than TQ_MAX_TRIS triangles; the host (rt_hip.hip persist_kernel, shp_ok) runs the builds without TQ for larger ones.
 constexpr int TQ_CAP = 128;
+constexpr int TQ_MAX_TRIS = 1 << 26;
+static_assert(TQ_MAX_TRIS == 0x3FFFFFF + 1 && 63u << 26 >> 26 == 63u, "job = owner lane (6 bits) << 26 | triangle");
 constexpr int TQ_OCC = TQ_CAP, TQ_T = TQ_CAP + 64, TQ_CNT = TQ_CAP + 128, TQ_WORDS = TQ_CAP + 132;
 // the waves' queues of a kernel without dynamic LDS (the 3-wave k_persist): a static array
 __device__ __forceinline__ int* tq_static() {

@@ -86,7 +86,8 @@ class SceneInfo(ctypes.Structure):  # rt_scene_info
 
 class LaunchInfo(ctypes.Structure):  # rt_launch_info
     _fields_ = [("variant", ctypes.c_int), ("hot_pct", ctypes.c_int), ("hot_lanes", ctypes.c_int),
-                ("cold_variant", ctypes.c_int), ("trial", ctypes.c_int), ("settled", ctypes.c_int)]
+                ("cold_variant", ctypes.c_int), ("trial", ctypes.c_int), ("settled", ctypes.c_int),
+                ("refresh", ctypes.c_int)]
 
 
 class CommInfo(ctypes.Structure):  # rt_comm_info
@@ -169,6 +170,9 @@ def hip():
         L.rt_comm_gather.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         L.rt_comm_gather_from.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         L.rt_comm_get_info.argtypes = [ctypes.c_void_p, P(CommInfo)]
+        L.rt_comm_relayout.argtypes = [ctypes.c_void_p]
+        L.rt_comm_set_timeout.argtypes = [ctypes.c_void_p, ctypes.c_double]
+        L.rt_comm_wait.argtypes = [ctypes.c_void_p]
         L.rt_comm_last_error.argtypes = [ctypes.c_void_p]
         L.rt_comm_last_error.restype = ctypes.c_char_p
         L.rt_comm_destroy.argtypes = [ctypes.c_void_p]

@@ -15,9 +15,9 @@ P = ctypes.POINTER
 KERNELS = {"auto": 0, "strict": 1, "fast": 2}
 # rt_frame.variant (launch configurations of the fast kernel, include/rt_hip.h); a variant name is also
 # accepted as `kernel` (kernel="coop4" == kernel="fast", variant="coop4")
-VARIANTS = {"default": 0, "persist": 1, "persist4": 2, "coop2": 4, "coop4": 5, "fan": 7, "hybrid": 11, "shpool": 13, "shdefer": 15}
+VARIANTS = {"default": 0, "persist": 1, "persist4": 2, "coop2": 4, "coop4": 5, "hybrid": 11, "shpool": 13, "shdefer": 15}
 VARIANT_NAMES = {v: k for k, v in VARIANTS.items()}
-HOT_KERNELS = {"coop4": 0, "coop2": 1, "fan": 2}  # rt_frame.hot_kernel (RT_HOT_*)
+HOT_KERNELS = {"coop4": 0, "coop2": 1}  # rt_frame.hot_kernel (RT_HOT_*)
 DEALING = {"default": 0, "global": 1, "rows": 2, "columns": 3, "blocks": 4, "row_major": 5}
 ACCEL = {"auto": 0, "reference": 1, "gpu": 2, "host": 3}
 ACCEL_NAMES = {v: k for k, v in ACCEL.items()}
@@ -131,6 +131,23 @@ class Comm:
         if 0 <= lr < len(here):
             r = here[lr]
             r._last = r._size
+
+    def set_timeout(self, seconds):
+        """rt_comm_set_timeout: the deadline of every host wait on a collective (a peer that never joins turns into
+        RT_E_TIMEOUT and an aborted communicator instead of a hang)"""
+        if _L.rt_comm_set_timeout(self._c, float(seconds)) != 0:
+            raise RtError("rt_comm_set_timeout failed")
+
+    def relayout(self):
+        """rt_comm_relayout (collective): the next gather exchanges the ranks' row sets again"""
+        if _L.rt_comm_relayout(self._c) != 0:
+            raise RtError("rt_comm_relayout failed")
+
+    def wait(self):
+        """rt_comm_wait: bounded wait for the last gather; raises on a timeout (the communicator is aborted)"""
+        rc = _L.rt_comm_wait(self._c)
+        if rc != 0:
+            raise RtError(f"rt_comm_wait: {rc} ({_L.rt_comm_last_error(self._c).decode()})")
 
     def info(self):
         """rt_comm_get_info: gathers, descriptor exchanges (one per layout), layouts checked pixel by pixel"""

@@ -200,7 +200,7 @@ class NativeGather:
     un-interleaving into frames(c)) on the context's stream, so the gather of one context's batch overlaps the
     next render of the other. Same row layout as FrameGather (8-row blocks, residues rotated per frame)."""
 
-    def __init__(self, renderers, H, W, C, rank, world, dist, like, frames=1, block=1, rotate=False):
+    def __init__(self, renderers, H, W, C, rank, world, dist, like, frames=1, block=1, rotate=False, timeout=120.0):
         import torch
         from . import device
         self.H, self.W, self.C, self.rank, self.world = H, W, C, rank, world
@@ -216,6 +216,7 @@ class NativeGather:
             dist.broadcast_object_list(ids, src=0)
         # one communicator for the rank, shared by its contexts (rt_comm_gather_from)
         self.comm = device.Comm([renderers[0]], world, rank, ids[0])
+        self.comm.set_timeout(timeout)  # every host wait on a collective bounded (rt_comm_set_timeout)
         self.renderers = list(renderers)
 
     def rows(self):
@@ -232,6 +233,11 @@ class NativeGather:
         """collective (every rank, after context c's render of nf frames): its frames -> rank 0's frames_of(c)"""
         out = self.full[c][:nf or self.frames] if self.rank == 0 else None
         self.comm.gather(root=0, out=out, src=self.renderers[c])
+
+    def wait(self):
+        """bounded wait for the last gather (rt_comm_wait): raises, with the communicator aborted, when a peer never
+        joined, instead of leaving the caller's device synchronisation to hang"""
+        self.comm.wait()
 
     def frames_of(self, c):
         return self.full[c] if self.rank == 0 else None

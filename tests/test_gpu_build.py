@@ -40,7 +40,7 @@ def same_bits(a, b):
     return np.array_equal(np.asarray(a, np.float32).view(np.int32), np.asarray(b, np.float32).view(np.int32))
 
 
-@pytest.mark.parametrize("kernel", ["fast", "persist4", "coop4", "fan"])
+@pytest.mark.parametrize("kernel", ["fast", "persist4", "coop4", "shdefer"])
 @pytest.mark.parametrize("name,W,H,fixture", [("car_boxed", 160, 90, "car_boxed_160x90_strict"),
                                               ("car_only", 160, 90, "car_only_160x90_strict"),
                                               ("dragon", 96, 54, "dragon_96x54_strict"),

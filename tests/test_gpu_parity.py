@@ -6,6 +6,7 @@ Bar (BASELINE.json north_star):
     the FAST kernel on the reference BVH; any BVH the product builds must stay within the stated
     per-channel tolerance RGB_TOL = 1e-5 of the reference (hits still exact).
 """
+import ctypes
 import json
 import os
 
@@ -18,10 +19,9 @@ pytestmark = pytest.mark.gpu
 RGB_TOL = 1e-5
 # every kernel and launch configuration the C-ABI exposes (rt_frame.kernel / rt_frame.variant): STRICT, FAST
 # with its default rule ("fast"), and each variant forced: k_persist at 4 waves/SIMD ("persist4"), k_coop
-# ("coopG": G lanes per ray), k_fan ("fan":
-# 1 + lights lanes per pixel). "shpool": k_persist with each level's shadow rays walked as a per-wave pool
+# ("coopG": G lanes per ray). "shpool": k_persist with each level's shadow rays walked as a per-wave pool
 # (rt_shpool.hpp); "shdefer": one pool for all levels' shadow rays.
-KERNELS = ["strict", "fast", "persist4", "coop2", "coop4", "fan", "shpool", "shdefer"]
+KERNELS = ["strict", "fast", "persist4", "coop2", "coop4", "shpool", "shdefer"]
 
 
 def select(kernel):
@@ -177,7 +177,7 @@ def test_strict_traversal_counters_match_reference_order(dev, scenes):
         assert st[k] == c[k], k
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "shpool"])
+@pytest.mark.parametrize("kernel", ["fast", "persist4", "coop4", "shpool", "shdefer"])
 @pytest.mark.parametrize("spp", [4, 16])
 def test_spp_matches_oracle(dev, scenes, spp, kernel):
     from tests.oracle_bind import OracleScene
@@ -212,7 +212,7 @@ def test_spp_of_a_two_light_scene_matches_oracle(dev, spp, kernel):
 _SPP64 = {}
 
 
-@pytest.mark.parametrize("kernel", ["fast", "persist4", "coop4", "fan", "shpool"])
+@pytest.mark.parametrize("kernel", ["fast", "persist4", "coop4", "shpool", "shdefer"])
 def test_car_boxed_64spp_matches_oracle(dev, scenes, kernel):
     """BASELINE config 5 (car_boxed 3840x2160, 64 spp, multi-bounce): the reference has one corner ray per
     pixel (cpu/src/main.c:228-239); SURVEY §8d defines spp = s x s stratified sub-pixel samples, mean of the
@@ -286,7 +286,7 @@ _ORACLE_FRAMES = {}
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan"])
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "shdefer"])
 def test_bench_config_full_frame_vs_oracle(dev, kernel):
     """the bench workload (dragon stand-in, 1920x1080, fast kernel, library SAH BVH) against the oracle
     at full size: hit indices, t and colours bit-exact"""
@@ -412,32 +412,39 @@ def test_cli_drop_in_writes_the_reference_bmp(tmp_path):
     assert len(list(cache.iterdir())) == 2
 
 
-@pytest.mark.parametrize("name,n_cand", [("sportscar", 7), ("car_boxed", 7), ("dragon", 7)])
-def test_autotuned_frames_equal_forced_configuration(dev, name, n_cand, monkeypatch, capfd):
-    """rt_render's launch autotuner (rt_frame.tune = 1, rt_hip.hip): the trial frame (every candidate, each
-    TUNE_REPS times, into the same outputs) and the frames after the decision are bit-exact to a forced
-    k_persist frame; the decision is logged once, over all candidates"""
+def test_tune_is_the_default_rule_and_removed_variants_are_refused(dev, scenes):
+    """rt_frame.tune: 1 is accepted and runs the default rule (the round-2 autotuner it selected was slower than the
+    measured rule everywhere and was removed), other values are refused; so are the removed variants (k_fan = 7, ...)
+    and hot kernels (RT_HOT_FAN = 2). A tune = 1 frame equals a tune = 0 frame bit for bit, with the same ray counts."""
     import torch
-    s = host.Scene.named(name).build_bvh(3)
     W, H = 96, 54
-    ref = render(dev, s, W, H, "persist")
-    monkeypatch.setenv("PRT_TUNE_LOG", "1")
-    r = dev.Renderer(0)
-    r.upload(s)
-    for frame in range(3):
-        hit = torch.full((H, W), -7, dtype=torch.int32, device="cuda")
-        t = torch.zeros((H, W), dtype=torch.float32, device="cuda")
-        rgb = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
-        r.render(host.camera(W, H), W, H, kernel="fast", rgb=rgb, hit=hit, t=t, tune=True)
+    outs = []
+    for tune in (0, 1):
+        r = dev.Renderer(0, counters=True)
+        r.upload(scenes["car_boxed"])
+        rgb = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        r.render(host.camera(W, H), W, H, rgb=rgb, tune=tune)
         r.sync()
-        np.testing.assert_array_equal(hit.cpu().numpy(), ref["hit"])
-        assert same_bits(t.cpu().numpy(), ref["t"]) and same_bits(rgb.cpu().numpy(), ref["rgb"]), frame
-        st = r.stats()  # one frame's rays, not the trial launches' sum
-        for k in ("rays", "primary", "shadow", "pixels"):
-            assert st[k] == ref["stats"][k], (frame, k, st[k], ref["stats"][k])
+        outs.append((rgb.cpu().numpy(), r.stats()["rays"]))
+        r.close()
+    assert same_bits(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
+    r = dev.Renderer(0)
+    r.upload(scenes["car_boxed"])
+    for kw in ({"tune": 2}, {"variant": 7}, {"variant": 3}, {"variant": 14}, {"hot_pct": 50, "hot_kernel": 2}):
+        fr = _frame_with(r, W, H, kw)
+        rc = dev._L.rt_render(r._ctx, ctypes.byref(host.camera(W, H)), ctypes.byref(fr), ctypes.byref(dev.Outputs()))
+        assert rc == -1, (kw, rc)  # RT_E_ARG
     r.close()
-    log = [l for l in capfd.readouterr().err.splitlines() if l.startswith("[prt tune]")]
-    assert len(log) == 1 and log[0].count(" ms") == n_cand, log
+
+
+def _frame_with(r, W, H, f):
+    """an rt_frame for the full W x H frame with raw launch fields (values the Python mirror would not produce)"""
+    fr, _ = r._frame(W, H, None, 4, 1, "fast", 0, False, 0, "default", 0)
+    fr.tune = f.get("tune", 0)
+    fr.variant = f.get("variant", 0)
+    fr.hot_pct = f.get("hot_pct", 0)
+    fr.hot_kernel = f.get("hot_kernel", 0)
+    return fr
 
 
 def moved_camera(W, H, dx, dz):
@@ -449,7 +456,7 @@ def moved_camera(W, H, dx, dz):
     return c
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "strict", "shpool"])
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "strict", "shpool", "shdefer"])
 @pytest.mark.parametrize("name", ["car_boxed", "dragon"])
 def test_frame_batch_equals_single_frames(dev, name, kernel):
     """rt_render_frames: a batch of frames (different cameras, one persistent launch on the fast paths)
@@ -602,7 +609,7 @@ def test_path_level_placements_render_the_same_frames(dev, name):
         assert a0["stats"]["rays"] == a1["stats"]["rays"], v
 
 
-@pytest.mark.parametrize("kernel", ["fast", "coop4", "fan", "shpool"])
+@pytest.mark.parametrize("kernel", ["fast", "coop4", "shpool", "shdefer"])
 def test_rotated_row_blocks_cover_every_frame(dev, kernel):
     """rt_frame.frame_shift: frame f of rank q renders block residue (q + f) % N (prt.dist rotate), rows
     past the image skipped — over the N ranks every frame of the batch is rendered exactly once, bit for
@@ -700,3 +707,44 @@ def render_cam(dev, scene, W, H, cam, kernel, rows=None):
     out = {"rgb": rgb.cpu().numpy(), "hit": hit.cpu().numpy(), "stats": r.stats()}
     r.close()
     return out
+
+
+def test_kernel_errors_fail_sync_and_download(dev):
+    """a traversal-stack overflow (rtd::C_ERR) fails rt_sync, rt_download and rt_get_stats (RT_E_KERNEL, -8) instead of
+    passing a truncated walk's frame as good: a handed-over BVH (accel="reference") 40 levels deep, whose nearer child
+    at every level is the interior one, so the farther leaf of each level stays on the walk's 34-entry stack"""
+    import torch
+    base = host.Scene.named("car_only")
+    n = 41
+    tris = np.ascontiguousarray(base.triangles[:n])
+    s = host.Scene(tris, base.lights)
+    nodes = [None]
+    big = ((-1e4, -1e4, -1e4), (1e4, 1e4, 1e4))
+
+    def node(tr_len, child):
+        return (big[0], big[1], tr_len, child)
+    cur, leaf = 0, 0
+    for level in range(n - 1):
+        c = len(nodes)
+        last = level == n - 2
+        nodes += [None, node(1, leaf)]  # (left, right = a leaf); ties: the left (interior) child is walked first
+        leaf += 1
+        nodes[cur] = node(0, c)
+        if last:
+            nodes[c] = node(1, leaf)
+            leaf += 1
+        cur = c
+    s.nodes = np.array(nodes, dtype=host.NODE_DTYPE)
+    s.tri_idx = np.arange(n, dtype=np.int32)
+    for kernel in ("strict", "fast"):
+        r = dev.Renderer(0)
+        r.upload(s, accel="reference")
+        rgb = torch.empty((16, 16, 3), dtype=torch.float32, device="cuda")
+        r.render(host.camera(16, 16), 16, 16, kernel=kernel, rgb=rgb)
+        with pytest.raises(dev.RtError, match="-8"):
+            r.sync()
+        with pytest.raises(dev.RtError, match="-8"):
+            r.download()
+        with pytest.raises(dev.RtError, match="-8"):
+            r.stats()
+        r.close()

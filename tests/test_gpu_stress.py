@@ -23,7 +23,7 @@ from prt import host
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 G = json.load(open(os.path.join(GOLD, "golden.json")))
-KERNELS = ["strict", "fast", "persist4", "coop4", "fan", "shpool", "shdefer"]
+KERNELS = ["strict", "fast", "persist4", "coop4", "shpool", "shdefer"]
 _SCENES = {}
 
 
