@@ -101,13 +101,17 @@ struct KArgs {
     const int* region_off;
     // nullable: the frame quantised on the fly (rt_outputs.bgra), one packed B|G<<8|R<<16|255<<24 per pixel
     unsigned* bgra;
+    // spp > 1 (the persistent kernels' multi-sample builds): one float4 per resident lane, [block][lane], holding the
+    // pixel's running sum of clamped samples across the sample loop, so that no register stays live across a sample's
+    // path (at the 4-wave kernels' 128-VGPR cap such values spilled inside the walks)
+    float4* lanebuf;
 };
 
 // Kernel arguments are laid out by the host compiler and read by the device compiler: both passes must
 // agree on every offset (an LDS pointer, 32-bit on gfx950 but 64-bit on the host, once shifted every
 // later field and hung a kernel). Pinned sizes catch such drift at compile time in whichever pass
 // disagrees; never put address-space-qualified pointers in these structs.
-static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 192 && sizeof(KArgs) == 416,
+static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 192 && sizeof(KArgs) == 424,
               "kernel-argument layout changed: update the pinned sizes only after checking both passes agree");
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

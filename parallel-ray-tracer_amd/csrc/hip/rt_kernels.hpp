@@ -1100,8 +1100,11 @@ __device__ __forceinline__ void render_pixel_shp(const KArgs& A, const Cam& C, i
 __device__ __forceinline__ void flush_u(const UCtr& u, unsigned long long* g);
 
 // Pixel (x, compact row k) of frame `frame` of the launch (outputs at frame * frame_px).
-// SPP1: a build for spp = 1 only (the stratified-sample loop compiled out, fewer live values around the path)
-template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0, bool SPP1 = false,
+// SPPM: 0 = either (the launch's spp decides at run time), 1 = a build for spp = 1 only (the stratified-sample loop
+// compiled out, fewer live values around the path), 2 = a build for spp > 1 only (the corner ray compiled out: one
+// inlined path; the host runs the SPPM = 1 builds for spp = 1). With A.lanebuf the running sum of a multi-sample pixel
+// lives in the lane's slot of it across the samples, not in registers.
+template <int MAXB, bool STRICT, bool COUNT, bool REG = true, int G = 1, int PB = 0, int SPPM = 0,
           bool TQ = false, bool PK = TQ>
 __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int frame, int x, int k,
                                              int* __restrict__ stk, Ctr& c, unsigned q = 0,
@@ -1114,9 +1117,44 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
     v3 col;
     if (A.bounce_hit)
         for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
-    if (SPP1 || A.spp <= 1) {
+    if (SPPM == 1 || (SPPM == 0 && A.spp <= 1)) {
         col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB, PK, TQ>(A, C.pos, primary_dir(C, (float)x, (float)y),
                                                                           stk, c, hit0, t0, (int)o, q, sstk, wcap));
+    } else if (SPPM == 2 && A.lanebuf) {  // stratified g x g sub-pixel grid, mean of clamped samples
+        // the persistent kernels' multi-sample builds: the lane's A.lanebuf slot carries the running sum and the pixel
+        // (x, compact row k) from sample to sample, so that no register stays live across a sample's path; hit / t of
+        // the first sample are stored as soon as it returns (the host guarantees W, n_rows <= 65535)
+        const int g = A.spp_grid;
+        float4* lb = A.lanebuf + (size_t)blockIdx.x * BLOCK + threadIdx.x;
+        *lb = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((unsigned)x | ((unsigned)k << 16)));
+        v3 acc = mk(0.0f, 0.0f, 0.0f);
+        for (int s = 0; s < g * g; ++s) {
+            __asm__ volatile("" ::: "memory");  // (read the slot back: no value forwarded in registers across the path)
+            const float4 e = *lb;
+            const unsigned px = __float_as_uint(e.w);
+            const int xs = (int)(px & 0xFFFFu), ks = (int)(px >> 16), ys = image_row(A, ks, frame);
+            const int sj = s / g, si = s - sj * g;
+            const float fx = (float)xs + ((float)si + 0.5f) / (float)g;
+            const float fy = (float)ys + ((float)sj + 0.5f) / (float)g;
+            const size_t os = (size_t)frame * A.frame_px + (size_t)ks * A.W + xs;
+            int h;
+            float tt;
+            const v3 cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB, PK, TQ>(
+                A, C.pos, primary_dir(C, fx, fy), stk, c, h, tt, s == 0 ? (int)os : -1, q, sstk, wcap));
+            if (s == 0 && q == 0) {
+                if (A.hit) A.hit[os] = h;
+                if (A.t) A.t[os] = tt;
+            }
+            __asm__ volatile("" ::: "memory");
+            const float4 a = *lb;
+            acc = add(mk(a.x, a.y, a.z), cs);
+            *lb = make_float4(acc.x, acc.y, acc.z, a.w);
+        }
+        const float nn = (float)(g * g);
+        c.pix++;
+        if (q != 0) return;
+        store_px(A.rgb, A.bgra, o, mk(acc.x / nn, acc.y / nn, acc.z / nn));
+        return;
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples
         const int g = A.spp_grid;
         v3 acc = mk(0.0f, 0.0f, 0.0f);
@@ -1259,7 +1297,7 @@ void k_persist(KArgs A) {
             render_pixel_shp<MAXB, COUNT, SPP1, SHP>(A, cam_of<BATCH>(A, frame), frame, x, k, x < A.W && k < A.n_rows,
                                                      stk, c, u, sstk, wcap);
         else if (x < A.W && k < A.n_rows)
-            render_pixel<MAXB, STRICT, COUNT, REG, 1, PB, SPP1, SHP == 3, SHP == 3 && DYN>(
+            render_pixel<MAXB, STRICT, COUNT, REG, 1, PB, SPP1 ? 1 : 2, SHP == 3, SHP == 3 && DYN>(
                 A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, 0u, sstk, wcap);
         if (TRACE) {  // {begin, end, wave | fallbacks << 32, wave steps | lane node visits << 32} (COUNT)
             const unsigned fb = wave_sum(c.fb - fb0), ws = wave_sum(c.ws - ws0), nv = wave_sum(c.chi + c.shi - nd0);

@@ -546,18 +546,30 @@ __device__ __forceinline__ void render_pixel_shp(const KArgs& A, const Cam& C, i
     if (A.bounce_hit && valid)
         for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
     v3 col;
-    if (SPP1 || A.spp <= 1) {
+    if constexpr (SPP1) {  // (the host runs the SPP1 builds for spp = 1, the others for spp > 1 only)
         col = clamp01(trace(primary_dir(C, (float)x, (float)y), hpix));
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples; hit / t from the first sample
+        // The lane's A.lanebuf slot carries the running sum and the pixel (x, compact row k) from sample to sample, so
+        // that no register stays live across a sample's path (spp_slot; the host guarantees W, n_rows <= 65535)
         const int g = A.spp_grid;
+        float4* lb = A.lanebuf + (size_t)blockIdx.x * BLOCK + threadIdx.x;
+        *lb = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((unsigned)x | ((unsigned)k << 16)));
         v3 acc = mk(0.0f, 0.0f, 0.0f);
-        for (int sj = 0; sj < g; ++sj)
-            for (int si = 0; si < g; ++si) {
-                const float fx = (float)x + ((float)si + 0.5f) / (float)g;
-                const float fy = (float)y + ((float)sj + 0.5f) / (float)g;
-                const v3 cs = clamp01(trace(primary_dir(C, fx, fy), si == 0 && sj == 0 ? hpix : -1));
-                acc = add(acc, cs);
-            }
+        for (int s = 0; s < g * g; ++s) {
+            __asm__ volatile("" ::: "memory");  // (read the slot back: no value forwarded in registers across the path)
+            const float4 e = *lb;
+            const unsigned px = __float_as_uint(e.w);
+            const int xs = (int)(px & 0xFFFFu), ks = (int)(px >> 16), ys = image_row(A, ks, frame);
+            const int sj = s / g, si = s - sj * g;
+            const float fx = (float)xs + ((float)si + 0.5f) / (float)g;
+            const float fy = (float)ys + ((float)sj + 0.5f) / (float)g;
+            const int hp = s == 0 && valid ? (int)((size_t)frame * A.frame_px + (size_t)ks * A.W + xs) : -1;
+            const v3 cs = clamp01(trace(primary_dir(C, fx, fy), hp));
+            __asm__ volatile("" ::: "memory");
+            const float4 a = *lb;
+            acc = add(mk(a.x, a.y, a.z), cs);
+            *lb = make_float4(acc.x, acc.y, acc.z, a.w);
+        }
         const float nn = (float)(g * g);
         col = mk(acc.x / nn, acc.y / nn, acc.z / nn);
     }
