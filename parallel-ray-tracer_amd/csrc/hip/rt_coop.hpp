@@ -196,7 +196,7 @@ __device__ __forceinline__ void closest_wide_g(const DWide& W, v3 o, v3 d, float
             hp = hlo;
         }
         if (next < 0) {
-            if (next == -2) c.err++;
+            if (next == -2) CTR_INC(c, err, C_ERR);
             break;
         }
     }
@@ -245,7 +245,7 @@ __device__ __forceinline__ bool visible_wide_g(const DWide& W, v3 o, v3 d, float
             best = g_minf<G>(lb);
         }
         if (next < 0) {
-            if (next == -2) c.err++;
+            if (next == -2) CTR_INC(c, err, C_ERR);
             break;
         }
     }
@@ -267,7 +267,7 @@ __device__ __forceinline__ int closest_g(const DScene& s, v3 o, v3 d, float& bes
         best = FMAX;
         nd = 0;
     }
-    c.fb++;  // strict re-walk, redundantly in every lane of the group
+    CTR_INC(c, fb, C_FALLBACK);  // strict re-walk, redundantly in every lane of the group
     closest_walk<true, COUNT, true>(s.ref, o, d, best, hp, nd, tie, stk, c);
     return hp >= 0 ? s.ref.tri_orig[hp] : -1;
 }
@@ -276,7 +276,7 @@ template <int G, bool COUNT>
 __device__ __forceinline__ bool visible_g(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c,
                                           unsigned q) {
     if (!degenerate(d)) return visible_wide_g<G, COUNT>(wide_for(s, true), o, d, ld2, stk, c, q);  // |d| = 1
-    c.fb++;
+    CTR_INC(c, fb, C_FALLBACK);
     return visible_walk<true, COUNT, true>(s.ref, o, d, ld2, stk, c);
 }
 

@@ -103,6 +103,7 @@ struct rt_ctx {
     std::vector<float> cams_last;  // the set d_cams holds (after its copy)
     rt_launch_info last_launch{};  // rt_get_launch_info
     float4* d_pathbuf = nullptr;  // PB kernels: per-wave path levels (rtd::KArgs::pathbuf)
+    float4* d_lanebuf = nullptr;  // k_persist's multi-sample builds: one slot per resident lane (rtd::KArgs::lanebuf)
     int* d_gstack = nullptr;      // DYN kernels: the binary walks' stacks (rtd::KArgs::gstack)
     float* h_cams = nullptr;  // pinned: CAM_SLOTS x cams_cap cameras
     int cams_cap = 0;
@@ -962,8 +963,11 @@ bool pbl_fits(const rtd::KArgs& A, int device, int shp = 0) {
 template <int MAXB>
 KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, size_t& dyn, bool pk_ok, bool tq_ok) {
     dyn = 0;
+    // (the k_persist builds are made either for spp = 1 (SPP1) or for spp > 1 only: each launch takes the one its spp
+    // needs; a tile trace -- the hybrid rule's measuring frame, PRT_TILE_TRACE -- is single-sample)
     if (A.tile_trace)
-        return count ? rtd::k_persist<MAXB, false, true, true, 3, true, true> : rtd::k_persist<MAXB, false, false, true, 3, true, true>;
+        return count ? rtd::k_persist<MAXB, false, true, true, 3, true, true, 0, false, true>
+                     : rtd::k_persist<MAXB, false, false, true, 3, true, true, 0, false, true>;
     if ((variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) && pk_ok && tq_ok) {
         const int shp = variant == RT_VARIANT_SHDEFER ? 2 : 1;
         if (pbl_fits<MAXB>(A, device, shp)) {
@@ -991,6 +995,9 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
     if (A.spp <= 1 && tq_ok)
         return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true, 0, false, true, 3>
                      : rtd::k_persist<MAXB, false, false, true, 3, false, true, 0, false, true, 3>;
+    if (A.spp <= 1)  // (scenes past the packed tests' triangle bound)
+        return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true, 0, false, true>
+                     : rtd::k_persist<MAXB, false, false, true, 3, false, true, 0, false, true>;
     return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true> : rtd::k_persist<MAXB, false, false, true, 3, false, true>;
 }
 
@@ -1132,6 +1139,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     while (g * g < f->spp) g++;
     if (f->spp < 1 || g * g != f->spp || g > 16) return arg_err(ctx, "rt_render: spp must be a square 1..256");
     if (f->kernel < RT_KERNEL_AUTO || f->kernel > RT_KERNEL_FAST) return arg_err(ctx, "rt_render: bad kernel");
+    if (f->spp > 1 && (f->width > 65535 || f->n_rows > 65535))  // (k_persist's multi-sample slots pack x and the row)
+        return arg_err(ctx, "rt_render: spp > 1 frames are at most 65535 pixels wide and 65535 rows high");
     // (variants 3, 6, 7, 8, 9, 10, 12, 14 -- the split pipeline, k_coop<8>, k_fan, k_chain, k_pool, k_relay, k_stream
     // -- measured slower than k_persist and were removed: refused)
     const bool known = f->variant == RT_VARIANT_DEFAULT || f->variant == RT_VARIANT_PERSIST ||
@@ -1229,8 +1238,11 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         HIPC(hipMalloc((void**)&ctx->d_pathbuf, sizeof(float4) * waves * 8 * 64));  // MAXB <= 8 levels
         // DYN kernels' binary-walk stacks: STACK ints per lane of every resident workgroup (<= 8 per CU)
         HIPC(hipMalloc((void**)&ctx->d_gstack, sizeof(int) * (size_t)cus * 8 * rtd::STACK * rtd::BLOCK));
+        // the multi-sample builds' per-lane slots (the running sum and the pixel between samples): every resident lane
+        HIPC(hipMalloc((void**)&ctx->d_lanebuf, sizeof(float4) * (size_t)cus * 8 * rtd::BLOCK));
     }
     A.pathbuf = ctx->d_pathbuf;
+    A.lanebuf = ctx->d_lanebuf;
     A.gstack = ctx->d_gstack;
     A.wcap = ctx->wide_n > 0 ? std::max(1, std::max(ctx->wide_depth, std::max(ctx->unit_depth, ctx->prim_depth))) : 0;
     if (n_frames > 1) {  // the batch's cameras, uploaded when they change
@@ -1248,7 +1260,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     const char* trace_path = std::getenv("PRT_TILE_TRACE");
     unsigned long long* d_trace = nullptr;
     const size_t trace_n = (size_t)A.n_tiles;
-    if (trace_path && kernel == RT_KERNEL_FAST && n_frames == 1) {
+    if (trace_path && kernel == RT_KERNEL_FAST && n_frames == 1 && f->spp == 1) {
         HIPC(hipMalloc((void**)&d_trace, sizeof(unsigned long long) * 4 * trace_n));
         HIPC(hipMemsetAsync(d_trace, 0, sizeof(unsigned long long) * 4 * trace_n, ctx->stream));
         A.tile_trace = d_trace;
@@ -2509,6 +2521,7 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     if (ctx->d_rgb_own) (void)hipFree(ctx->d_rgb_own);
     if (ctx->d_cams) (void)hipFree(ctx->d_cams);
     if (ctx->d_pathbuf) (void)hipFree(ctx->d_pathbuf);
+    if (ctx->d_lanebuf) (void)hipFree(ctx->d_lanebuf);
     if (ctx->d_gstack) (void)hipFree(ctx->d_gstack);
     if (ctx->h_cams) (void)hipHostFree(ctx->h_cams);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);

@@ -48,7 +48,30 @@ struct Ctr {
     unsigned prim, refl, shad, skip, hits, chi, chl, cht, shi, shl, sht, pix, err, fb, nb, ws, wsh, q1, q2, q3, q4;
     unsigned lvl;    // the bounce level of the walks the lane runs (the histogram's level)
     unsigned* hist;  // RT_FLAG_COUNTERS kernels that keep the histogram: the workgroup's 32 slots in LDS (hist_lds)
+    // evm (k_persist's production builds): the ray / pixel / fallback / error events are added to the workgroup's LDS
+    // words `ev` (C_* slots) by one lane per wave and event (ev_add) instead of being counted in eight vector registers
+    // held across every walk (at the 4-wave kernels' 128-VGPR cap those registers were spills)
+    bool evm;
+    unsigned* ev;
 };
+
+// The workgroup's event counters of an evm kernel (k_persist without RT_FLAG_COUNTERS): 16 words of LDS, C_PRIM ..
+// C_FALLBACK, added to the launch's counters once at the end.
+template <bool EV>
+__device__ __forceinline__ unsigned* ev_lds() {
+    __shared__ unsigned e[16];
+    return e;
+}
+// one event for every active lane: the wave's first active lane adds their number (divergent code included)
+__device__ __forceinline__ void ev_add(unsigned* ev, int slot) {
+    const unsigned long long ex = __builtin_amdgcn_read_exec();
+    if ((threadIdx.x & 63u) == (unsigned)__builtin_ctzll(ex)) atomicAdd(ev + slot, (unsigned)__builtin_popcountll(ex));
+}
+#define CTR_INC(c, field, slot)          \
+    do {                                 \
+        if ((c).evm) ev_add((c).ev, slot); \
+        else (c).field++;                \
+    } while (0)
 
 // The wave-step histogram of a counting k_persist workgroup (LDS atomics; the 32 slots go to counters + C_HIST at the
 // end). Instantiated only by the counting kernels, so the others' LDS budget is untouched.
@@ -180,7 +203,7 @@ __device__ __forceinline__ void closest_walk(const DBvh& B, v3 o, v3 d, float& b
             children<STRICT>(B, cur, o, d, p, ni, nt, fi, ft);
             const bool vn = visit<STRICT>(nt, best), vf = visit<STRICT>(ft, best);
             if (sp + 2 > STACK) {  // cannot happen for depth <= 32 BVHs; reported, never silent
-                c.err++;
+                CTR_INC(c, err, C_ERR);
                 break;
             }
             if (REG) {
@@ -251,7 +274,7 @@ __device__ __forceinline__ bool visible_walk(const DBvh& B, v3 o, v3 d, float ld
             children<STRICT>(B, cur, o, d, p, ni, nt, fi, ft);
             const bool vn = visit<STRICT>(nt, best), vf = visit<STRICT>(ft, best);
             if (sp + 2 > STACK) {
-                c.err++;
+                CTR_INC(c, err, C_ERR);
                 break;
             }
             if (REG) {
@@ -687,7 +710,7 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
             }
         }
         if (next < 0) {
-            if (next == -2) c.err++;
+            if (next == -2) CTR_INC(c, err, C_ERR);
             break;
         }
     }
@@ -768,7 +791,7 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
             }
         }
         if (next < 0) {
-            if (next == -2) c.err++;
+            if (next == -2) CTR_INC(c, err, C_ERR);
             break;
         }
     }
@@ -804,12 +827,12 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
             closest_walk<false, COUNT, REG>(s.acc, o, d, best, hp, nd, tie, bstk, c);
             if (!tie) return hp >= 0 ? s.acc.tri_orig[hp] : -1;
         }
-        c.fb++;
+        CTR_INC(c, fb, C_FALLBACK);
         hp = -1;
         best = FMAX;
         nd = 0;
     } else if (!STRICT) {
-        c.fb++;
+        CTR_INC(c, fb, C_FALLBACK);
     }
     closest_walk<true, COUNT, REG>(s.ref, o, d, best, hp, nd, tie, bstk, c);
     return hp >= 0 ? s.ref.tri_orig[hp] : -1;
@@ -824,7 +847,7 @@ __device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, 
             return visible_wide<COUNT, PIPE, PK, TQ>(wide_for(s, true), o, d, ld2, stk, c, wcap, tq);
         return visible_walk<false, COUNT, REG>(s.acc, o, d, ld2, bstk, c);
     }
-    if (!STRICT) c.fb++;
+    if (!STRICT) CTR_INC(c, fb, C_FALLBACK);
     return visible_walk<true, COUNT, REG>(s.ref, o, d, ld2, bstk, c);
 }
 
@@ -883,8 +906,8 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
     float best;
     int nd;
     if (COUNT) c.lvl = (unsigned)it;
-    if (it == 0) c.prim++;
-    else c.refl++;
+    if (it == 0) CTR_INC(c, prim, C_PRIM);
+    else CTR_INC(c, refl, C_REFL);
     int orig;
     if constexpr (G > 1) orig = closest_g<G, COUNT>(s, o, d, best, nd, stk, c, q, it > 0);
     else orig = closest<STRICT, COUNT, REG, false, PK, TQ>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0, tq);  // it > 0: |d| = 1
@@ -900,7 +923,7 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
         tail = false;
         return true;
     }
-    c.hits++;
+    CTR_INC(c, hits, C_HITS);
     const v3 ip = add(o, mul(d, best));  // raytracer.c:137-138
     const float4 sh0 = s.shade[2 * orig], sh1 = s.shade[2 * orig + 1];
     const int m = __float_as_int(sh0.w);
@@ -921,9 +944,9 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
         int V;
         if (dot(tmp2, n) < 0) {
             V = 0;
-            c.skip++;
+            CTR_INC(c, skip, C_SKIP);
         } else {
-            c.shad++;
+            CTR_INC(c, shad, C_SHAD);
             if constexpr (G > 1) V = visible_g<G, COUNT>(s, ip, l, ld2, stk, c, q) ? 1 : 0;
             else V = visible<STRICT, COUNT, REG, false, PK, TQ>(s, ip, l, ld2, stk, c, sstk, wcap, tq) ? 1 : 0;
         }
@@ -1090,6 +1113,28 @@ __device__ __forceinline__ v3 primary_dir(const Cam& C, float fx, float fy) {
 __device__ __forceinline__ v3 primary_dir(const KArgs& A, float fx, float fy) {
     return primary_dir(cam_of(A, 0), fx, fy);
 }
+// The same inside a multi-sample loop: the wave-uniform camera re-read from its scalar registers at every sample
+// (an empty asm the compiler cannot look through), so that ul - pos, a loop invariant it would otherwise hoist into
+// vector registers live across every sample's path, is formed per sample
+__device__ __forceinline__ v3 primary_dir_sample(const Cam& C, float fx, float fy) {
+    float p[12] = {C.pos.x, C.pos.y, C.pos.z, C.ul.x, C.ul.y, C.ul.z, C.ix.x, C.ix.y, C.ix.z, C.iy.x, C.iy.y, C.iy.z};
+#pragma unroll
+    for (int i = 0; i < 12; i++) __asm__ volatile("" : "+s"(p[i]));
+    return primary_dir(Cam{mk(p[0], p[1], p[2]), mk(p[3], p[4], p[5]), mk(p[6], p[7], p[8]), mk(p[9], p[10], p[11])},
+                       fx, fy);
+}
+// The lane's index in its wave, computed where it is used (v_mbcnt in an asm the compiler cannot hoist or keep): in the
+// 4-wave kernels every register held across the walks costs a spill, and this one is two instructions to remake.
+__device__ __forceinline__ unsigned lane_now() {
+    unsigned l;
+    __asm__ volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+// a lane's A.lanebuf slot ([block][lane]): the wave's slots from scalar registers, the lane's offset remade per use
+__device__ __forceinline__ float4* lane_slot(const KArgs& A) {
+    const unsigned wave = (unsigned)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6)));
+    return reinterpret_cast<float4*>(reinterpret_cast<char*>(A.lanebuf + (size_t)wave * 64) + lane_now() * 16u);
+}
 
 // the shadow-pool kernels' pixel (rt_shpool.hpp, RT_VARIANT_SHPOOL): every lane of the wave calls it
 struct UCtr;
@@ -1120,16 +1165,17 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
     if (SPPM == 1 || (SPPM == 0 && A.spp <= 1)) {
         col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB, PK, TQ>(A, C.pos, primary_dir(C, (float)x, (float)y),
                                                                           stk, c, hit0, t0, (int)o, q, sstk, wcap));
-    } else if (SPPM == 2 && A.lanebuf) {  // stratified g x g sub-pixel grid, mean of clamped samples
+    } else if (SPPM == 2) {  // stratified g x g sub-pixel grid, mean of clamped samples
         // the persistent kernels' multi-sample builds: the lane's A.lanebuf slot carries the running sum and the pixel
         // (x, compact row k) from sample to sample, so that no register stays live across a sample's path; hit / t of
-        // the first sample are stored as soon as it returns (the host guarantees W, n_rows <= 65535)
+        // the first sample are stored as soon as it returns (the host sets A.lanebuf for every k_persist launch and
+        // guarantees W, n_rows <= 65535 for spp > 1)
         const int g = A.spp_grid;
-        float4* lb = A.lanebuf + (size_t)blockIdx.x * BLOCK + threadIdx.x;
-        *lb = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((unsigned)x | ((unsigned)k << 16)));
+        *lane_slot(A) = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((unsigned)x | ((unsigned)k << 16)));
         v3 acc = mk(0.0f, 0.0f, 0.0f);
         for (int s = 0; s < g * g; ++s) {
             __asm__ volatile("" ::: "memory");  // (read the slot back: no value forwarded in registers across the path)
+            float4* lb = lane_slot(A);
             const float4 e = *lb;
             const unsigned px = __float_as_uint(e.w);
             const int xs = (int)(px & 0xFFFFu), ks = (int)(px >> 16), ys = image_row(A, ks, frame);
@@ -1140,18 +1186,21 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
             int h;
             float tt;
             const v3 cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB, PK, TQ>(
-                A, C.pos, primary_dir(C, fx, fy), stk, c, h, tt, s == 0 ? (int)os : -1, q, sstk, wcap));
-            if (s == 0 && q == 0) {
-                if (A.hit) A.hit[os] = h;
-                if (A.t) A.t[os] = tt;
-            }
+                A, C.pos, primary_dir_sample(C, fx, fy), stk, c, h, tt, s == 0 ? (int)os : -1, q, sstk, wcap));
             __asm__ volatile("" ::: "memory");
+            lb = lane_slot(A);
             const float4 a = *lb;
+            if (s == 0 && q == 0) {  // (the output index from the slot again, not held across the path)
+                const unsigned pa = __float_as_uint(a.w);
+                const size_t oa = (size_t)frame * A.frame_px + (size_t)(pa >> 16) * A.W + (pa & 0xFFFFu);
+                if (A.hit) A.hit[oa] = h;
+                if (A.t) A.t[oa] = tt;
+            }
             acc = add(mk(a.x, a.y, a.z), cs);
             *lb = make_float4(acc.x, acc.y, acc.z, a.w);
         }
         const float nn = (float)(g * g);
-        c.pix++;
+        CTR_INC(c, pix, C_PIX);
         if (q != 0) return;
         store_px(A.rgb, A.bgra, o, mk(acc.x / nn, acc.y / nn, acc.z / nn));
         return;
@@ -1176,7 +1225,7 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
         const float nn = (float)(g * g);
         col = mk(acc.x / nn, acc.y / nn, acc.z / nn);
     }
-    c.pix++;
+    CTR_INC(c, pix, C_PIX);
     if (q != 0) return;  // a group's pixel is written once
     store_px(A.rgb, A.bgra, o, col);
     if (A.hit) A.hit[o] = hit0;
@@ -1271,6 +1320,13 @@ void k_persist(KArgs A) {
         if (threadIdx.x < 32) c.hist[threadIdx.x] = 0u;
         __syncthreads();
     }
+    constexpr bool EVM = !COUNT && !TRACE;  // (the tile trace reads the per-lane fallback counts)
+    if constexpr (EVM) {
+        c.evm = true;
+        c.ev = ev_lds<true>();
+        if (threadIdx.x < 16) c.ev[threadIdx.x] = 0u;
+        __syncthreads();
+    }
     UCtrOf<SHP> u = {};  // SHP: the wave-uniform ray counts (rt_shpool.hpp)
     if constexpr (SHP == 3) {  // the wave's packed-triangle queue starts clear
         if constexpr (DYN) {
@@ -1289,7 +1345,8 @@ void k_persist(KArgs A) {
         unsigned tile;
         if (!next_item(A, lane, reg, frame, tile)) break;
         const int tx = (int)(tile % (unsigned)A.tiles_x), ty = (int)(tile / (unsigned)A.tiles_x);
-        const int x = tx * 8 + (lane & 7), k = ty * 8 + (lane >> 3);
+        const unsigned ln = lane_now();  // (remade per tile rather than held, or spilled, across the walks)
+        const int x = tx * 8 + (int)(ln & 7u), k = ty * 8 + (int)(ln >> 3);
         unsigned long long t0 = 0;
         const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
         if (TRACE) t0 = __builtin_amdgcn_s_memrealtime();
@@ -1311,6 +1368,10 @@ void k_persist(KArgs A) {
     }
     flush<COUNT>(c, A.counters);
     if constexpr (SHP == 1 || SHP == 2) flush_u(u, A.counters);
+    if constexpr (EVM) {  // every wave of the workgroup leaves the tile loop and reaches this point
+        __syncthreads();
+        if (threadIdx.x < 16 && c.ev[threadIdx.x]) atomicAdd(A.counters + threadIdx.x, (unsigned long long)c.ev[threadIdx.x]);
+    }
     if constexpr (COUNT) {  // every wave of the workgroup leaves the tile loop and reaches this point
         __syncthreads();
         if (threadIdx.x < 32 && c.hist[threadIdx.x]) atomicAdd(A.counters + C_HIST + threadIdx.x, (unsigned long long)c.hist[threadIdx.x]);

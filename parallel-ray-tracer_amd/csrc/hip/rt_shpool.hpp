@@ -160,7 +160,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
                 o = ipo;
                 d = l;
                 if (degenerate(d)) {  // zero direction component: the reference's NaN slabs, walked strictly
-                    c.fb++;
+                    CTR_INC(c, fb, C_FALLBACK);
                     if (visible_walk<true, COUNT, true>(s.ref, o, d, ld2, sstk ? sstk : stk, c))
                         atomicOr(reinterpret_cast<unsigned*>(lvl + (wo & 511)) + 3, 1u << ((wo >> 9) & 31));
                 } else {
@@ -257,7 +257,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
                     }
                 }
                 if (occ || next < 0) {
-                    if (!occ && next == -2) c.err++;
+                    if (!occ && next == -2) CTR_INC(c, err, C_ERR);
                     if (!occ)  // the owner's visibility bit
                         atomicOr(reinterpret_cast<unsigned*>(lvl + (wo & 511)) + 3, 1u << ((wo >> 9) & 31));
                     busy = false;
@@ -541,22 +541,23 @@ __device__ __forceinline__ void render_pixel_shp(const KArgs& A, const Cam& C, i
     const int y = image_row(A, k, frame);
     valid = valid && y < A.H;  // frame_shift: a rotated rank's compact rows past the image
     u.pix += popc_wave(valid);
-    const size_t o = (size_t)frame * A.frame_px + (size_t)k * A.W + x;
-    const int hpix = valid ? (int)o : -1;
-    if (A.bounce_hit && valid)
+    if (A.bounce_hit && valid) {
+        const size_t o = (size_t)frame * A.frame_px + (size_t)k * A.W + x;
         for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
-    v3 col;
+    }
     if constexpr (SPP1) {  // (the host runs the SPP1 builds for spp = 1, the others for spp > 1 only)
-        col = clamp01(trace(primary_dir(C, (float)x, (float)y), hpix));
+        const size_t o = (size_t)frame * A.frame_px + (size_t)k * A.W + x;
+        const v3 col = clamp01(trace(primary_dir(C, (float)x, (float)y), valid ? (int)o : -1));
+        if (valid) store_px(A.rgb, A.bgra, o, col);
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples; hit / t from the first sample
         // The lane's A.lanebuf slot carries the running sum and the pixel (x, compact row k) from sample to sample, so
         // that no register stays live across a sample's path (spp_slot; the host guarantees W, n_rows <= 65535)
         const int g = A.spp_grid;
-        float4* lb = A.lanebuf + (size_t)blockIdx.x * BLOCK + threadIdx.x;
-        *lb = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((unsigned)x | ((unsigned)k << 16)));
+        *lane_slot(A) = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((unsigned)x | ((unsigned)k << 16)));
         v3 acc = mk(0.0f, 0.0f, 0.0f);
         for (int s = 0; s < g * g; ++s) {
             __asm__ volatile("" ::: "memory");  // (read the slot back: no value forwarded in registers across the path)
+            float4* lb = lane_slot(A);
             const float4 e = *lb;
             const unsigned px = __float_as_uint(e.w);
             const int xs = (int)(px & 0xFFFFu), ks = (int)(px >> 16), ys = image_row(A, ks, frame);
@@ -564,16 +565,19 @@ __device__ __forceinline__ void render_pixel_shp(const KArgs& A, const Cam& C, i
             const float fx = (float)xs + ((float)si + 0.5f) / (float)g;
             const float fy = (float)ys + ((float)sj + 0.5f) / (float)g;
             const int hp = s == 0 && valid ? (int)((size_t)frame * A.frame_px + (size_t)ks * A.W + xs) : -1;
-            const v3 cs = clamp01(trace(primary_dir(C, fx, fy), hp));
+            const v3 cs = clamp01(trace(primary_dir_sample(C, fx, fy), hp));
             __asm__ volatile("" ::: "memory");
+            lb = lane_slot(A);
             const float4 a = *lb;
             acc = add(mk(a.x, a.y, a.z), cs);
             *lb = make_float4(acc.x, acc.y, acc.z, a.w);
         }
         const float nn = (float)(g * g);
-        col = mk(acc.x / nn, acc.y / nn, acc.z / nn);
+        __asm__ volatile("" ::: "memory");
+        const unsigned px = __float_as_uint(lane_slot(A)->w);  // (the pixel from the slot: nothing of it live across the loop)
+        const size_t o = (size_t)frame * A.frame_px + (size_t)(px >> 16) * A.W + (px & 0xFFFFu);
+        if (valid) store_px(A.rgb, A.bgra, o, mk(acc.x / nn, acc.y / nn, acc.z / nn));
     }
-    if (valid) store_px(A.rgb, A.bgra, o, col);
 }
 
 }  // namespace rtd

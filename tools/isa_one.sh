@@ -22,9 +22,17 @@ mkdir -p /tmp/isa
 python3 - <<'PY'
 import re
 s = open('/tmp/isa/one.s').read()
+# the code of each kernel (between its label and its descriptor) for the spill instructions it really executes
+code = {}
+for m in re.finditer(r'^(_Z\S+):[^\n]*$(.*?)^\s*\.section\s+\.rodata', s, re.S | re.M):
+    code[m.group(1)] = m.group(2)
 for b in s.split('.amdhsa_kernel ')[1:]:
     name = b.split('\n')[0]
     g = lambda k: re.search(k + r'\s+(\d+)', b).group(1)
+    c = code.get(name, '')
+    st, ld = len(re.findall(r'scratch_store', c)), len(re.findall(r'scratch_load', c))
+    wl = len(re.findall(r'v_writelane_b32', c))
     print(f"{name[:80]:80s} vgpr {g(r'.amdhsa_next_free_vgpr'):>4} sgpr {g(r'.amdhsa_next_free_sgpr'):>4} "
-          f"scratch {g(r'.amdhsa_private_segment_fixed_size'):>4} lds {g(r'.amdhsa_group_segment_fixed_size'):>6}")
+          f"scratch {g(r'.amdhsa_private_segment_fixed_size'):>4} (spill st/ld {st}/{ld}, sgpr->vgpr-lane {wl}) "
+          f"lds {g(r'.amdhsa_group_segment_fixed_size'):>6}")
 PY
