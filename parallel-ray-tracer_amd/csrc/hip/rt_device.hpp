@@ -49,6 +49,7 @@ struct DWide {
     const float4* __restrict__ nodes;  // nullptr: no wide view (the fast walk uses `acc`)
     const float4* __restrict__ tris;   // 48-B triangle records in wide-leaf order
     const int* __restrict__ tri_orig;  // wide-leaf position -> original triangle index
+    int n;                             // wide nodes (the LDS staging of the top levels copies min(n, NTOP) of them)
 };
 
 struct DScene {
@@ -111,7 +112,7 @@ struct KArgs {
 // agree on every offset (an LDS pointer, 32-bit on gfx950 but 64-bit on the host, once shifted every
 // later field and hung a kernel). Pinned sizes catch such drift at compile time in whichever pass
 // disagrees; never put address-space-qualified pointers in these structs.
-static_assert(sizeof(DWide) == 24 && sizeof(DScene) == 192 && sizeof(KArgs) == 424,
+static_assert(sizeof(DWide) == 32 && sizeof(DScene) == 216 && sizeof(KArgs) == 448,
               "kernel-argument layout changed: update the pinned sizes only after checking both passes agree");
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

@@ -1171,12 +1171,12 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     std::memset(&A, 0, sizeof A);
     A.s.ref = dview(ctx->ref);
     A.s.acc = ctx->acc.nodes ? dview(ctx->acc) : A.s.ref;
-    A.s.wide = rtd::DWide{ctx->wide_nodes, ctx->wide_tris, ctx->wide_orig};
-    A.s.unit = rtd::DWide{ctx->unit_nodes, ctx->unit_tris, ctx->unit_orig};
+    A.s.wide = rtd::DWide{ctx->wide_nodes, ctx->wide_tris, ctx->wide_orig, ctx->wide_n};
+    A.s.unit = rtd::DWide{ctx->unit_nodes, ctx->unit_tris, ctx->unit_orig, ctx->unit_n};
     // the primary view when every primary direction of every frame of the launch is short enough for it
     bool prim_ok = ctx->prim_nodes != nullptr;
     for (int i = 0; i < n_frames && prim_ok; i++) prim_ok = primary_dmax(cams + i, f->width, f->height) <= PRIMARY_D;
-    if (prim_ok) A.s.prim = rtd::DWide{ctx->prim_nodes, ctx->prim_tris, ctx->prim_orig};
+    if (prim_ok) A.s.prim = rtd::DWide{ctx->prim_nodes, ctx->prim_tris, ctx->prim_orig, ctx->prim_n};
     A.s.shade = ctx->d_shade;
     A.s.mats = ctx->d_mats;
     A.s.lights = ctx->d_lights;

@@ -53,6 +53,9 @@ struct Ctr {
     // held across every walk (at the 4-wave kernels' 128-VGPR cap those registers were spills)
     bool evm;
     unsigned* ev;
+    // LDS_TOP kernels: the first NTOP wide nodes (the root and its interior children, breadth-first) of the primary
+    // view [0] and of the unit-direction view [1], staged in the workgroup's LDS (stage_top); null: none
+    const float4* top[2];
 };
 
 // The workgroup's event counters of an evm kernel (k_persist without RT_FLAG_COUNTERS): 16 words of LDS, C_PRIM ..
@@ -66,6 +69,17 @@ __device__ __forceinline__ unsigned* ev_lds() {
 __device__ __forceinline__ void ev_add(unsigned* ev, int slot) {
     const unsigned long long ex = __builtin_amdgcn_read_exec();
     if ((threadIdx.x & 63u) == (unsigned)__builtin_ctzll(ex)) atomicAdd(ev + slot, (unsigned)__builtin_popcountll(ex));
+}
+// LDS_TOP: the two views' top nodes (NTOP each, 1,440 B per workgroup), copied by the workgroup at kernel start
+constexpr int NTOP = 9;  // the root + its <= 8 interior children (breadth-first records 0 .. 8)
+#ifndef PRT_LDS_TOP
+#define PRT_LDS_TOP 0
+#endif
+constexpr bool LDS_TOP = PRT_LDS_TOP != 0;
+template <bool T>
+__device__ __forceinline__ float4* top_lds() {
+    __shared__ float4 t[2 * NTOP * 5];
+    return t;
 }
 #define CTR_INC(c, field, slot)          \
     do {                                 \
@@ -373,8 +387,11 @@ __device__ __forceinline__ float ubyte(unsigned w, int b) { return (float)((w >>
 struct WNode {
     float4 f0, f1, f2, f3, f4;
 };
-__device__ __forceinline__ WNode wload(const DWide& W, int node) {
-    const float4* N = W.nodes + 5 * node;
+// The upper levels in LDS (LDS_TOP, north star "LDS-staged upper BVH levels"): every walk starts with the root and
+// most continue into its children; with `top` set, a node below NTOP is read from the workgroup's LDS copy. The
+// address is selected, not branched on (a flat load serves both), so the next-node load stays unconditional.
+__device__ __forceinline__ WNode wload(const DWide& W, int node, const float4* top = nullptr) {
+    const float4* N = (top && node < NTOP) ? top + 5 * node : W.nodes + 5 * node;
     return WNode{N[0], N[1], N[2], N[3], N[4]};
 }
 
@@ -633,11 +650,12 @@ __device__ __forceinline__ bool shadow_tris_packed(const DWide& W, v3 o, v3 d, f
 // TQ: a step whose lanes hold 3+ triangles tests them packed (closest_tris_packed; tq: the wave's queue).
 template <bool COUNT, bool PIPE = false, bool PK = false, bool TQ = false>
 __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& best, int& hp, int& nd, bool& tie,
-                                             int* __restrict__ stk, Ctr& c, int wcap = WSTACK, int* tq = nullptr) {
+                                             int* __restrict__ stk, Ctr& c, int wcap = WSTACK, int* tq = nullptr,
+                                             const float4* top = nullptr) {
     const RayPre p = ray_pre(o, d);
     const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
     int sp = 0;
-    WNode N = wload(W, 0);
+    WNode N = wload(W, 0, top);
     for (;;) {
         unsigned nh, th, imask, nl;
         int cb, tb;
@@ -652,7 +670,7 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
         // the next node's loads go out before this node's triangle tests, unconditionally (a walk that has ended
         // reloads the root): a load under a branch is copied into the merged register right after it, and that
         // copy waits for the load (dragon 0.712 -> 0.689 ms per frame, sportscar 0.931 -> 0.901, car_boxed 0.870 -> 0.858)
-        N = wload(W, next >= 0 ? next : 0);
+        N = wload(W, next >= 0 ? next : 0, top);
         if constexpr (TQ) {
             if (__builtin_amdgcn_readfirstlane((int)(__ballot(__builtin_popcount(th) >= TQ_MIN) != 0ull)) &&
                 closest_tris_packed<COUNT>(W, o, d, th, tb, best, hp, nd, tie, tq, c))
@@ -718,13 +736,13 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
 
 template <bool COUNT, bool PIPE = false, bool PK = false, bool TQ = false>
 __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c,
-                                             int wcap = WSTACK, int* tq = nullptr) {
+                                             int wcap = WSTACK, int* tq = nullptr, const float4* top = nullptr) {
     const RayPre p = ray_pre(o, d);
     const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
     float best = FMAX;
     const float reach = shadow_reach(o, ld2);
     int sp = 0;
-    WNode N = wload(W, 0);
+    WNode N = wload(W, 0, top);
     for (;;) {
         unsigned nh, th, imask, nl;
         int cb, tb;
@@ -736,7 +754,7 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
             count_step(c, true);
         }
         const int next = wide_next<PK>(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
-        N = wload(W, next >= 0 ? next : 0);  // unconditional (closest_wide)
+        N = wload(W, next >= 0 ? next : 0, top);  // unconditional (closest_wide)
         if constexpr (TQ) {
             bool occ = false;
             if (__builtin_amdgcn_readfirstlane((int)(__ballot(__builtin_popcount(th) >= TQ_MIN) != 0ull)) &&
@@ -821,7 +839,7 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
     if (!STRICT && !degenerate(d)) {
         if (s.wide.nodes) {
             const DWide& W = wide_for(s, unit);
-            closest_wide<COUNT, PIPE, PK, TQ>(W, o, d, best, hp, nd, tie, stk, c, wcap, tq);
+            closest_wide<COUNT, PIPE, PK, TQ>(W, o, d, best, hp, nd, tie, stk, c, wcap, tq, c.top[unit ? 1 : 0]);
             if (!tie) return hp >= 0 ? W.tri_orig[hp] : -1;
         } else {
             closest_walk<false, COUNT, REG>(s.acc, o, d, best, hp, nd, tie, bstk, c);
@@ -844,7 +862,7 @@ __device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, 
     int* __restrict__ bstk = sstk ? sstk : stk;
     if (!STRICT && !degenerate(d)) {
         if (s.wide.nodes)  // |d| = 1
-            return visible_wide<COUNT, PIPE, PK, TQ>(wide_for(s, true), o, d, ld2, stk, c, wcap, tq);
+            return visible_wide<COUNT, PIPE, PK, TQ>(wide_for(s, true), o, d, ld2, stk, c, wcap, tq, c.top[1]);
         return visible_walk<false, COUNT, REG>(s.acc, o, d, ld2, bstk, c);
     }
     if (!STRICT) CTR_INC(c, fb, C_FALLBACK);
@@ -1319,6 +1337,21 @@ void k_persist(KArgs A) {
         c.hist = hist_lds<true>();
         if (threadIdx.x < 32) c.hist[threadIdx.x] = 0u;
         __syncthreads();
+    }
+    if constexpr (LDS_TOP) {  // the top nodes of the primary and the unit-direction views (wide_for's choices)
+        if (A.s.wide.nodes) {
+            float4* t = top_lds<true>();
+            const DWide& P = A.s.prim.nodes ? A.s.prim : A.s.wide;
+            const DWide& U = A.s.unit.nodes ? A.s.unit : A.s.wide;
+            for (int i = threadIdx.x; i < 2 * NTOP * 5; i += BLOCK) {
+                const DWide& W = i < NTOP * 5 ? P : U;
+                const int r = i % (NTOP * 5);
+                if (r < 5 * W.n) t[i] = W.nodes[r];
+            }
+            __syncthreads();
+            c.top[0] = t;
+            c.top[1] = t + NTOP * 5;
+        }
     }
     constexpr bool EVM = !COUNT && !TRACE;  // (the tile trace reads the per-lane fallback counts)
     if constexpr (EVM) {

@@ -169,7 +169,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
                     best = FMAX;
                     reach = shadow_reach(o, ld2);
                     sp = 0;
-                    N = wload(W, 0);
+                    N = wload(W, 0, c.top[1]);
                     busy = true;
                 }
             }
@@ -191,7 +191,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
                     count_step(c, true);
                 }
                 next = wide_next<true>(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
-                N = wload(W, next >= 0 ? next : 0);  // unconditional (closest_wide)
+                N = wload(W, next >= 0 ? next : 0, c.top[1]);  // unconditional (closest_wide)
             }
             bool occ = false, seq = true;
             if constexpr (TQ) {
