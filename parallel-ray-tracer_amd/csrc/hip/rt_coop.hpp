@@ -102,12 +102,13 @@ __device__ __forceinline__ void wide_node_g(const WNode& nd, const RayPre& p, un
         const unsigned nxw = bx ? hxw[h] : lxw[h], fxw = bx ? lxw[h] : hxw[h];
         const unsigned nyw = by ? hyw[h] : lyw[h], fyw = by ? lyw[h] : hyw[h];
         const unsigned nzw = bz ? hzw[h] : lzw[h], fzw = bz ? lzw[h] : hzw[h];
-        const float tnx = __builtin_fmaf((float)((nxw >> sh) & 0xFFu), kx, ax);
-        const float tfx = __builtin_fmaf((float)((fxw >> sh) & 0xFFu), kx, ax);
-        const float tny = __builtin_fmaf((float)((nyw >> sh) & 0xFFu), ky, ay);
-        const float tfy = __builtin_fmaf((float)((fyw >> sh) & 0xFFu), ky, ay);
-        const float tnz = __builtin_fmaf((float)((nzw >> sh) & 0xFFu), kz, az);
-        const float tfz = __builtin_fmaf((float)((fzw >> sh) & 0xFFu), kz, az);
+        // (plane = 2^e * (QBIAS + q) + p: QBIAS + q is exact in float, the FMA rounds once, as wide_node's fma_mix)
+        const float tnx = __builtin_fmaf((float)(QBIAS + ((nxw >> sh) & 0xFFu)), kx, ax);
+        const float tfx = __builtin_fmaf((float)(QBIAS + ((fxw >> sh) & 0xFFu)), kx, ax);
+        const float tny = __builtin_fmaf((float)(QBIAS + ((nyw >> sh) & 0xFFu)), ky, ay);
+        const float tfy = __builtin_fmaf((float)(QBIAS + ((fyw >> sh) & 0xFFu)), ky, ay);
+        const float tnz = __builtin_fmaf((float)(QBIAS + ((nzw >> sh) & 0xFFu)), kz, az);
+        const float tfz = __builtin_fmaf((float)(QBIAS + ((fzw >> sh) & 0xFFu)), kz, az);
         const float lo = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, BOX_TMIN));
         const float hi = fminf(fminf(tfx, tfy), fminf(tfz, lim));
         hit |= lo <= hi ? (1u << s) : 0u;

@@ -380,7 +380,42 @@ __device__ __forceinline__ void count_step(Ctr& c, bool shadow) {
     if (c.hist && f) atomicAdd(c.hist + (shadow ? 16u : 0u) + 4u * (c.lvl < 3u ? c.lvl : 3u) + b, 1u);
 }
 
-__device__ __forceinline__ float ubyte(unsigned w, int b) { return (float)((w >> (8 * b)) & 0xFFu); }
+// Plane decoding (rt_wide.cpp): plane = fmaf(2^e, QBIAS + q, p). QBIAS + q is an f16 integer with the bits
+// 0x6400 | q, so one v_perm_b32 makes two of them from two plane bytes of a node word (the constant bytes 0x64 from
+// its second source), and v_fma_mix_f32 converts a half inside the FMA: t = (QBIAS + q) * k + a with the product
+// exact and one rounding -- fmaf((float)(QBIAS + q), k, a) bit for bit (checked exhaustively over q and 2^31 (k, a)
+// pairs incl. specials on the GPU, tools/mix/mix_check.hip). Per node visit: 24 perms + 48 FMAs instead of 48 byte
+// conversions + 48 FMAs.
+constexpr unsigned QBIAS = 1024u;
+__device__ __forceinline__ unsigned plane_pair(unsigned w, int pair) {  // bytes 2 pair, 2 pair + 1 -> two f16 halves
+    return __builtin_amdgcn_perm(w, 0x64646464u, pair ? 0x00070006u : 0x00050004u);
+}
+__device__ __forceinline__ float max_raw(float a, float b) {
+    float r;
+    __asm__("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float min_raw(float a, float b) {
+    float r;
+    __asm__("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+    float r;
+    __asm__("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float min3_raw(float a, float b, float c) {
+    float r;
+    __asm__("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float fma_half(unsigned h2, int hi, float k, float a) {  // fmaf(f16 half of h2, k, a)
+    float r;
+    if (hi) __asm__("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h2), "v"(k), "v"(a));
+    else __asm__("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h2), "v"(k), "v"(a));
+    return r;
+}
 
 // Tests the 8 children of wide node `node`: nh = hit interior slots as bits (s ^ oct), th = triangle
 // bits (relative to tbase) of every hit leaf slot.
@@ -409,7 +444,7 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
     tbase = __float_as_int(f1.y);
     const unsigned m[2] = {__float_as_uint(f1.z), __float_as_uint(f1.w)};
     // The ray in the node's grid: plane q of axis x is entered at t = fma(q, 2^ex / d.x, (p.x - o.x) / d.x),
-    // computed as fma(q, kx, ax) with kx = 2^ex * (1/d.x) (exact: power-of-two scale) and
+    // computed as fma(1024 + q, kx, ax) (fma_half) with kx = 2^ex * (1/d.x) (exact: power-of-two scale) and
     // ax = fma(p.x, 1/d.x, -o.x/d.x): one FMA per plane. Its rounding reach (a few ulp of max|coord| / |d|)
     // is covered >= 20x by the boxes' inflation (2^-16 max|coord|, rt_hip.hip).
     const float ax = __builtin_fmaf(f0.x, p.ix, -p.ox), ay = __builtin_fmaf(f0.y, p.iy, -p.oy),
@@ -423,18 +458,20 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
     unsigned hit8 = 0;  // bit s: child slot s entered within [0, lim]
 #pragma unroll
     for (int s = 0; s < 8; s++) {
-        const int h = s >> 2, b = s & 3;
-        const float tnx = __builtin_fmaf(ubyte(bx ? hx[h] : lx[h], b), kx, ax);
-        const float tfx = __builtin_fmaf(ubyte(bx ? lx[h] : hx[h], b), kx, ax);
-        const float tny = __builtin_fmaf(ubyte(by ? hy[h] : ly[h], b), ky, ay);
-        const float tfy = __builtin_fmaf(ubyte(by ? ly[h] : hy[h], b), ky, ay);
-        const float tnz = __builtin_fmaf(ubyte(bz ? hz[h] : lz[h], b), kz, az);
-        const float tfz = __builtin_fmaf(ubyte(bz ? lz[h] : hz[h], b), kz, az);
+        const int h = s >> 2, pr = (s >> 1) & 1, hb = s & 1;
+        const float tnx = fma_half(plane_pair(bx ? hx[h] : lx[h], pr), hb, kx, ax);
+        const float tfx = fma_half(plane_pair(bx ? lx[h] : hx[h], pr), hb, kx, ax);
+        const float tny = fma_half(plane_pair(by ? hy[h] : ly[h], pr), hb, ky, ay);
+        const float tfy = fma_half(plane_pair(by ? ly[h] : hy[h], pr), hb, ky, ay);
+        const float tnz = fma_half(plane_pair(bz ? hz[h] : lz[h], pr), hb, kz, az);
+        const float tfz = fma_half(plane_pair(bz ? lz[h] : hz[h], pr), hb, kz, az);
         // Inflation (2^-16 max|coord|) puts every computed near plane strictly before and every far plane
         // strictly after the child's true box, per axis, so the interval below contains the true one; the
         // folded test max(tmin, BOX_TMIN) <= min(tmax, lim) only adds visits: conservative (BOX_TMIN below).
-        const float lo = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, BOX_TMIN));
-        const float hi = fminf(fminf(tfx, tfy), fminf(tfz, lim));
+        // (max3 / min3 of the asm results directly: fmaxf / fminf would first canonicalise each asm output, one
+        // v_max_f32 per plane; the entries are never NaN here -- zero direction components walk strictly)
+        const float lo = max3_raw(tnx, tny, max_raw(tnz, BOX_TMIN));
+        const float hi = min3_raw(tfx, tfy, min_raw(tfz, lim));
         hit8 |= lo <= hi ? (1u << s) : 0u;
     }
     // interior hits, permuted into visiting order: bit k = slot k ^ oct (XOR by oct swaps bits, pairs and

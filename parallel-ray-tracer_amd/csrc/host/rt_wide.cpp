@@ -205,7 +205,18 @@ struct WBuilder {
     }
 };
 
-inline float fma_decode(float scale, int q, float p) { return std::fmaf(scale, (float)q, p); }
+// A plane is decoded as fmaf(2^e, QBIAS + q, p): QBIAS + q (1024 .. 1279) is an f16 integer whose bits are 0x6400 | q,
+// so the device forms two such halves from two plane bytes with one v_perm_b32 and feeds them to v_fma_mix_f32, which
+// converts the half exactly inside the FMA (rt_kernels.hpp wide_node): one perm per two planes instead of a byte
+// conversion per plane, the same single rounding. The grid's origin p therefore lies QBIAS steps below the node.
+constexpr int QBIAS = 1024;
+inline float fma_decode(float scale, int q, float p) { return std::fmaf(scale, (float)(QBIAS + q), p); }
+// the largest float <= x
+inline float round_down(double x) {
+    float f = (float)x;
+    if ((double)f > x) f = std::nextafter(f, -INFINITY);
+    return f;
+}
 
 inline uint32_t f2u(float f) {
     uint32_t u;
@@ -213,33 +224,33 @@ inline uint32_t f2u(float f) {
     return u;
 }
 
-// Quantise one axis of up to 8 child boxes (already grown) on the grid p + 2^e * q, q in 0..255.
-// Returns the biased exponent byte (e + 127); qlo/qhi receive the planes.
-int quantise_axis(const float* lo, const float* hi, int k, float& p, int* qlo, int* qhi) {
-    p = INFINITY;
-    float top = -INFINITY;
+// Quantise one axis of up to 8 child boxes (already grown) on the grid pb + 2^e * (QBIAS + q), q in 0..255.
+// Returns the biased exponent byte (e + 127); pb receives the grid's origin, qlo/qhi the planes.
+int quantise_axis(const float* lo, const float* hi, int k, float& pb, int* qlo, int* qhi) {
+    float p = INFINITY, top = -INFINITY;
     for (int c = 0; c < k; c++) {
         p = std::min(p, lo[c]);
         top = std::max(top, hi[c]);
     }
     const double ext = (double)top - (double)p;
     int e = ext > 0 ? (int)std::ceil(std::log2(ext / 255.0)) : -126;
-    e = std::max(-126, std::min(e, 120));
+    e = std::max(-126, std::min(e, 100));  // (QBIAS * 2^e stays finite)
     for (;; e++) {
         const float scale = std::ldexp(1.0f, e);
+        pb = round_down((double)p - (double)QBIAS * scale);  // q = 0 decodes to the lowest plane or below it
         bool ok = true;
         for (int c = 0; c < k && ok; c++) {
-            int a = (int)std::floor(((double)lo[c] - (double)p) / scale);
+            int a = (int)std::floor(((double)lo[c] - (double)pb) / scale) - QBIAS;
             a = std::max(0, std::min(a, 255));
-            while (a > 0 && fma_decode(scale, a, p) > lo[c]) a--;
-            int b = (int)std::ceil(((double)hi[c] - (double)p) / scale);
+            while (a > 0 && fma_decode(scale, a, pb) > lo[c]) a--;
+            int b = (int)std::ceil(((double)hi[c] - (double)pb) / scale) - QBIAS;
             b = std::max(0, b);
-            while (b <= 255 && fma_decode(scale, b, p) < hi[c]) b++;
-            if (b > 255 || fma_decode(scale, a, p) > lo[c]) ok = false;
+            while (b <= 255 && fma_decode(scale, b, pb) < hi[c]) b++;
+            if (b > 255 || fma_decode(scale, a, pb) > lo[c]) ok = false;
             qlo[c] = a;
             qhi[c] = b;
         }
-        if (ok || e >= 126) return e + 127;
+        if (ok || e >= 110) return e + 127;
     }
 }
 

@@ -140,7 +140,8 @@ def wbvh_build(nodes, tri_idx, tris, inflate=0.0):
 
 def wbvh_decode(words):
     """decoded view of wide nodes: p [N,3] f32, scale [N,3] f32, imask [N], child_base [N], tri_base [N],
-    meta [N,8] u8, qlo/qhi [N,3,8] u8 and the decoded child boxes lo/hi [N,8,3] (fmaf(scale, q, p))"""
+    meta [N,8] u8, qlo/qhi [N,3,8] u8 and the decoded child boxes lo/hi [N,8,3] (fmaf(scale, 1024 + q, p): the planes'
+    f16-ready bias, rt_wide.cpp QBIAS)"""
     w = np.ascontiguousarray(words, dtype=np.uint32)
     p = w[:, 0:3].view(np.float32)
     e = np.stack([(w[:, 3] >> (8 * a)) & 0xFF for a in range(3)], 1).astype(np.int64)
@@ -149,9 +150,9 @@ def wbvh_decode(words):
     meta = w[:, 6:8].copy().view(np.uint8).reshape(-1, 8)
     q = w[:, 8:20].copy().view(np.uint8).reshape(-1, 6, 8)
     qlo, qhi = q[:, 0:3], q[:, 3:6]
-    # fmaf(scale, q, p) == p + scale * q rounded once (the product is exact): evaluate in f64, round to f32
-    lo = (p[:, :, None].astype(np.float64) + scale[:, :, None].astype(np.float64) * qlo).astype(np.float32)
-    hi = (p[:, :, None].astype(np.float64) + scale[:, :, None].astype(np.float64) * qhi).astype(np.float32)
+    # fmaf(scale, 1024 + q, p) == p + scale * (1024 + q) rounded once (the product is exact): evaluate in f64, round
+    lo = (p[:, :, None].astype(np.float64) + scale[:, :, None].astype(np.float64) * (1024.0 + qlo)).astype(np.float32)
+    hi = (p[:, :, None].astype(np.float64) + scale[:, :, None].astype(np.float64) * (1024.0 + qhi)).astype(np.float32)
     return {"p": p, "scale": scale, "imask": imask, "child_base": w[:, 4].astype(np.int64),
             "tri_base": w[:, 5].astype(np.int64), "meta": meta, "qlo": qlo, "qhi": qhi,
             "lo": lo.transpose(0, 2, 1), "hi": hi.transpose(0, 2, 1)}
