@@ -541,6 +541,13 @@ __device__ __forceinline__ int wide_next(unsigned nh, int cb, unsigned imask, un
 // than TQ_MAX_TRIS triangles; the host (rt_hip.hip persist_kernel, shp_ok) runs the builds without TQ for larger ones.
 constexpr int TQ_CAP = 128;
 constexpr int TQ_MAX_TRIS = 1 << 26;
+// The shadow walks' triangle tests with the exact reciprocal (rcp_ieee, bit-identical to the IEEE division): same box,
+// 20-frame batches, dragon 0.559 -> 0.556 ms per frame, car_boxed 0.811 -> 0.807, sportscar 0.838 -> 0.831
+// (profiles/r5e; round 4 had measured the opposite on a kernel that spilled)
+#ifndef PRT_SHADOW_RCP
+#define PRT_SHADOW_RCP 1
+#endif
+constexpr bool SHADOW_RCP = PRT_SHADOW_RCP != 0;
 static_assert(TQ_MAX_TRIS == 0x3FFFFFF + 1 && 63u << 26 >> 26 == 63u, "job = owner lane (6 bits) << 26 | triangle");
 constexpr int TQ_OCC = TQ_CAP, TQ_T = TQ_CAP + 64, TQ_CNT = TQ_CAP + 128, TQ_WORDS = TQ_CAP + 132;
 // the waves' queues of a kernel without dynamic LDS (the 3-wave k_persist): a static array
@@ -662,7 +669,7 @@ __device__ __forceinline__ bool shadow_tris_packed(const DWide& W, v3 o, v3 d, f
     if (has) {
         PRT_TRI_ITER(c, q2);
         int k;
-        const float tt = hit_triangle(oo, dd, W.tris + 3 * (int)(job & 0x3FFFFFFu), k);
+        const float tt = hit_triangle<SHADOW_RCP>(oo, dd, W.tris + 3 * (int)(job & 0x3FFFFFFu), k);
         if (COUNT) c.sht++;
         if (tt < FMAX) {
             const v3 q = add(oo, mul(dd, tt));
@@ -806,7 +813,7 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
                 const int i = tb + __builtin_ctz(th);
                 th &= th - 1u;
                 int k;
-                const float tt = hit_triangle(o, d, W.tris + 3 * i, k);
+                const float tt = hit_triangle<SHADOW_RCP>(o, d, W.tris + 3 * i, k);
                 if (COUNT) c.sht++;
                 if (tt < best) {
                     best = tt;

@@ -216,7 +216,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
                             if (j < T) {
                                 PRT_TRI_ITER(c, q2);
                                 int k;
-                                const float tt = hit_triangle(oo, dd, W.tris + 3 * (int)(job & 0x3FFFFFFu), k);
+                                const float tt = hit_triangle<SHADOW_RCP>(oo, dd, W.tris + 3 * (int)(job & 0x3FFFFFFu), k);
                                 if (COUNT) c.sht++;
                                 if (tt < FMAX) {
                                     const v3 q = add(oo, mul(dd, tt));
@@ -244,7 +244,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
                     const int i = tb + __builtin_ctz(th);
                     th &= th - 1u;
                     int k;
-                    const float tt = hit_triangle(o, d, W.tris + 3 * i, k);
+                    const float tt = hit_triangle<SHADOW_RCP>(o, d, W.tris + 3 * i, k);
                     if (COUNT) c.sht++;
                     if (tt < best) {
                         best = tt;
