@@ -10,6 +10,7 @@
 #include <type_traits>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -1155,6 +1156,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     HIPC(hipSetDevice(ctx->device));
     const size_t pixels = (size_t)f->width * f->n_rows;  // per frame
     const size_t all_px = pixels * (size_t)n_frames;
+    if (all_px > (size_t)INT_MAX)  // (the kernels index a launch's output pixels with 32-bit integers)
+        return arg_err(ctx, "rt_render: the launch's frames x pixels exceed 2^31 - 1");
     float* rgb = out ? out->rgb : nullptr;
     unsigned* bgra = out ? out->bgra : nullptr;
     if (!rgb && !bgra) {  // a quantised-only frame writes no f32 pixels at all

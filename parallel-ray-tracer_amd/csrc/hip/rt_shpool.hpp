@@ -271,6 +271,17 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
+// A per-pixel output index as the compiler cannot see through (OPAQUE_OUT): the 64-bit output addresses formed from it
+// are made where they are stored instead of once per pixel and held -- or spilled -- across the path's walks (the
+// per-level pool kernel spilled three of them: 24 B per lane, stored per pixel).
+#ifndef PRT_OPAQUE_OUT
+#define PRT_OPAQUE_OUT 1
+#endif
+__device__ __forceinline__ int opaque(int v) {
+    if (PRT_OPAQUE_OUT) __asm__ volatile("" : "+v"(v));
+    return v;
+}
+
 // trace_path (rt_kernels.hpp) with each level's shadow rays walked by shadow_pool: the path loop runs in step over
 // the wave (a lane whose path has ended, or that holds no pixel, stays in it as a shadow worker) and a level's
 // colour is formed after the pool with path_step's expressions in the reference's order. Path levels in the LDS
@@ -306,11 +317,12 @@ __device__ __forceinline__ v3 trace_path_shp(const KArgs& A, bool alive, v3 o, v
             int nd;
             const int orig = closest<false, COUNT, true, false, true, true>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0, tq);
             if (hpix >= 0) {
+                const int h = opaque(hpix);  // (the outputs' addresses formed here, not hoisted and held: OPAQUE_OUT)
                 if (it == 0) {
-                    if (A.hit) A.hit[hpix] = orig;
-                    if (A.t) A.t[hpix] = best;
+                    if (A.hit) A.hit[h] = orig;
+                    if (A.t) A.t[h] = best;
                 }
-                if (A.bounce_hit) A.bounce_hit[(size_t)hpix * A.bounces + it] = orig;
+                if (A.bounce_hit) A.bounce_hit[(size_t)h * A.bounces + it] = orig;
             }
             if (orig < 0) {  // raytracer.c:132-135
                 pb[it * 64] = make_float4(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z, __int_as_float(0));
@@ -432,11 +444,12 @@ __device__ __forceinline__ v3 trace_path_dfr(const KArgs& A, bool alive, v3 o, v
             const int orig =
                 closest<false, COUNT, true, false, true, true>(s, o, d, best, nd, stk, c, sstk, wcap, it > 0, tq);
             if (hpix >= 0) {
+                const int h = opaque(hpix);  // (the outputs' addresses formed here, not hoisted and held: OPAQUE_OUT)
                 if (it == 0) {
-                    if (A.hit) A.hit[hpix] = orig;
-                    if (A.t) A.t[hpix] = best;
+                    if (A.hit) A.hit[h] = orig;
+                    if (A.t) A.t[h] = best;
                 }
-                if (A.bounce_hit) A.bounce_hit[(size_t)hpix * A.bounces + it] = orig;
+                if (A.bounce_hit) A.bounce_hit[(size_t)h * A.bounces + it] = orig;
             }
             if (orig < 0) {  // raytracer.c:132-135 (the colour is written by the shading loop below)
                 hid[it * 64] = -1;
@@ -546,9 +559,9 @@ __device__ __forceinline__ void render_pixel_shp(const KArgs& A, const Cam& C, i
         for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
     }
     if constexpr (SPP1) {  // (the host runs the SPP1 builds for spp = 1, the others for spp > 1 only)
-        const size_t o = (size_t)frame * A.frame_px + (size_t)k * A.W + x;
-        const v3 col = clamp01(trace(primary_dir(C, (float)x, (float)y), valid ? (int)o : -1));
-        if (valid) store_px(A.rgb, A.bgra, o, col);
+        const int o = (int)((size_t)frame * A.frame_px + (size_t)k * A.W + x);  // (< 2^31: rt_render's output bound)
+        const v3 col = clamp01(trace(primary_dir(C, (float)x, (float)y), valid ? o : -1));
+        if (valid) store_px(A.rgb, A.bgra, (size_t)opaque(o), col);
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples; hit / t from the first sample
         // The lane's A.lanebuf slot carries the running sum and the pixel (x, compact row k) from sample to sample, so
         // that no register stays live across a sample's path (spp_slot; the host guarantees W, n_rows <= 65535)
