@@ -107,13 +107,17 @@ struct KArgs {
     // pixel's running sum of clamped samples across the sample loop, so that no register stays live across a sample's
     // path (at the 4-wave kernels' 128-VGPR cap such values spilled inside the walks)
     float4* lanebuf;
+    // spp > 1 in the kernels with an LDS path buffer (PB = 2): the same slots in dynamic LDS instead, [wave][lane] from
+    // int offset slot_off (the host appends them to the launch's LDS layout), so that the per-sample sums never leave
+    // the CU (64 spp at 4K: 530 M slot updates per frame)
+    int slot_off;
 };
 
 // Kernel arguments are laid out by the host compiler and read by the device compiler: both passes must
 // agree on every offset (an LDS pointer, 32-bit on gfx950 but 64-bit on the host, once shifted every
 // later field and hung a kernel). Pinned sizes catch such drift at compile time in whichever pass
 // disagrees; never put address-space-qualified pointers in these structs.
-static_assert(sizeof(DWide) == 32 && sizeof(DScene) == 216 && sizeof(KArgs) == 448,
+static_assert(sizeof(DWide) == 32 && sizeof(DScene) == 216 && sizeof(KArgs) == 456,
               "kernel-argument layout changed: update the pinned sizes only after checking both passes agree");
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

@@ -930,13 +930,23 @@ KFn persist4(bool pbl, bool spp1, bool count) {
     return nullptr;
 }
 
+// the spp > 1 sample-sum slots of an LDS-path-buffer launch (one float4 per lane, after the rest of its layout)
+size_t slot_bytes(const rtd::KArgs& A) { return A.spp > 1 ? sizeof(float4) * rtd::BLOCK : 0; }
+// the kernel arguments of a launch with `dyn` bytes of dynamic LDS: its slots' offset (ints) when it has them
+rtd::KArgs with_slots(const rtd::KArgs& A, size_t dyn) {
+    rtd::KArgs B = A;
+    B.slot_off = dyn && slot_bytes(A) ? (int)((dyn - slot_bytes(A)) / sizeof(int)) : -1;
+    return B;
+}
+
 // dynamic LDS of the 4-wave kernels' LDS layout: the wide stack sized to the scene's wide depth, then the path levels
 // (and, for the all-levels pool, each level's hit triangle)
+// (and, for spp > 1, the lanes' sample-sum slots at the end: rtd::KArgs::slot_off)
 template <int MAXB>
 size_t pbl_bytes(const rtd::KArgs& A, int shp = 0) {
     return sizeof(int) * (size_t)rtd::wstack_words(A.wcap, shp > 0) * rtd::BLOCK + sizeof(float4) * rtd::BLOCK * MAXB +
            (shp == 2 ? sizeof(int) * (rtd::BLOCK * MAXB + rtd::BLOCK / 64 * rtd::TQ_WORDS) : 0) +
-           (shp == 1 || shp == 3 ? sizeof(int) * (rtd::BLOCK / 64 * rtd::TQ_WORDS) : 0);
+           (shp == 1 || shp == 3 ? sizeof(int) * (rtd::BLOCK / 64 * rtd::TQ_WORDS) : 0) + slot_bytes(A);
 }
 // Does that layout fit 4 workgroups per CU for this scene? (the LDS path buffer measured 1.2 % faster than the global
 // slab on dragon, 2.3 % on car_boxed; the shadow pool needs it)
@@ -1009,7 +1019,7 @@ void launch_paths(const rtd::KArgs& A, int variant, bool count, int device, hipS
     size_t dyn = 0;
     const KFn k = persist_kernel<MAXB>(A, variant, count, device, dyn, pk_ok, tq_ok);
     const int blocks = std::max(1, std::min(resident(k, device, cap > 0 ? cap : 8, dyn), (A.n_tiles * A.n_frames + 3) / 4));
-    k<<<blocks, rtd::BLOCK, dyn, s>>>(A);
+    k<<<blocks, rtd::BLOCK, dyn, s>>>(with_slots(A, dyn));
 }
 
 rtd::DBvh dview(const DevView& v) { return rtd::DBvh{v.nodes, v.leaves, v.tris, v.orig, v.root}; }
@@ -1878,7 +1888,7 @@ int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c) {
     const int nc = n_hot > 0 ? std::max(1, std::min((n_hot + 3) / 4, rcp / 2)) : 0;
     const int np = std::max(1, std::min(rp - (int)((long long)nc * rp / rcp), (n_cold + 3) / 4));
     if (n_hot == 0) {  // (a whole frame in the measured order)
-        if (n_cold > 0) kp<<<np, rtd::BLOCK, dyn, ctx->stream>>>(P);
+        if (n_cold > 0) kp<<<np, rtd::BLOCK, dyn, ctx->stream>>>(with_slots(P, dyn));
         HIPC(hipGetLastError());
         return RT_OK;
     }
@@ -1886,7 +1896,7 @@ int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c) {
     HIPC(hipStreamWaitEvent(h.s2, h.fork, 0));
     if (n_hot > 0) kc<<<nc, rtd::BLOCK, 0, h.s2>>>(B);
     HIPC(hipGetLastError());
-    if (n_cold > 0) kp<<<np, rtd::BLOCK, dyn, ctx->stream>>>(P);
+    if (n_cold > 0) kp<<<np, rtd::BLOCK, dyn, ctx->stream>>>(with_slots(P, dyn));
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(h.join, h.s2));
     HIPC(hipStreamWaitEvent(ctx->stream, h.join, 0));

@@ -165,6 +165,17 @@ __device__ __forceinline__ bool visit(float t, float best) {
     return t <= best * PRUNE_SLACK && t != FMAX;
 }
 
+// A per-pixel output index as the compiler cannot see through (OPAQUE_OUT): the 64-bit output addresses formed from it
+// are made where they are stored instead of once per pixel and held -- or spilled -- across the path's walks (the
+// per-level pool kernel spilled three of them, 24 B per lane stored per pixel; the packed spp > 1 build one per sample).
+#ifndef PRT_OPAQUE_OUT
+#define PRT_OPAQUE_OUT 1
+#endif
+__device__ __forceinline__ int opaque(int v) {
+    if (PRT_OPAQUE_OUT) __asm__ volatile("" : "+v"(v));
+    return v;
+}
+
 // ---------------------------------------------------------------- closest hit
 // bvh_traverse, cpu/src/bvh.c:317-358. Stack of node refs in LDS, [depth][lane] so that the 64 lanes
 // of a wave always hit 64 distinct banks whatever their stack depths.
@@ -977,7 +988,7 @@ __device__ __forceinline__ bool path_step(const DScene& s, int bounces, int it, 
         hit0 = orig;
         t0 = best;
     }
-    if (bh && bh_pix >= 0) bh[(size_t)bh_pix * bounces + it] = orig;  // per-level dump (uniform base, nullable)
+    if (bh && bh_pix >= 0) bh[(size_t)opaque(bh_pix) * bounces + it] = orig;  // per-level dump (uniform base, nullable)
     if (orig < 0) {  // raytracer.c:132-135
         if constexpr (PB) pb[it * 64] = make_float4(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z, __int_as_float(0));
         else set3<MAXB>(cols, it, mk(0.0f + amb.x, 0.0f + amb.y, 0.0f + amb.z));
@@ -1193,9 +1204,15 @@ __device__ __forceinline__ unsigned lane_now() {
     return l;
 }
 // a lane's A.lanebuf slot ([block][lane]): the wave's slots from scalar registers, the lane's offset remade per use
+template <bool LDS = false>
 __device__ __forceinline__ float4* lane_slot(const KArgs& A) {
-    const unsigned wave = (unsigned)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6)));
-    return reinterpret_cast<float4*>(reinterpret_cast<char*>(A.lanebuf + (size_t)wave * 64) + lane_now() * 16u);
+    const unsigned wave = (unsigned)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if constexpr (LDS) {  // (the PB = 2 kernels: the launch's slots after its LDS layout, KArgs::slot_off)
+        extern __shared__ int lds_dyn[];
+        return reinterpret_cast<float4*>(lds_dyn + A.slot_off) + wave * 64u + lane_now();
+    }
+    const unsigned gw = (unsigned)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (BLOCK / 64))) + wave;
+    return reinterpret_cast<float4*>(reinterpret_cast<char*>(A.lanebuf + (size_t)gw * 64) + lane_now() * 16u);
 }
 
 // the shadow-pool kernels' pixel (rt_shpool.hpp, RT_VARIANT_SHPOOL): every lane of the wave calls it
@@ -1218,26 +1235,26 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
                                              int* __restrict__ sstk = nullptr, int wcap = WSTACK) {
     const int y = image_row(A, k, frame);
     if (y >= A.H) return;  // frame_shift: a rotated rank's compact rows past the image
-    const size_t o = (size_t)frame * A.frame_px + (size_t)k * A.W + x;
+    const int o = (int)((size_t)frame * A.frame_px + (size_t)k * A.W + x);  // (< 2^31: rt_render's bound)
     int hit0 = -1;
     float t0 = FMAX;
     v3 col;
     if (A.bounce_hit)
-        for (int i = 0; i < A.bounces; i++) A.bounce_hit[o * (size_t)A.bounces + i] = -2;
+        for (int i = 0; i < A.bounces; i++) A.bounce_hit[(size_t)o * A.bounces + i] = -2;
     if (SPPM == 1 || (SPPM == 0 && A.spp <= 1)) {
         col = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB, PK, TQ>(A, C.pos, primary_dir(C, (float)x, (float)y),
-                                                                          stk, c, hit0, t0, (int)o, q, sstk, wcap));
+                                                                          stk, c, hit0, t0, o, q, sstk, wcap));
     } else if (SPPM == 2) {  // stratified g x g sub-pixel grid, mean of clamped samples
         // the persistent kernels' multi-sample builds: the lane's A.lanebuf slot carries the running sum and the pixel
         // (x, compact row k) from sample to sample, so that no register stays live across a sample's path; hit / t of
         // the first sample are stored as soon as it returns (the host sets A.lanebuf for every k_persist launch and
         // guarantees W, n_rows <= 65535 for spp > 1)
         const int g = A.spp_grid;
-        *lane_slot(A) = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((unsigned)x | ((unsigned)k << 16)));
+        *lane_slot<PB == 2>(A) = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((unsigned)x | ((unsigned)k << 16)));
         v3 acc = mk(0.0f, 0.0f, 0.0f);
         for (int s = 0; s < g * g; ++s) {
             __asm__ volatile("" ::: "memory");  // (read the slot back: no value forwarded in registers across the path)
-            float4* lb = lane_slot(A);
+            float4* lb = lane_slot<PB == 2>(A);
             const float4 e = *lb;
             const unsigned px = __float_as_uint(e.w);
             const int xs = (int)(px & 0xFFFFu), ks = (int)(px >> 16), ys = image_row(A, ks, frame);
@@ -1250,7 +1267,7 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
             const v3 cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB, PK, TQ>(
                 A, C.pos, primary_dir_sample(C, fx, fy), stk, c, h, tt, s == 0 ? (int)os : -1, q, sstk, wcap));
             __asm__ volatile("" ::: "memory");
-            lb = lane_slot(A);
+            lb = lane_slot<PB == 2>(A);
             const float4 a = *lb;
             if (s == 0 && q == 0) {  // (the output index from the slot again, not held across the path)
                 const unsigned pa = __float_as_uint(a.w);
@@ -1264,7 +1281,10 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
         const float nn = (float)(g * g);
         CTR_INC(c, pix, C_PIX);
         if (q != 0) return;
-        store_px(A.rgb, A.bgra, o, mk(acc.x / nn, acc.y / nn, acc.z / nn));
+        __asm__ volatile("" ::: "memory");
+        const unsigned pf = __float_as_uint(lane_slot<PB == 2>(A)->w);  // (the pixel from the slot: nothing held across the loop)
+        store_px(A.rgb, A.bgra, (size_t)frame * A.frame_px + (size_t)(pf >> 16) * A.W + (pf & 0xFFFFu),
+                 mk(acc.x / nn, acc.y / nn, acc.z / nn));
         return;
     } else {  // stratified g x g sub-pixel grid, mean of clamped samples
         const int g = A.spp_grid;
@@ -1277,7 +1297,7 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
                 float tt;
                 v3 cs;
                 cs = clamp01(trace_path<MAXB, STRICT, COUNT, REG, G, PB, PK, TQ>(
-                        A, C.pos, primary_dir(C, fx, fy), stk, c, h, tt, si == 0 && sj == 0 ? (int)o : -1, q, sstk, wcap));
+                        A, C.pos, primary_dir(C, fx, fy), stk, c, h, tt, si == 0 && sj == 0 ? o : -1, q, sstk, wcap));
                 acc = add(acc, cs);
                 if (si == 0 && sj == 0) {
                     hit0 = h;
@@ -1289,9 +1309,10 @@ __device__ __forceinline__ void render_pixel(const KArgs& A, const Cam& C, int f
     }
     CTR_INC(c, pix, C_PIX);
     if (q != 0) return;  // a group's pixel is written once
-    store_px(A.rgb, A.bgra, o, col);
-    if (A.hit) A.hit[o] = hit0;
-    if (A.t) A.t[o] = t0;
+    const int oo = opaque(o);
+    store_px(A.rgb, A.bgra, (size_t)oo, col);
+    if (A.hit) A.hit[oo] = hit0;
+    if (A.t) A.t[oo] = t0;
 }
 
 // ---------------------------------------------------------------- kernels

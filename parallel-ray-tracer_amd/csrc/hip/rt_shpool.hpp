@@ -271,17 +271,6 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
-// A per-pixel output index as the compiler cannot see through (OPAQUE_OUT): the 64-bit output addresses formed from it
-// are made where they are stored instead of once per pixel and held -- or spilled -- across the path's walks (the
-// per-level pool kernel spilled three of them: 24 B per lane, stored per pixel).
-#ifndef PRT_OPAQUE_OUT
-#define PRT_OPAQUE_OUT 1
-#endif
-__device__ __forceinline__ int opaque(int v) {
-    if (PRT_OPAQUE_OUT) __asm__ volatile("" : "+v"(v));
-    return v;
-}
-
 // trace_path (rt_kernels.hpp) with each level's shadow rays walked by shadow_pool: the path loop runs in step over
 // the wave (a lane whose path has ended, or that holds no pixel, stays in it as a shadow worker) and a level's
 // colour is formed after the pool with path_step's expressions in the reference's order. Path levels in the LDS
@@ -566,11 +555,11 @@ __device__ __forceinline__ void render_pixel_shp(const KArgs& A, const Cam& C, i
         // The lane's A.lanebuf slot carries the running sum and the pixel (x, compact row k) from sample to sample, so
         // that no register stays live across a sample's path (spp_slot; the host guarantees W, n_rows <= 65535)
         const int g = A.spp_grid;
-        *lane_slot(A) = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((unsigned)x | ((unsigned)k << 16)));
+        *lane_slot<true>(A) = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((unsigned)x | ((unsigned)k << 16)));
         v3 acc = mk(0.0f, 0.0f, 0.0f);
         for (int s = 0; s < g * g; ++s) {
             __asm__ volatile("" ::: "memory");  // (read the slot back: no value forwarded in registers across the path)
-            float4* lb = lane_slot(A);
+            float4* lb = lane_slot<true>(A);
             const float4 e = *lb;
             const unsigned px = __float_as_uint(e.w);
             const int xs = (int)(px & 0xFFFFu), ks = (int)(px >> 16), ys = image_row(A, ks, frame);
@@ -580,14 +569,14 @@ __device__ __forceinline__ void render_pixel_shp(const KArgs& A, const Cam& C, i
             const int hp = s == 0 && valid ? (int)((size_t)frame * A.frame_px + (size_t)ks * A.W + xs) : -1;
             const v3 cs = clamp01(trace(primary_dir_sample(C, fx, fy), hp));
             __asm__ volatile("" ::: "memory");
-            lb = lane_slot(A);
+            lb = lane_slot<true>(A);
             const float4 a = *lb;
             acc = add(mk(a.x, a.y, a.z), cs);
             *lb = make_float4(acc.x, acc.y, acc.z, a.w);
         }
         const float nn = (float)(g * g);
         __asm__ volatile("" ::: "memory");
-        const unsigned px = __float_as_uint(lane_slot(A)->w);  // (the pixel from the slot: nothing of it live across the loop)
+        const unsigned px = __float_as_uint(lane_slot<true>(A)->w);  // (the pixel from the slot: nothing of it live across the loop)
         const size_t o = (size_t)frame * A.frame_px + (size_t)(px >> 16) * A.W + (px & 0xFFFFu);
         if (valid) store_px(A.rgb, A.bgra, o, mk(acc.x / nn, acc.y / nn, acc.z / nn));
     }
