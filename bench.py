@@ -559,7 +559,7 @@ def main():
     nan = float("nan")
     if not args.no_latency:
         sd = seam(lambda i: cam, n_after=72)
-        sw = seam(walk)
+        sw = seam(walk, n_after=16)
         sf = seam(lambda i, k=sw["mid_camera"]: walk(k))
     else:
         sd = sw = sf = {"median": nan, "mean": nan, "settle": None, "info": None, "mid_camera": None, "refresh_ms": [],
@@ -643,6 +643,7 @@ def main():
             "frame_latency_ms": lat.item() if not args.no_latency else None,
             "frame_latency_detail": {"default_rule_ms": lat_default, "default_rule_mean_ms": sd["mean"],
                                      "refresh_frame_ms": sd["refresh_ms"], "walkthrough_ms": lat_walk,
+                                     "walkthrough_mean_ms": sw["mean"], "walkthrough_refresh_ms": sw["refresh_ms"],
                                      "fixed_at_walk_ms": sf["median"], "walk_mid_camera": sw["mid_camera"],
                                      "settle_frames": settle_frames, "settle_frames_walkthrough": settle_walk,
                                      "choice": seam_info,
@@ -651,8 +652,10 @@ def main():
                                              "time of the 72 frames after rt_get_launch_info reports the rule settled (its "
                                              "measuring and trial frames excluded; its periodic tile-list refresh, one "
                                              "settled measuring frame per 64, included: refresh_frame_ms, and in "
-                                             "default_rule_mean_ms), fixed reference camera; walkthrough_ms: the median of 9 "
-                                             "settled frames with the camera moved every frame; fixed_at_walk_ms: the fixed "
+                                             "default_rule_mean_ms), fixed reference camera; walkthrough_ms: the median of 16 "
+                                             "settled frames with the camera moved every frame (their mean, and the tile-list "
+                                             "refresh frames among them: walkthrough_mean_ms, walkthrough_refresh_ms); "
+                                             "fixed_at_walk_ms: the fixed "
                                              "camera placed at the walkthrough's middle measured camera (walk_mid_camera)"},
             "roofline": {**roof, "traffic": traffic,
                          "kernel_ms": k_avg_ms, "alg_bytes_per_launch": bytes_launch, "frames_per_launch": F,

@@ -437,6 +437,19 @@ def test_tune_is_the_default_rule_and_removed_variants_are_refused(dev, scenes):
     r.close()
 
 
+def test_launch_pixel_bound_is_refused(dev, scenes):
+    """the kernels index a launch's output pixels (frames x rows x width) with 32-bit integers: rt_render refuses a
+    launch of more than 2^31 - 1 pixels (RT_E_ARG) before it allocates or launches anything"""
+    r = dev.Renderer(0)
+    r.upload(scenes["car_boxed"])
+    W = H = 46341  # 2,147,488,281 pixels
+    fr = _frame_with(r, W, H, {})
+    rc = dev._L.rt_render(r._ctx, ctypes.byref(host.camera(W, H)), ctypes.byref(fr), ctypes.byref(dev.Outputs()))
+    msg = dev._L.rt_last_error(r._ctx).decode()
+    r.close()
+    assert rc == -1 and "2^31" in msg, (rc, msg)
+
+
 def _frame_with(r, W, H, f):
     """an rt_frame for the full W x H frame with raw launch fields (values the Python mirror would not produce)"""
     fr, _ = r._frame(W, H, None, 4, 1, "fast", 0, False, 0, "default", 0)
