@@ -26,6 +26,10 @@
 #include "rt_output.hpp"
 #include "rt_build.hpp"
 #include "rt_comm_logic.hpp"
+#include "rt_treelet.hpp"
+#ifndef PRT_TREELET
+#define PRT_TREELET 2  // treelet-restructuring passes over the GPU-built binary tree (0: none)
+#endif
 
 #include <chrono>
 #include <hipcub/hipcub.hpp>
@@ -522,6 +526,23 @@ int gpu_ploc(rt_ctx* ctx, const rt_triangle* T, int n, int R, std::vector<rt_bvh
     PLOC(hipMemcpyAsync(hhi.data(), nhi, sizeof(float4) * nn2, hipMemcpyDeviceToHost, st));
     PLOC(hipStreamSynchronize(st));
 #undef PLOC
+    if (PRT_TREELET > 0 && n >= 3) {  // treelet restructuring on the host (rt_treelet.hpp)
+        rtt::Tree T;
+        T.n = n;
+        T.root = root;
+        T.left.assign(hl.begin(), hl.begin() + ni);
+        T.right.assign(hr.begin(), hr.begin() + ni);
+        T.box.resize(2 * (size_t)n - 1);
+        for (size_t i = 0; i < T.box.size(); i++)
+            T.box[i] = rtt::Box{{hlo[i].x, hlo[i].y, hlo[i].z}, {hhi[i].x, hhi[i].y, hhi[i].z}};
+        for (int p = 0; p < PRT_TREELET; p++) rtt::optimize_pass(T);
+        std::copy(T.left.begin(), T.left.end(), hl.begin());
+        std::copy(T.right.begin(), T.right.end(), hr.begin());
+        for (size_t i = (size_t)n; i < T.box.size(); i++) {
+            hlo[i] = make_float4(T.box[i].lo[0], T.box[i].lo[1], T.box[i].lo[2], hlo[i].w);
+            hhi[i] = make_float4(T.box[i].hi[0], T.box[i].hi[1], T.box[i].hi[2], hhi[i].w);
+        }
+    }
     // reference layout, depth-first: children at consecutive indices, leaves numbered left to right
     out.clear();
     out.reserve(nn2);

@@ -35,5 +35,35 @@ def main():
         print(scene, v, " ".join(f"{m} {t:.3f}" for m, t in res.items()), flush=True)
 
 
+def stale(scene):
+    """the default rule settled on one camera (its lists measured there), then frames of cameras d walk steps away:
+    how fast the rule's per-tile knowledge goes stale (the lists refresh only every 64 frames of a decided shape)"""
+    W, H = 1920, 1080
+    s = host.Scene.named(scene).build_bvh(3)
+    px = torch.empty((H, W), dtype=torch.int32, device="cuda")
+    r = device.Renderer(0)
+    r.upload(s)
+    n = 0
+    while True:
+        r.render(cam_at(W, H, 20), W, H, bgra=px)
+        r.sync()
+        n += 1
+        if r.launch_info()["settled"] or n > 60:
+            break
+    out = []
+    for d in (0, 1, 2, 4, 8, 16):
+        ts = []
+        for _ in range(3):
+            r.render(cam_at(W, H, 20 + d), W, H, bgra=px)
+            ts.append(r.sync())
+        out.append(f"d{d} {sorted(ts)[1]:.3f}")
+    info = r.launch_info()
+    r.close()
+    print(scene, "stale:", " ".join(out), info, flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[2] == "stale":
+        stale(sys.argv[1])
+        sys.exit(0)
     main()
