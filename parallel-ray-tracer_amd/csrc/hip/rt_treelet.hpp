@@ -39,7 +39,10 @@ struct Tree {
     std::vector<Box> box;
 };
 
-constexpr int TREELET = 7;            // leaves per treelet (2^7 subsets)
+#ifndef PRT_TREELET_LEAVES
+#define PRT_TREELET_LEAVES 7
+#endif
+constexpr int TREELET = PRT_TREELET_LEAVES;  // leaves per treelet (2^7 subsets)
 constexpr double C_INNER = 1.2, C_LEAF = 1.0;  // the SAH prices of the paper
 
 // SAH cost of every subtree (bottom-up): C_INNER * area of each internal node + C_LEAF * area of each leaf
