@@ -264,11 +264,21 @@ __device__ __forceinline__ int closest_g(const DScene& s, v3 o, v3 d, float& bes
         const DWide& W = wide_for(s, unit);
         closest_wide_g<G, COUNT>(W, o, d, best, hp, nd, tie, stk, c, q);
         if (!tie) return hp >= 0 ? W.tri_orig[hp] : -1;
+        CTR_INC(c, fb, C_FALLBACK);  // strict re-walk, redundantly in every lane of the group
+        if (TIE_BOUNDED) {  // (bounded just past the tie: closest)
+            const float tb = tie_bound(o, best);
+            hp = -1;
+            nd = 0;
+            best = tb;
+            closest_walk<true, COUNT, true>(s.ref, o, d, best, hp, nd, tie, stk, c);
+            if (hp >= 0) return s.ref.tri_orig[hp];
+        }
         hp = -1;
         best = FMAX;
         nd = 0;
+    } else {
+        CTR_INC(c, fb, C_FALLBACK);
     }
-    CTR_INC(c, fb, C_FALLBACK);  // strict re-walk, redundantly in every lane of the group
     closest_walk<true, COUNT, true>(s.ref, o, d, best, hp, nd, tie, stk, c);
     return hp >= 0 ? s.ref.tri_orig[hp] : -1;
 }
