@@ -252,8 +252,8 @@ def main():
                          "on RCCL, torch on gloo (the one-GPU rehearsal: RCCL refuses two ranks on one device)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--timeout", type=float, default=240.0,
-                    help="N > 1: seconds any rank may wait on a collective (the process group's timeout, the native "
-                         "gather's bounded waits) and, x 2.5, on the whole run (a watchdog prints every thread's stack and "
+                    help="N > 1: seconds any rank may wait on a native gather (x 2 on the process group's collectives, "
+                         "which agree on a gather's failure) and, x 2.5, on the whole run (a watchdog prints every thread's stack and "
                          "exits non-zero): a first multi-GPU run that deadlocks fails loudly instead of hanging")
     args = ap.parse_args()
 
@@ -284,7 +284,7 @@ def main():
 
         import torch.distributed as dist
 
-        tmo = datetime.timedelta(seconds=args.timeout)
+        tmo = datetime.timedelta(seconds=2 * args.timeout)  # (twice the native gather's: its failures are agreed on)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
@@ -403,6 +403,29 @@ def main():
                 if fg.pending(b):
                     fg.finish(b)
 
+    if gmode == "native":
+        # the first multi-rank run of the native gather must not end the run: one probe launch + gather with bounded
+        # waits (the descriptor exchange, the coverage check, rt_comm_wait); any rank's failure -> every rank falls
+        # back to torch.distributed's gather (agreed over the process group, whose timeout is twice the gather's)
+        err = ""
+        try:
+            launch(min(plan))
+            ng.wait()
+            torch.cuda.synchronize()
+        except Exception as e:
+            err = repr(e)
+        errs = [err]
+        if dist:
+            errs = [None] * world
+            dist.all_gather_object(errs, err)
+        if any(errs):
+            try:
+                ng.close()
+            except Exception:
+                pass
+            ng, gmode = None, "torch"
+            gather_note = "torch.distributed.gather (the native gather's probe failed: " + next(e for e in errs if e) + ")"
+
     # setup, like the upload: the library's default rule measures its candidates on the first launches of a shape
     # (PERSIST4 vs the shadow pool, rt_get_launch_info: trial / settled), so
     # each batch size of the plan runs here until every context has settled, then `warmup` frames run untimed.
@@ -411,6 +434,8 @@ def main():
         for i in range(32):
             launch(nf)
             if i >= 2 * n_streams - 1:
+                if ng:
+                    ng.wait()  # (bounded: a collective that never completes raises instead of hanging)
                 torch.cuda.synchronize()
                 settled = [all(r.launch_info()["settled"] for r in rends)]
                 if dist:  # every rank stops together (the gathers are collective), once all have settled
