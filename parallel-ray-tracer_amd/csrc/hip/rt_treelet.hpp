@@ -43,7 +43,10 @@ struct Tree {
 #define PRT_TREELET_LEAVES 7
 #endif
 constexpr int TREELET = PRT_TREELET_LEAVES;  // leaves per treelet (2^7 subsets)
-constexpr double C_INNER = 1.2, C_LEAF = 1.0;  // the SAH prices of the paper
+#ifndef PRT_TREELET_CI
+#define PRT_TREELET_CI 1.2
+#endif
+constexpr double C_INNER = PRT_TREELET_CI, C_LEAF = 1.0;  // the SAH prices of the paper
 
 // SAH cost of every subtree (bottom-up): C_INNER * area of each internal node + C_LEAF * area of each leaf
 inline std::vector<double> subtree_costs(const Tree& T, const std::vector<int>& post) {
