@@ -87,28 +87,30 @@ __device__ __forceinline__ void wide_node_g(const WNode& nd, const RayPre& p, un
                 az = __builtin_fmaf(f0.z, p.iz, -p.oz);
     const float kx = sx * p.ix, ky = sy * p.iy, kz = sz * p.iz;
     const bool bx = (oct & 1u) != 0, by = (oct & 2u) != 0, bz = (oct & 4u) != 0;
-    // near / far plane words per half (slots 0..3 / 4..7), chosen by the octant
-    const unsigned lxw[2] = {__float_as_uint(f2.x), __float_as_uint(f2.y)},
-                   lyw[2] = {__float_as_uint(f2.z), __float_as_uint(f2.w)},
-                   lzw[2] = {__float_as_uint(f3.x), __float_as_uint(f3.y)},
-                   hxw[2] = {__float_as_uint(f3.z), __float_as_uint(f3.w)},
-                   hyw[2] = {__float_as_uint(f4.x), __float_as_uint(f4.y)},
-                   hzw[2] = {__float_as_uint(f4.z), __float_as_uint(f4.w)};
+    // the slot pairs' plane words per axis (rt_device.hpp: word j = qlo[2j], qhi[2j], qlo[2j+1], qhi[2j+1])
+    const unsigned xw[4] = {__float_as_uint(f2.x), __float_as_uint(f2.y), __float_as_uint(f2.z), __float_as_uint(f2.w)},
+                   yw[4] = {__float_as_uint(f3.x), __float_as_uint(f3.y), __float_as_uint(f3.z), __float_as_uint(f3.w)},
+                   zw[4] = {__float_as_uint(f4.x), __float_as_uint(f4.y), __float_as_uint(f4.z), __float_as_uint(f4.w)};
+    // near / far byte of a slot's planes by the octant: lo at bit 16 (s & 1), hi 8 bits above
+    const unsigned nxs = bx ? 8u : 0u, fxs = 8u - nxs, nys = by ? 8u : 0u, fys = 8u - nys, nzs = bz ? 8u : 0u,
+                   fzs = 8u - nzs;
     unsigned hit = 0;
 #pragma unroll
     for (int j = 0; j < 8 / G; j++) {
         const unsigned s = q + (unsigned)(j * G);
-        const unsigned h = s >> 2, sh = 8u * (s & 3u);
-        const unsigned nxw = bx ? hxw[h] : lxw[h], fxw = bx ? lxw[h] : hxw[h];
-        const unsigned nyw = by ? hyw[h] : lyw[h], fyw = by ? lyw[h] : hyw[h];
-        const unsigned nzw = bz ? hzw[h] : lzw[h], fzw = bz ? lzw[h] : hzw[h];
+        // the pair's word: j * G / 2 + (q >> 1) (G = 2: q >> 1 == 0; G = 4: one of two words, selected)
+        const int w0 = j * G / 2;
+        const bool w1 = G > 2 && (q >> 1) != 0u;
+        const unsigned xs = w1 ? xw[w0 + (G > 2 ? 1 : 0)] : xw[w0], ys = w1 ? yw[w0 + (G > 2 ? 1 : 0)] : yw[w0],
+                       zs = w1 ? zw[w0 + (G > 2 ? 1 : 0)] : zw[w0];
+        const unsigned sh = 16u * (s & 1u);
         // (plane = 2^e * (QBIAS + q) + p: QBIAS + q is exact in float, the FMA rounds once, as wide_node's fma_mix)
-        const float tnx = __builtin_fmaf((float)(QBIAS + ((nxw >> sh) & 0xFFu)), kx, ax);
-        const float tfx = __builtin_fmaf((float)(QBIAS + ((fxw >> sh) & 0xFFu)), kx, ax);
-        const float tny = __builtin_fmaf((float)(QBIAS + ((nyw >> sh) & 0xFFu)), ky, ay);
-        const float tfy = __builtin_fmaf((float)(QBIAS + ((fyw >> sh) & 0xFFu)), ky, ay);
-        const float tnz = __builtin_fmaf((float)(QBIAS + ((nzw >> sh) & 0xFFu)), kz, az);
-        const float tfz = __builtin_fmaf((float)(QBIAS + ((fzw >> sh) & 0xFFu)), kz, az);
+        const float tnx = __builtin_fmaf((float)(QBIAS + ((xs >> (sh + nxs)) & 0xFFu)), kx, ax);
+        const float tfx = __builtin_fmaf((float)(QBIAS + ((xs >> (sh + fxs)) & 0xFFu)), kx, ax);
+        const float tny = __builtin_fmaf((float)(QBIAS + ((ys >> (sh + nys)) & 0xFFu)), ky, ay);
+        const float tfy = __builtin_fmaf((float)(QBIAS + ((ys >> (sh + fys)) & 0xFFu)), ky, ay);
+        const float tnz = __builtin_fmaf((float)(QBIAS + ((zs >> (sh + nzs)) & 0xFFu)), kz, az);
+        const float tfz = __builtin_fmaf((float)(QBIAS + ((zs >> (sh + fzs)) & 0xFFu)), kz, az);
         const float lo = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, BOX_TMIN));
         const float hi = fminf(fminf(tfx, tfy), fminf(tfz, lim));
         hit |= lo <= hi ? (1u << s) : 0u;

@@ -40,7 +40,7 @@ struct DBvh {
 // The fast walk's 8-wide quantised BVH (rt_wide.cpp; replaces `acc` when present). 80-B nodes:
 //   f4[0] = p.x p.y p.z | bits: e.x+127, e.y+127, e.z+127, imask (bytes 0..3)
 //   f4[1] = child_base, tri_base, meta[0..3], meta[4..7]
-//   f4[2] = qlo.x[0..7], qlo.y[0..7]   f4[3] = qlo.z[0..7], qhi.x[0..7]   f4[4] = qhi.y[0..7], qhi.z[0..7]
+//   f4[2] = the x planes, f4[3] = y, f4[4] = z: word j = bytes qlo[2j], qhi[2j], qlo[2j+1], qhi[2j+1]
 // child box plane = fmaf(2^e, 1024 + q, p) (exact product, one rounding; the bias makes 1024 + q an f16 integer whose
 // bits are 0x6400 | q, rt_kernels.hpp fma_half); slot s holds the child in octant s
 // of the node (bit 0 = +x, 1 = +y, 2 = +z). imask bit s: slot s is an interior node, at

@@ -398,8 +398,18 @@ __device__ __forceinline__ void count_step(Ctr& c, bool shadow) {
 // pairs incl. specials on the GPU, tools/mix/mix_check.hip). Per node visit: 24 perms + 48 FMAs instead of 48 byte
 // conversions + 48 FMAs.
 constexpr unsigned QBIAS = 1024u;
-__device__ __forceinline__ unsigned plane_pair(unsigned w, int pair) {  // bytes 2 pair, 2 pair + 1 -> two f16 halves
-    return __builtin_amdgcn_perm(w, 0x64646464u, pair ? 0x00070006u : 0x00050004u);
+// A node word holds one slot pair's planes of one axis (qlo[2j], qhi[2j], qlo[2j+1], qhi[2j+1]); the byte selector picks
+// the pair's near or far planes by the ray's sign on that axis (plane_sel), so no per-node select of words is needed.
+__device__ __forceinline__ unsigned plane_pair(unsigned w, unsigned sel) {  // two planes of a word -> two f16 halves
+    return __builtin_amdgcn_perm(w, 0x64646464u, sel);
+}
+// the selector of a pair's near (far = false: far) planes: bytes 0 / 2 (the lo planes) or 1 / 3 (hi) of the word
+// (perm indices 4..7), each under a constant 0x64 byte (index 0)
+#ifndef PRT_SEL_FAR_XOR
+#define PRT_SEL_FAR_XOR 1
+#endif
+__device__ __forceinline__ unsigned plane_sel(bool neg, bool near) {
+    return (neg == near) ? 0x00070005u : 0x00060004u;
 }
 __device__ __forceinline__ float max_raw(float a, float b) {
     float r;
@@ -461,21 +471,31 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
     const float ax = __builtin_fmaf(f0.x, p.ix, -p.ox), ay = __builtin_fmaf(f0.y, p.iy, -p.oy),
                 az = __builtin_fmaf(f0.z, p.iz, -p.oz);
     const float kx = sx * p.ix, ky = sy * p.iy, kz = sz * p.iz;
-    // near / far plane bytes per axis from the direction signs (== min / max of the two slab ends)
+    // near / far plane bytes per axis from the direction signs (== min / max of the two slab ends): byte selectors
+    // (loop-invariant over the walk: oct is the ray's)
     const bool bx = (oct & 1u) != 0, by = (oct & 2u) != 0, bz = (oct & 4u) != 0;
-    const unsigned lx[2] = {__float_as_uint(f2.x), __float_as_uint(f2.y)}, ly[2] = {__float_as_uint(f2.z), __float_as_uint(f2.w)},
-                   lz[2] = {__float_as_uint(f3.x), __float_as_uint(f3.y)}, hx[2] = {__float_as_uint(f3.z), __float_as_uint(f3.w)},
-                   hy[2] = {__float_as_uint(f4.x), __float_as_uint(f4.y)}, hz[2] = {__float_as_uint(f4.z), __float_as_uint(f4.w)};
+    const unsigned nsx = plane_sel(bx, true), nsy = plane_sel(by, true), nsz = plane_sel(bz, true);
+#if PRT_SEL_FAR_XOR
+    // far = near with the other byte of each plane pair; derived per node (an opaque copy keeps the compiler from
+    // holding three more loop-invariant registers)
+    const unsigned fsx = (unsigned)opaque((int)nsx) ^ 0x00010001u, fsy = (unsigned)opaque((int)nsy) ^ 0x00010001u,
+                   fsz = (unsigned)opaque((int)nsz) ^ 0x00010001u;
+#else
+    const unsigned fsx = plane_sel(bx, false), fsy = plane_sel(by, false), fsz = plane_sel(bz, false);
+#endif
+    const unsigned wx[4] = {__float_as_uint(f2.x), __float_as_uint(f2.y), __float_as_uint(f2.z), __float_as_uint(f2.w)},
+                   wy[4] = {__float_as_uint(f3.x), __float_as_uint(f3.y), __float_as_uint(f3.z), __float_as_uint(f3.w)},
+                   wz[4] = {__float_as_uint(f4.x), __float_as_uint(f4.y), __float_as_uint(f4.z), __float_as_uint(f4.w)};
     unsigned hit8 = 0;  // bit s: child slot s entered within [0, lim]
 #pragma unroll
     for (int s = 0; s < 8; s++) {
-        const int h = s >> 2, pr = (s >> 1) & 1, hb = s & 1;
-        const float tnx = fma_half(plane_pair(bx ? hx[h] : lx[h], pr), hb, kx, ax);
-        const float tfx = fma_half(plane_pair(bx ? lx[h] : hx[h], pr), hb, kx, ax);
-        const float tny = fma_half(plane_pair(by ? hy[h] : ly[h], pr), hb, ky, ay);
-        const float tfy = fma_half(plane_pair(by ? ly[h] : hy[h], pr), hb, ky, ay);
-        const float tnz = fma_half(plane_pair(bz ? hz[h] : lz[h], pr), hb, kz, az);
-        const float tfz = fma_half(plane_pair(bz ? lz[h] : hz[h], pr), hb, kz, az);
+        const int j = s >> 1, hb = s & 1;
+        const float tnx = fma_half(plane_pair(wx[j], nsx), hb, kx, ax);
+        const float tfx = fma_half(plane_pair(wx[j], fsx), hb, kx, ax);
+        const float tny = fma_half(plane_pair(wy[j], nsy), hb, ky, ay);
+        const float tfy = fma_half(plane_pair(wy[j], fsy), hb, ky, ay);
+        const float tnz = fma_half(plane_pair(wz[j], nsz), hb, kz, az);
+        const float tfz = fma_half(plane_pair(wz[j], fsz), hb, kz, az);
         // Inflation (2^-16 max|coord|) puts every computed near plane strictly before and every far plane
         // strictly after the child's true box, per axis, so the interval below contains the true one; the
         // folded test max(tmin, BOX_TMIN) <= min(tmax, lim) only adds visits: conservative (BOX_TMIN below).
@@ -632,8 +652,12 @@ __device__ __forceinline__ bool closest_tris_packed(const DWide& W, v3 o, v3 d, 
     if (nt) {
         const unsigned long long kc = key[lane];
         const unsigned fl = flag[lane];
-        key[lane] = 0ull;
-        flag[lane] = 0u;
+        // (zeroed through an opaque 32-bit zero: a 64-bit constant pair is one the register allocator spills rather
+        // than rematerialises, and its reload waits for the next node's load)
+        const int z = opaque(0);
+        reinterpret_cast<int*>(key + lane)[0] = z;
+        reinterpret_cast<int*>(key + lane)[1] = z;
+        flag[lane] = z;
         const unsigned long long kw = ~kc;
         const float mt = __uint_as_float((unsigned)(kw >> 32));
         if (kc != 0ull) {

@@ -400,8 +400,12 @@ extern "C" int rth_wbvh_build_cost(const rt_bvh_node* bvh, int n_nodes, const in
             }
         }
         std::memcpy(&W[6], meta, 8);
-        // qlo_x qlo_y | qlo_z qhi_x | qhi_y qhi_z  (8 bytes each)
-        for (int pl = 0; pl < 6; pl++) std::memcpy(&W[8 + 2 * pl], q8[pl], 8);
+        // per axis a, four words: word j = qlo[2j], qhi[2j], qlo[2j + 1], qhi[2j + 1] (one slot pair's two planes
+        // side by side, so that a single byte permute picks a pair's near or far planes by the ray's sign)
+        for (int a = 0; a < 3; a++)
+            for (int j = 0; j < WIDTH / 2; j++)
+                W[8 + 4 * a + j] = (uint32_t)q8[a][2 * j] | ((uint32_t)q8[3 + a][2 * j] << 8) |
+                                   ((uint32_t)q8[a][2 * j + 1] << 16) | ((uint32_t)q8[3 + a][2 * j + 1] << 24);
     }
     if ((int)order.size() != n_tris) return RT_E_ARG;  // a triangle referenced twice or never
     uint32_t* nodes = (uint32_t*)std::malloc(sizeof(uint32_t) * words.size());

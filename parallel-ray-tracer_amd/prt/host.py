@@ -148,8 +148,8 @@ def wbvh_decode(words):
     scale = np.ldexp(np.float32(1), (e - 127).astype(np.int32)).astype(np.float32)
     imask = (w[:, 3] >> 24) & 0xFF
     meta = w[:, 6:8].copy().view(np.uint8).reshape(-1, 8)
-    q = w[:, 8:20].copy().view(np.uint8).reshape(-1, 6, 8)
-    qlo, qhi = q[:, 0:3], q[:, 3:6]
+    q = w[:, 8:20].copy().view(np.uint8).reshape(-1, 3, 8, 2)  # per axis: slot pairs' (lo, hi) side by side
+    qlo, qhi = q[..., 0], q[..., 1]
     # fmaf(scale, 1024 + q, p) == p + scale * (1024 + q) rounded once (the product is exact): evaluate in f64, round
     lo = (p[:, :, None].astype(np.float64) + scale[:, :, None].astype(np.float64) * (1024.0 + qlo)).astype(np.float32)
     hi = (p[:, :, None].astype(np.float64) + scale[:, :, None].astype(np.float64) * (1024.0 + qhi)).astype(np.float32)
