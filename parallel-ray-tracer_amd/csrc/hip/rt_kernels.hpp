@@ -411,6 +411,23 @@ __device__ __forceinline__ unsigned plane_pair(unsigned w, unsigned sel) {  // t
 __device__ __forceinline__ unsigned plane_sel(bool neg, bool near) {
     return (neg == near) ? 0x00070005u : 0x00060004u;
 }
+// 2 h + c with the compare's lane mask as the carry: one instruction per slot where a select and an OR took two
+#ifndef PRT_HIT_ADDC
+#define PRT_HIT_ADDC 1
+#endif
+constexpr bool HIT_ADDC = PRT_HIT_ADDC != 0;
+__device__ __forceinline__ unsigned shift_in(unsigned h, bool c) {
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(c);
+    unsigned r;
+    unsigned long long co;
+    __asm__("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(h), "s"(m));
+    return r;
+}
+__device__ __forceinline__ unsigned far_sel(unsigned near_sel) {
+    unsigned r;
+    __asm__ volatile("v_xor_b32 %0, 0x10001, %1" : "=v"(r) : "v"(near_sel));
+    return r;
+}
 __device__ __forceinline__ float max_raw(float a, float b) {
     float r;
     __asm__("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -476,10 +493,9 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
     const bool bx = (oct & 1u) != 0, by = (oct & 2u) != 0, bz = (oct & 4u) != 0;
     const unsigned nsx = plane_sel(bx, true), nsy = plane_sel(by, true), nsz = plane_sel(bz, true);
 #if PRT_SEL_FAR_XOR
-    // far = near with the other byte of each plane pair; derived per node (an opaque copy keeps the compiler from
-    // holding three more loop-invariant registers)
-    const unsigned fsx = (unsigned)opaque((int)nsx) ^ 0x00010001u, fsy = (unsigned)opaque((int)nsy) ^ 0x00010001u,
-                   fsz = (unsigned)opaque((int)nsz) ^ 0x00010001u;
+    // far = near with the other byte of each plane pair, derived per node (a volatile XOR: hoisted, the compiler
+    // would hold three more loop-invariant registers and spill)
+    const unsigned fsx = far_sel(nsx), fsy = far_sel(nsy), fsz = far_sel(nsz);
 #else
     const unsigned fsx = plane_sel(bx, false), fsy = plane_sel(by, false), fsz = plane_sel(bz, false);
 #endif
@@ -488,7 +504,7 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
                    wz[4] = {__float_as_uint(f4.x), __float_as_uint(f4.y), __float_as_uint(f4.z), __float_as_uint(f4.w)};
     unsigned hit8 = 0;  // bit s: child slot s entered within [0, lim]
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
+    for (int s = HIT_ADDC ? 7 : 0; HIT_ADDC ? s >= 0 : s < 8; s += HIT_ADDC ? -1 : 1) {
         const int j = s >> 1, hb = s & 1;
         const float tnx = fma_half(plane_pair(wx[j], nsx), hb, kx, ax);
         const float tfx = fma_half(plane_pair(wx[j], fsx), hb, kx, ax);
@@ -503,7 +519,8 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
         // v_max_f32 per plane; the entries are never NaN here -- zero direction components walk strictly)
         const float lo = max3_raw(tnx, tny, max_raw(tnz, BOX_TMIN));
         const float hi = min3_raw(tfx, tfy, min_raw(tfz, lim));
-        hit8 |= lo <= hi ? (1u << s) : 0u;
+        if (HIT_ADDC) hit8 = shift_in(hit8, lo <= hi);  // (slots 7 .. 0: slot s ends at bit s)
+        else hit8 |= lo <= hi ? (1u << s) : 0u;
     }
     // interior hits, permuted into visiting order: bit k = slot k ^ oct (XOR by oct swaps bits, pairs and
     // nibbles of the 8-bit mask)
