@@ -38,7 +38,7 @@ struct DBvh {
 };
 
 // The fast walk's 8-wide quantised BVH (rt_wide.cpp; replaces `acc` when present). 80-B nodes:
-//   f4[0] = p.x p.y p.z | bits: e.x+127, e.y+127, e.z+127, imask (bytes 0..3)
+//   f4[0] = p.x p.y p.z | bits: e.x, e.y, e.z (signed bytes), imask (bytes 0..3)
 //   f4[1] = child_base, tri_base, meta[0..3], meta[4..7]
 //   f4[2] = the x planes, f4[3] = y, f4[4] = z: word j = bytes qlo[2j], qhi[2j], qlo[2j+1], qhi[2j+1]
 // child box plane = fmaf(2^e, 1024 + q, p) (exact product, one rounding; the bias makes 1024 + q an f16 integer whose

@@ -474,9 +474,7 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
                                           unsigned& th, int& cbase, int& tbase, unsigned& imask, unsigned& nleaf,
                                           unsigned ord_xor = 0u) {
     const float4 f0 = nd.f0, f1 = nd.f1, f2 = nd.f2, f3 = nd.f3, f4 = nd.f4;
-    const unsigned e = __float_as_uint(f0.w);
-    const float sx = __uint_as_float((e & 0xFFu) << 23), sy = __uint_as_float(((e >> 8) & 0xFFu) << 23),
-                sz = __uint_as_float(((e >> 16) & 0xFFu) << 23);
+    const unsigned e = __float_as_uint(f0.w);  // exponents (signed bytes) | interior mask
     imask = e >> 24;
     cbase = __float_as_int(f1.x);
     tbase = __float_as_int(f1.y);
@@ -487,7 +485,9 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
     // is covered >= 20x by the boxes' inflation (2^-16 max|coord|, rt_hip.hip).
     const float ax = __builtin_fmaf(f0.x, p.ix, -p.ox), ay = __builtin_fmaf(f0.y, p.iy, -p.oy),
                 az = __builtin_fmaf(f0.z, p.iz, -p.oz);
-    const float kx = sx * p.ix, ky = sy * p.iy, kz = sz * p.iz;
+    const float kx = __builtin_ldexpf(p.ix, (int)(signed char)(e & 0xFFu)),
+                ky = __builtin_ldexpf(p.iy, (int)(signed char)((e >> 8) & 0xFFu)),
+                kz = __builtin_ldexpf(p.iz, (int)(signed char)((e >> 16) & 0xFFu));
     // near / far plane bytes per axis from the direction signs (== min / max of the two slab ends): byte selectors
     // (loop-invariant over the walk: oct is the ray's)
     const bool bx = (oct & 1u) != 0, by = (oct & 2u) != 0, bz = (oct & 4u) != 0;

@@ -225,7 +225,7 @@ inline uint32_t f2u(float f) {
 }
 
 // Quantise one axis of up to 8 child boxes (already grown) on the grid pb + 2^e * (QBIAS + q), q in 0..255.
-// Returns the biased exponent byte (e + 127); pb receives the grid's origin, qlo/qhi the planes.
+// Returns the grid's exponent e (-126 .. 110); pb receives the grid's origin, qlo/qhi the planes.
 int quantise_axis(const float* lo, const float* hi, int k, float& pb, int* qlo, int* qhi) {
     float p = INFINITY, top = -INFINITY;
     for (int c = 0; c < k; c++) {
@@ -250,7 +250,7 @@ int quantise_axis(const float* lo, const float* hi, int k, float& pb, int* qlo, 
             qlo[c] = a;
             qhi[c] = b;
         }
-        if (ok || e >= 110) return e + 127;
+        if (ok || e >= 110) return e;
     }
 }
 
@@ -371,7 +371,9 @@ extern "C" int rth_wbvh_build_cost(const rt_bvh_node* bvh, int n_nodes, const in
         uint32_t imask = 0;
         for (int s = 0; s < WIDTH; s++)
             if (kid_in[s] >= 0 && !kid_leaf[kid_in[s]]) imask |= 1u << s;
-        W[3] = (uint32_t)eb[0] | ((uint32_t)eb[1] << 8) | ((uint32_t)eb[2] << 16) | (imask << 24);
+        // the exponents as signed bytes: the walks scale 1/d by them with one v_ldexp_f32 each
+        W[3] = (uint32_t)(uint8_t)(int8_t)eb[0] | ((uint32_t)(uint8_t)(int8_t)eb[1] << 8) |
+               ((uint32_t)(uint8_t)(int8_t)eb[2] << 16) | (imask << 24);
         const int child_base = (int)queue.size();
         const int tri_base = (int)order.size();
         W[4] = (uint32_t)child_base;

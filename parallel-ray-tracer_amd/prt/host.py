@@ -144,8 +144,8 @@ def wbvh_decode(words):
     f16-ready bias, rt_wide.cpp QBIAS)"""
     w = np.ascontiguousarray(words, dtype=np.uint32)
     p = w[:, 0:3].view(np.float32)
-    e = np.stack([(w[:, 3] >> (8 * a)) & 0xFF for a in range(3)], 1).astype(np.int64)
-    scale = np.ldexp(np.float32(1), (e - 127).astype(np.int32)).astype(np.float32)
+    e = np.stack([(w[:, 3] >> (8 * a)) & 0xFF for a in range(3)], 1).astype(np.uint8).view(np.int8)  # signed bytes
+    scale = np.ldexp(np.float32(1), e.astype(np.int32)).astype(np.float32)
     imask = (w[:, 3] >> 24) & 0xFF
     meta = w[:, 6:8].copy().view(np.uint8).reshape(-1, 8)
     q = w[:, 8:20].copy().view(np.uint8).reshape(-1, 3, 8, 2)  # per axis: slot pairs' (lo, hi) side by side
