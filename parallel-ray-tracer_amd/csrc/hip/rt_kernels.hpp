@@ -463,6 +463,26 @@ struct WNode {
 // The upper levels in LDS (LDS_TOP, north star "LDS-staged upper BVH levels"): every walk starts with the root and
 // most continue into its children; with `top` set, a node below NTOP is read from the workgroup's LDS copy. The
 // address is selected, not branched on (a flat load serves both), so the next-node load stays unconditional.
+// PRT_PIN_NODE: the node's five float4 held in register quads at the walk loop's head (an empty asm), so that the
+// loads of the next node land where the node test reads them
+#ifndef PRT_PIN_NODE
+#define PRT_PIN_NODE 1
+#endif
+typedef float pin4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void pin_q(float4& f) {
+    pin4 v = {f.x, f.y, f.z, f.w};
+    __asm__ volatile("" : "+v"(v));
+    f = make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void pin_node(WNode& N) {
+    if (PRT_PIN_NODE) {
+        pin_q(N.f0);
+        pin_q(N.f1);
+        pin_q(N.f2);
+        pin_q(N.f3);
+        pin_q(N.f4);
+    }
+}
 __device__ __forceinline__ WNode wload(const DWide& W, int node, const float4* top = nullptr) {
     const float4* N = (top && node < NTOP) ? top + 5 * node : W.nodes + 5 * node;
     return WNode{N[0], N[1], N[2], N[3], N[4]};
@@ -755,6 +775,7 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
     for (;;) {
         unsigned nh, th, imask, nl;
         int cb, tb;
+        pin_node(N);
         wide_node<COUNT>(N, p, oct, best * PRUNE_SLACK, nh, th, cb, tb, imask, nl);
         if (COUNT) {
             c.chi++;
@@ -842,6 +863,7 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
     for (;;) {
         unsigned nh, th, imask, nl;
         int cb, tb;
+        pin_node(N);
         wide_node<COUNT>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nl, SHADOW_ORDER_XOR);
         if (COUNT) {
             c.shi++;

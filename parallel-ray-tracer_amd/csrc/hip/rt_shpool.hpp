@@ -183,6 +183,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
             if (busy) {  // one step of visible_wide
                 unsigned nh, imask, nlf;
                 int cb;
+                pin_node(N);
                 wide_node<COUNT>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nlf, SHADOW_ORDER_XOR);
                 if (COUNT) {
                     c.shi++;
