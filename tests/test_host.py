@@ -176,6 +176,7 @@ def _check_wbvh(s, inflate):
     inside the node's 32-triangle window; children of a node are consecutive records"""
     words, order, info = host.wbvh_build(s.nodes, s.tri_idx, s.triangles, inflate)
     D = host.wbvh_decode(words)
+    memo = {}
     n = len(s.triangles)
     assert sorted(order.tolist()) == list(range(n))
     v = s.triangles["coords"].astype(np.float32)  # [n, 3, 3]
@@ -196,7 +197,7 @@ def _check_wbvh(s, inflate):
             if s_ in internal:
                 c = int(D["child_base"][k]) + sum(1 for j in internal if j < s_)
                 stack.append((c, d + 1))
-                sub = _wbvh_subtree_tris(D, c, order)
+                sub = _wbvh_subtree_tris(D, c, order, memo)
             elif m:
                 cnt, off = m >> 5, m & 31
                 assert 1 <= cnt <= 4 and off + cnt <= 32
@@ -210,8 +211,10 @@ def _check_wbvh(s, inflate):
     return info
 
 
-def _wbvh_subtree_tris(D, k, order, memo={}):
-    key = (id(D), k)
+def _wbvh_subtree_tris(D, k, order, memo):
+    """the triangles under wide node k (memo: one dict per decoded tree -- a module-level cache keyed by id(D) would
+    serve a collected tree's entries to a later tree that reuses its address)"""
+    key = k
     if key in memo:
         return memo[key]
     out = []
@@ -220,7 +223,7 @@ def _wbvh_subtree_tris(D, k, order, memo={}):
         m = int(D["meta"][k, s_])
         if s_ in internal:
             c = int(D["child_base"][k]) + sum(1 for j in internal if j < s_)
-            out.append(_wbvh_subtree_tris(D, c, order))
+            out.append(_wbvh_subtree_tris(D, c, order, memo))
         elif m:
             off, cnt = m & 31, m >> 5
             out.append(order[int(D["tri_base"][k]) + off: int(D["tri_base"][k]) + off + cnt])
