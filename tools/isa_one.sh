@@ -16,7 +16,7 @@ mkdir -p /tmp/isa
     esac
   done
 } > /tmp/isa/one.hip
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -fno-slp-vectorize \
     -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -Iparallel-ray-tracer_amd/csrc/hip \
     $ISA_FLAGS --cuda-device-only -S -o /tmp/isa/one.s /tmp/isa/one.hip || exit 1
 python3 - <<'PY'

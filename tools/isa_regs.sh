@@ -1,7 +1,7 @@
 #!/bin/bash
 # VGPR / scratch / LDS per kernel of librt_hip (device-only compile to assembly; no GPU needed)
 cd "$(dirname "$0")/.."
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -fno-slp-vectorize \
     -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -Iparallel-ray-tracer_amd/csrc \
     -Iparallel-ray-tracer_amd/csrc/hip --cuda-device-only -S -o /tmp/rt_isa.s \
     parallel-ray-tracer_amd/csrc/hip/rt_hip.hip 2>/dev/null || exit 1
