@@ -32,7 +32,14 @@ typedef struct rt_ctx rt_ctx;
 
 /* rt_opts.flags */
 enum {
-    RT_FLAG_COUNTERS = 1 /* also count traversal work (node visits, triangle tests): slower */
+    RT_FLAG_COUNTERS = 1,       /* also count traversal work (node visits, triangle tests): slower */
+    /* The kernels' packed builds have field bounds: 5-byte stack entries hold a 24-bit child base (at most 2^24 wide
+     * nodes per view), packed triangle-test jobs a 26-bit triangle index (fewer than 2^26 triangles). Scenes past them
+     * run the unpacked builds. These two flags select those builds for any scene, so that they can be checked on
+     * scenes of test size (tests/test_gpu_unpacked.py). The result is bit-identical either way. */
+    RT_FLAG_UNPACKED_STACK = 2, /* as for a scene of more than 2^24 wide nodes: no packed stack entries (no pool
+                                   kernels, PERSIST4 with two-word entries) */
+    RT_FLAG_UNPACKED_TRIS = 4   /* as for a scene of 2^26 or more triangles: no packed triangle tests */
 };
 
 typedef struct rt_opts {
@@ -99,7 +106,8 @@ enum {
     RT_VARIANT_DEFAULT = 0,  /* the library's rule, measured per frame shape: frame batches and spp > 1 try
                                 RT_VARIANT_PERSIST4 and the pool kernel -- RT_VARIANT_SHDEFER where its LDS path buffer
                                 fits, else RT_VARIANT_SHPOOL -- three times each on their first launches and keep the
-                                faster by the median (RT_VARIANT_PERSIST4 alone where no pool fits); single 1-spp frames
+                                faster, by the minimum of each candidate's trials, or by their medians when a
+                                candidate's median exceeds 50 ms (RT_VARIANT_PERSIST4 alone where no pool fits); single 1-spp frames
                                 run RT_VARIANT_HYBRID (RT_VARIANT_PERSIST where it cannot run); rt_get_launch_info */
     RT_VARIANT_PERSIST = 1,  /* k_persist: one lane per pixel path, walks in lockstep, 3 waves per SIMD */
     RT_VARIANT_PERSIST4 = 2, /* k_persist at 4 waves per SIMD (path levels in LDS) */
@@ -248,7 +256,19 @@ typedef struct rt_launch_info {
                          periodic list refresh, every 64 frames of a shape, is reported by `refresh`) */
     int refresh;      /* 1: a decided hybrid shape's measuring frame that renews its tile lists (k_persist with per-tile
                          times; part of the rule's steady cost, settled = 1) */
+    unsigned build;   /* the k_persist instantiation that ran (of the cold tiles, for a hybrid launch): RT_BUILD_* bits;
+                         0 for the other kernels (strict, k_coop alone) */
 } rt_launch_info;
+/* rt_launch_info.build */
+enum {
+    RT_BUILD_WAVES4 = 1,       /* 4 waves per SIMD (<= 128 VGPRs); else 3 */
+    RT_BUILD_PACKED_STACK = 2, /* 5-byte wide-stack entries */
+    RT_BUILD_PACKED_TRIS = 4,  /* packed triangle tests through the wave's LDS queue */
+    RT_BUILD_LDS_PATHS = 8,    /* the path levels in LDS (else a global slab, or registers at 3 waves) */
+    RT_BUILD_POOL_LEVEL = 16,  /* the per-level shadow pool (RT_VARIANT_SHPOOL) */
+    RT_BUILD_POOL_ALL = 32,    /* one shadow pool for all levels (RT_VARIANT_SHDEFER) */
+    RT_BUILD_TRACE = 64        /* the measuring build with per-tile times */
+};
 int rt_get_launch_info(rt_ctx* ctx, rt_launch_info* info);
 /* load_from_gpu(): copies the last frame's compact rows to host (synchronous); nullable args. RT_E_KERNEL when the
  * render reported a traversal-stack overflow (its frame is not valid). */

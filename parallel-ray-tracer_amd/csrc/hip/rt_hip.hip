@@ -879,8 +879,9 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     ctx->prim_tris_n = prim_nodes.empty() ? 0 : prim_tris_n;
     ctx->n_lights = sc->n_lights;
     ctx->n_tris = n;
-    ctx->pk_ok = std::max(ctx->wide_n, std::max(ctx->unit_n, ctx->prim_n)) <= rtd::WIDE_MAX_NODES;
-    ctx->tq_ok = n < rtd::TQ_MAX_TRIS;
+    ctx->pk_ok = std::max(ctx->wide_n, std::max(ctx->unit_n, ctx->prim_n)) <= rtd::WIDE_MAX_NODES &&
+                 !(ctx->flags & RT_FLAG_UNPACKED_STACK);
+    ctx->tq_ok = n < rtd::TQ_MAX_TRIS && !(ctx->flags & RT_FLAG_UNPACKED_TRIS);
     ctx->amb[0] = sc->amb.x;
     ctx->amb[1] = sc->amb.y;
     ctx->amb[2] = sc->amb.z;
@@ -993,17 +994,30 @@ bool pbl_fits(const rtd::KArgs& A, int device, int shp = 0) {
 // a tile trace (A.tile_trace: the hybrid launch's measuring frame, PRT_TILE_TRACE) runs the 3-wave build with
 // per-tile timestamps.
 template <int MAXB>
-KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, size_t& dyn, bool pk_ok, bool tq_ok) {
+KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, size_t& dyn, bool pk_ok, bool tq_ok,
+                   unsigned* build = nullptr) {
     dyn = 0;
+    unsigned bd = 0;  // rt_launch_info.build of the instantiation returned (RT_BUILD_*)
+    struct Report {
+        unsigned* out;
+        unsigned& v;
+        ~Report() {
+            if (out) *out = v;
+        }
+    } report{build, bd};
     // (the k_persist builds are made either for spp = 1 (SPP1) or for spp > 1 only: each launch takes the one its spp
     // needs; a tile trace -- the hybrid rule's measuring frame, PRT_TILE_TRACE -- is single-sample)
-    if (A.tile_trace)
+    if (A.tile_trace) {
+        bd = RT_BUILD_TRACE;
         return count ? rtd::k_persist<MAXB, false, true, true, 3, true, true, 0, false, true>
                      : rtd::k_persist<MAXB, false, false, true, 3, true, true, 0, false, true>;
+    }
     if ((variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) && pk_ok && tq_ok) {
         const int shp = variant == RT_VARIANT_SHDEFER ? 2 : 1;
         if (pbl_fits<MAXB>(A, device, shp)) {
             dyn = pbl_bytes<MAXB>(A, shp);
+            bd = RT_BUILD_WAVES4 | RT_BUILD_PACKED_STACK | RT_BUILD_PACKED_TRIS | RT_BUILD_LDS_PATHS |
+                 (shp == 2 ? RT_BUILD_POOL_ALL : RT_BUILD_POOL_LEVEL);
             return shp == 2 ? persist4<MAXB, 2>(true, A.spp <= 1, count) : persist4<MAXB, 1>(true, A.spp <= 1, count);
         }
     }
@@ -1013,20 +1027,24 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
     if ((variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) && pk_ok &&
         tq_ok && pbl_fits<MAXB>(A, device, 3)) {
         dyn = pbl_bytes<MAXB>(A, 3);
+        bd = RT_BUILD_WAVES4 | RT_BUILD_PACKED_STACK | RT_BUILD_PACKED_TRIS | RT_BUILD_LDS_PATHS;
         return persist4<MAXB, 3>(true, A.spp <= 1, count);
     }
     if (variant == RT_VARIANT_PERSIST4 || variant == RT_VARIANT_SHPOOL || variant == RT_VARIANT_SHDEFER) {
         const bool pbl = pbl_fits<MAXB>(A, device);
         if (pbl) dyn = pbl_bytes<MAXB>(A);
+        bd = RT_BUILD_WAVES4 | (pbl ? RT_BUILD_LDS_PATHS : 0u);
         // (the bench's batches: the spp = 1 build)
         return persist4<MAXB, 0>(pbl, A.spp <= 1, count);
     }
     // the 3-wave kernel's spp = 1 build with packed triangle tests (queues in static LDS): same box, single frames
     // dragon 1.27 -> 1.16 ms, sportscar 2.40 -> 2.29, car_boxed 1.96 -> 1.84; the default rule's single frames (its
     // cold tiles) sportscar 1.708 -> 1.671, car_boxed 1.210 -> 1.183
-    if (A.spp <= 1 && tq_ok)
+    if (A.spp <= 1 && tq_ok) {
+        bd = RT_BUILD_PACKED_TRIS;
         return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true, 0, false, true, 3>
                      : rtd::k_persist<MAXB, false, false, true, 3, false, true, 0, false, true, 3>;
+    }
     if (A.spp <= 1)  // (scenes past the packed tests' triangle bound)
         return count ? rtd::k_persist<MAXB, false, true, true, 3, false, true, 0, false, true>
                      : rtd::k_persist<MAXB, false, false, true, 3, false, true, 0, false, true>;
@@ -1036,9 +1054,9 @@ KFn persist_kernel(const rtd::KArgs& A, int variant, bool count, int device, siz
 // `cap`: workgroups per CU at most (0: the occupancy limit); the grid never exceeds the tiles / 4.
 template <int MAXB>
 void launch_paths(const rtd::KArgs& A, int variant, bool count, int device, hipStream_t s, int cap, bool pk_ok,
-                  bool tq_ok) {
+                  bool tq_ok, unsigned* build = nullptr) {
     size_t dyn = 0;
-    const KFn k = persist_kernel<MAXB>(A, variant, count, device, dyn, pk_ok, tq_ok);
+    const KFn k = persist_kernel<MAXB>(A, variant, count, device, dyn, pk_ok, tq_ok, build);
     const int blocks = std::max(1, std::min(resident(k, device, cap > 0 ? cap : 8, dyn), (A.n_tiles * A.n_frames + 3) / 4));
     k<<<blocks, rtd::BLOCK, dyn, s>>>(with_slots(A, dyn));
 }
@@ -1107,7 +1125,7 @@ std::vector<int> region_layout(const std::vector<int>& ord, int tx, int ty, int 
 }
 
 template <int MAXB>
-int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c);  // below
+int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsigned* build = nullptr);  // below
 
 // A frame batch's cameras to d_cams when they differ from the set it holds. The copy runs in stream order (after the
 // renders in flight, which read the old set) from a ring of pinned slots; only a slot whose previous copy has not
@@ -1265,15 +1283,18 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     }
     A.n_frames = n_frames;
     A.frame_px = pixels;
-    if (kernel == RT_KERNEL_FAST && !ctx->d_pathbuf) {  // path buffer of the PB kernels: every resident wave
+    if (kernel == RT_KERNEL_FAST && (!ctx->d_pathbuf || !ctx->d_gstack || !ctx->d_lanebuf)) {
+        // (each buffer its own check: a failed allocation of one of them leaves the others, and the next render
+        // retries the missing one instead of launching with a null buffer)
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
         const size_t waves = (size_t)cus * 8 * (rtd::BLOCK / 64);  // <= 8 workgroups per CU (resident() cap)
-        HIPC(hipMalloc((void**)&ctx->d_pathbuf, sizeof(float4) * waves * 8 * 64));  // MAXB <= 8 levels
+        // path buffer of the PB kernels: every resident wave, MAXB <= 8 levels
+        if (!ctx->d_pathbuf) HIPC(hipMalloc((void**)&ctx->d_pathbuf, sizeof(float4) * waves * 8 * 64));
         // DYN kernels' binary-walk stacks: STACK ints per lane of every resident workgroup (<= 8 per CU)
-        HIPC(hipMalloc((void**)&ctx->d_gstack, sizeof(int) * (size_t)cus * 8 * rtd::STACK * rtd::BLOCK));
+        if (!ctx->d_gstack) HIPC(hipMalloc((void**)&ctx->d_gstack, sizeof(int) * (size_t)cus * 8 * rtd::STACK * rtd::BLOCK));
         // the multi-sample builds' per-lane slots (the running sum and the pixel between samples): every resident lane
-        HIPC(hipMalloc((void**)&ctx->d_lanebuf, sizeof(float4) * (size_t)cus * 8 * rtd::BLOCK));
+        if (!ctx->d_lanebuf) HIPC(hipMalloc((void**)&ctx->d_lanebuf, sizeof(float4) * (size_t)cus * 8 * rtd::BLOCK));
     }
     A.pathbuf = ctx->d_pathbuf;
     A.lanebuf = ctx->d_lanebuf;
@@ -1434,15 +1455,20 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 if (q == hipSuccess) {
                     float ms[2] = {1e30f, 1e30f};
                     constexpr int R = rt_ctx::BatchRule::ROUNDS;
+                    float t[2][R];
+                    float med_max = 0.0f;
                     for (int c = 0; c < nc; c++) {
-                        float t[R];
                         for (int r = 0; r < R; r++) {
                             const int sl = (int)(b.launch[c][r] % rt_ctx::NEV);
-                            HIPC(hipEventElapsedTime(&t[r], ctx->ev0s[sl], ctx->ev1s[sl]));
+                            HIPC(hipEventElapsedTime(&t[c][r], ctx->ev0s[sl], ctx->ev1s[sl]));
                         }
-                        std::sort(t, t + R);
-                        ms[c] = t[R / 2] > rt_ctx::BatchRule::LONG_MS ? t[R / 2] : t[0];
+                        std::sort(t[c], t[c] + R);
+                        med_max = std::max(med_max, t[c][R / 2]);
                     }
+                    // one statistic for every candidate (like with like): the median when the launches are long
+                    // (some candidate's median over LONG_MS), else the minimum
+                    const bool by_median = med_max > rt_ctx::BatchRule::LONG_MS;
+                    for (int c = 0; c < nc; c++) ms[c] = by_median ? t[c][R / 2] : t[c][0];
                     b.choice = 0;
                     for (int c = 1; c < nc; c++)
                         if (ms[c] < ms[b.choice]) b.choice = c;
@@ -1719,7 +1745,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 li.hot_pct = ctx->hy.pct[pk.c];
                 li.hot_lanes = ctx->hy.lanes[pk.c];
                 li.cold_variant = ctx->hy.cold[pk.c];
-                return f->bounces <= 4 ? launch_hybrid<4>(ctx, A, count, pk.c) : launch_hybrid<8>(ctx, A, count, pk.c);
+                return f->bounces <= 4 ? launch_hybrid<4>(ctx, A, count, pk.c, &li.build)
+                                       : launch_hybrid<8>(ctx, A, count, pk.c, &li.build);
             }
             rt_ctx::Hybrid& h = ctx->hy;
             if (pk.kind == 0) {  // measuring frame: k_persist with per-tile times, copied to the host behind it
@@ -1728,8 +1755,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 li.trial = li.refresh ? 0 : 1;
                 li.settled = li.refresh;
                 P.tile_trace = h.d_tr;
-                if (f->bounces <= 4) launch_paths<4>(P, RT_VARIANT_PERSIST, count, ctx->device, ctx->stream, cp, ctx->pk_ok, ctx->tq_ok);
-                else launch_paths<8>(P, RT_VARIANT_PERSIST, count, ctx->device, ctx->stream, cp, ctx->pk_ok, ctx->tq_ok);
+                if (f->bounces <= 4) launch_paths<4>(P, RT_VARIANT_PERSIST, count, ctx->device, ctx->stream, cp, ctx->pk_ok, ctx->tq_ok, &li.build);
+                else launch_paths<8>(P, RT_VARIANT_PERSIST, count, ctx->device, ctx->stream, cp, ctx->pk_ok, ctx->tq_ok, &li.build);
                 HIPC(hipGetLastError());
                 HIPC(hipMemcpyAsync(h.h_tr, h.d_tr, sizeof(unsigned long long) * 4 * h.n_tiles, hipMemcpyDeviceToHost,
                                     ctx->stream));
@@ -1740,8 +1767,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             md = pk.c;  // a whole-frame kernel: chosen, tried, or while the measurement / trials are on their way
             li.variant = md;
         }
-        if (f->bounces <= 4) launch_paths<4>(P, md, count, ctx->device, ctx->stream, cp, ctx->pk_ok, ctx->tq_ok);
-        else launch_paths<8>(P, md, count, ctx->device, ctx->stream, cp, ctx->pk_ok, ctx->tq_ok);
+        if (f->bounces <= 4) launch_paths<4>(P, md, count, ctx->device, ctx->stream, cp, ctx->pk_ok, ctx->tq_ok, &li.build);
+        else launch_paths<8>(P, md, count, ctx->device, ctx->stream, cp, ctx->pk_ok, ctx->tq_ok, &li.build);
         return RT_OK;
     };
     {
@@ -1884,7 +1911,7 @@ namespace {
 // persistent grids together fill the chip (the hot grid is sized to start every hot tile at once, at most half the
 // chip), and the context stream waits for both.
 template <int MAXB>
-int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c) {
+int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsigned* build) {
     rt_ctx::Hybrid& h = ctx->hy;
     const int n_hot = h.n_hot[c], n_cold = h.n_cold[c];
     int* lists = h.d_lists + h.at[c];
@@ -1903,7 +1930,7 @@ int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c) {
     P.region_off = h.cold_regions ? lists + n_hot : nullptr;
     P.tile_order = lists + n_hot + (h.cold_regions ? 9 : 0);
     size_t dyn = 0;
-    const KFn kp = persist_kernel<MAXB>(P, h.cold[c], count, ctx->device, dyn, ctx->pk_ok, ctx->tq_ok);
+    const KFn kp = persist_kernel<MAXB>(P, h.cold[c], count, ctx->device, dyn, ctx->pk_ok, ctx->tq_ok, build);
     const int rp = resident(kp, ctx->device, 8, dyn);
     const int rcp = resident(kc, ctx->device);
     const int nc = n_hot > 0 ? std::max(1, std::min((n_hot + 3) / 4, rcp / 2)) : 0;

@@ -83,6 +83,9 @@ inline double optimize_pass(Tree& T) {
     std::vector<int> part(FULL + 1);
     std::vector<Box> sbox(FULL + 1);
     for (int N : post) {
+        // N's cost from its children's current costs: a treelet rebuilt below N since the pass began lowered them
+        // (post order: every child is final here), and the test below must compare against the tree as it now is
+        cost[N] = C_INNER * area(T.box[N]) + cost[T.left[N - T.n]] + cost[T.right[N - T.n]];
         // the treelet: open the leaf of largest area until TREELET leaves (or none can be opened)
         int leaves[TREELET], inner[TREELET];
         int nl = 2, ni = 1;

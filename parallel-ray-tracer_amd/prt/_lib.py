@@ -87,7 +87,12 @@ class SceneInfo(ctypes.Structure):  # rt_scene_info
 class LaunchInfo(ctypes.Structure):  # rt_launch_info
     _fields_ = [("variant", ctypes.c_int), ("hot_pct", ctypes.c_int), ("hot_lanes", ctypes.c_int),
                 ("cold_variant", ctypes.c_int), ("trial", ctypes.c_int), ("settled", ctypes.c_int),
-                ("refresh", ctypes.c_int)]
+                ("refresh", ctypes.c_int), ("build", ctypes.c_uint)]
+
+
+# rt_launch_info.build bits (RT_BUILD_*)
+BUILD_BITS = {"waves4": 1, "packed_stack": 2, "packed_tris": 4, "lds_paths": 8, "pool_level": 16, "pool_all": 32,
+              "trace": 64}
 
 
 class CommInfo(ctypes.Structure):  # rt_comm_info

@@ -22,6 +22,8 @@ DEALING = {"default": 0, "global": 1, "rows": 2, "columns": 3, "blocks": 4, "row
 ACCEL = {"auto": 0, "reference": 1, "gpu": 2, "host": 3}
 ACCEL_NAMES = {v: k for k, v in ACCEL.items()}
 FLAG_COUNTERS = 1
+FLAG_UNPACKED_STACK = 2  # the builds scenes of more than 2^24 wide nodes run (rt_hip.h RT_FLAG_UNPACKED_STACK)
+FLAG_UNPACKED_TRIS = 4   # the builds scenes of 2^26 or more triangles run (RT_FLAG_UNPACKED_TRIS)
 
 
 class RtError(RuntimeError):
@@ -201,9 +203,10 @@ def _rows(rows, height):
 class Renderer:
     """One rt_ctx on one device (gpu.cuh:23-26 seam, explicit instead of global)."""
 
-    def __init__(self, device=0, counters=False, stream=None):
+    def __init__(self, device=0, counters=False, stream=None, flags=0):
+        """flags: more rt_opts.flags (FLAG_UNPACKED_STACK / FLAG_UNPACKED_TRIS: the unpacked builds for any scene)"""
         self._ctx = ctypes.c_void_p()
-        opts = Opts(device, FLAG_COUNTERS if counters else 0, stream)
+        opts = Opts(device, (FLAG_COUNTERS if counters else 0) | flags, stream)
         rc = _L.rt_create(ctypes.byref(opts), ctypes.byref(self._ctx))
         if rc != 0:
             raise RtError(f"rt_create(device={device}) failed with status {rc}")
@@ -334,6 +337,7 @@ class Renderer:
         d = {f: getattr(i, f) for f, _ in _lib.LaunchInfo._fields_}
         d["variant"] = VARIANT_NAMES.get(d["variant"], d["variant"])
         d["cold_variant"] = VARIANT_NAMES.get(d["cold_variant"], d["cold_variant"])
+        d["build_bits"] = sorted(k for k, v in _lib.BUILD_BITS.items() if d["build"] & v)
         return d
 
     def stats(self):
