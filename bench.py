@@ -378,7 +378,8 @@ def main():
     # N > 1: the rule's choice for each launch size (frames per launch), agreed over the ranks after setup
     variant = {}
 
-    def launch(nf):
+    def launch(nf, gather=True):
+        # gather=False: the render alone (the N > 1 line's render-only timing: exposed gather = wall - render)
         b = launch_no[0] % 2
         c = launch_no[0] % n_streams
         launch_no[0] += 1
@@ -386,14 +387,16 @@ def main():
         if gmode == "native":  # render, then the gather on the context's stream (ordered after the render)
             rends[c].render_frames(path(nf), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
                                    kernel=args.kernel, variant=variant.get(nf, args.variant), **out(ng.target(c)[:nf]))
-            ng.gather(c, nf)
+            if gather:
+                ng.gather(c, nf)
             return
         with torch.cuda.stream(streams[c]):  # block b is rendered by context c on its stream
             if fg.pending(b):
                 fg.finish(b)
             rends[c].render_frames(path(nf), W, H, rows=my_rows, bounces=args.bounces, spp=args.spp,
                                    kernel=args.kernel, variant=variant.get(nf, args.variant), **out(fg.target(b)))
-            fg.start(b)
+            if gather:
+                fg.start(b)
 
     def drain():
         if gmode == "native":
@@ -508,6 +511,28 @@ def main():
         ts_ = rr_.kernel_times(len(mine)) if mine else []
         kfull += [t for t, nf in zip(ts_, mine) if nf == F]
     kfull = kfull or [float("nan")]
+    # N > 1 (verdict r5 item 6: a first multi-rank run must be attributable from its one line): every rank's median
+    # kernel ms per frame, and the exposed gather -- the timed region's wall time minus the slowest rank's wall time
+    # for the same launches rendered without their gathers (each rank timed alone: no barrier inside)
+    ranks_detail = None
+    if world > 1:
+        kmed = sorted(kfull)[len(kfull) // 2] / F
+        launch_no[0] = 0  # (the same contexts in the same order as the timed launches)
+        torch.cuda.synchronize()
+        t_r = time.perf_counter()
+        for nf in plan:
+            launch(nf, gather=False)
+        torch.cuda.synchronize()
+        render_wall = time.perf_counter() - t_r
+        every = [None] * world
+        dist.all_gather_object(every, {"rank": rank, "kernel_ms_per_frame": kmed, "render_wall_ms": render_wall * 1e3,
+                                       "variant": rends[timed[-1][0]].launch_info()["variant"]})
+        ks = [e["kernel_ms_per_frame"] for e in every]
+        walls = [e["render_wall_ms"] for e in every]
+        ranks_detail = {"kernel_ms_per_frame": {"per_rank": ks, "min": min(ks), "max": max(ks),
+                                                "spread": max(ks) / min(ks) - 1.0 if min(ks) > 0 else None},
+                        "render_wall_ms": {"per_rank": walls, "max": max(walls)},
+                        "variant_per_rank": [e["variant"] for e in every]}
     # whole-job rays of the timed launches: each launch's count (the counters of a launch of that many frames of
     # the camera path) summed over the plan and over the ranks (rotated rows: a rank's share differs frame by
     # frame, the frames' totals do not)
@@ -528,6 +553,14 @@ def main():
     elapsed = el.item()
     rays_total = int(rays_t.item())
     rays_frame = rays_total / K
+    if ranks_detail is not None:
+        ranks_detail["wall_ms"] = elapsed * 1e3
+        ranks_detail["exposed_gather_ms"] = elapsed * 1e3 - ranks_detail["render_wall_ms"]["max"]
+        ranks_detail["gather_mode"] = gmode
+        ranks_detail["rule"] = ("kernel_ms_per_frame: each rank's median HIP-event time of its timed full-size launches "
+                                "/ frames per launch; render_wall_ms: each rank's wall time for the timed plan's launches "
+                                "without their gathers (timed alone after the timed region); exposed_gather_ms = the "
+                                "timed region's wall time (max over ranks) - the slowest rank's render_wall_ms")
 
     # algorithmic bytes of this rank's full-batch launch: one extra untimed launch with traversal counters
     # (the timed launches' own configuration; a hybrid single frame's counters are its whole-frame kernel's, or
@@ -663,6 +696,7 @@ def main():
                        if world > 1 else "single GPU", "frames_per_launch": F, "gather": gather_note,
                        # the native gather's communicator over the whole run: gathers, row-set exchanges (1 per layout)
                        "gather_comm": ng.info() if ng else None,
+                       "gather_mode": gmode, "ranks": ranks_detail,
                        "launch": timed_launch, "accel_built": info["accel_built"], "accel_build_ms": info["build_ms"],
                        "wide_depth": info["wide_depth"]},
             "frame_latency_ms": lat.item() if not args.no_latency else None,

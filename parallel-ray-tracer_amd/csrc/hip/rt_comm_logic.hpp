@@ -103,4 +103,34 @@ Wait bounded_wait(Query query, double timeout_s, int& err) {
     }
 }
 
+// A communicator's outstanding send / recv groups, waited for in issue order (rt_comm_wait, the exchange and coverage
+// waits of a gather, and any host wait on a stream that holds a group: rt_sync, rt_download, ...). Group j's local
+// part -- the render before it, marked by its `pre` event -- depends only on this rank's own work once group j - 1 has
+// completed, so it is waited for without a deadline; the deadline covers the collective itself and starts when the
+// local part has completed. A long render (a 64-spp 4K frame) therefore never turns into a timeout, and a peer that
+// never joins still does. pre(j) / done(j): 0 complete, 1 not yet, < 0 an error (returned in err).
+// Returns Done with n_done = n, else the Error or Timeout of group n_done (groups 0 .. n_done - 1 completed).
+template <class PreQ, class DoneQ>
+Wait settle(int n, PreQ pre, DoneQ done, double timeout_s, int& err, int& n_done) {
+    using clk = std::chrono::steady_clock;
+    n_done = 0;
+    for (int j = 0; j < n; j++) {
+        const auto t0 = clk::now();
+        for (;;) {  // the local part: no deadline (spin ~200 us, then sleep between polls)
+            const int q = pre(j);
+            if (q == 0) break;
+            if (q < 0) {
+                err = q;
+                return Wait::Error;
+            }
+            if (std::chrono::duration<double>(clk::now() - t0).count() > 2e-4)
+                std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+        const Wait w = bounded_wait([&] { return done(j); }, timeout_s, err);
+        if (w != Wait::Done) return w;
+        n_done = j + 1;
+    }
+    return Wait::Done;
+}
+
 }  // namespace rtc

@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -53,6 +54,14 @@ struct HostView {
     std::vector<int2> leaves;
     std::vector<int> orig;
     int root = 0;
+};
+
+// The multi-process communicator whose send / recv groups a context's stream holds (rt_ctx::comm_link): shared by both,
+// so that a host wait on that stream (rt_sync, rt_download, rt_destroy, ...) first waits, bounded, for the
+// communicator's outstanding groups -- a peer that never joins turns into RT_E_TIMEOUT there too, not into a hang --
+// and so that either side may be destroyed first (rt_comm_destroy clears cm).
+struct CommLink {
+    rt_comm* cm = nullptr;
 };
 
 }  // namespace
@@ -133,6 +142,7 @@ struct rt_ctx {
     hipEvent_t copy_ev = nullptr;             // rt_gather: this (source) context's peer copies issued
     long long launches = 0;
     bool rendered = false;
+    std::shared_ptr<CommLink> comm_link;  // the communicator with a send / recv group on this stream (CommLink)
     // the default rule of frame batches and spp > 1 (PERSIST4 or SHPOOL), measured per shape (render_batch)
     struct BatchRule {
         long long scene = -1;
@@ -1827,10 +1837,14 @@ extern "C" int rt_get_launch_info(rt_ctx* ctx, rt_launch_info* info) {
 }
 
 namespace {
+int comm_settle_ctx(rt_ctx* ctx, const char* who);  // (below, with the communicators)
 // Waits for the context stream; with a render behind it, reads that render's error counter (rtd::C_ERR: a traversal
 // stack overflowed, rt_kernels.hpp) in the same wait, so that a frame computed with a truncated walk never passes as
-// good: RT_E_KERNEL.
+// good: RT_E_KERNEL. A stream holding a multi-process gather's send / recv group is first waited for through the
+// communicator's bounded wait (comm_settle): a peer that never joins fails the call with RT_E_TIMEOUT instead of
+// blocking in hipStreamSynchronize.
 int sync_checked(rt_ctx* ctx, const char* who) {
+    if (int rc = comm_settle_ctx(ctx, who)) return rc;
     if (ctx->rendered)
         HIPC(hipMemcpyAsync(ctx->h_err, ctx->d_counters + rtd::C_ERR, sizeof(unsigned long long), hipMemcpyDeviceToHost,
                             ctx->stream));
@@ -1858,6 +1872,7 @@ extern "C" int rt_sync(rt_ctx* ctx, float* kernel_ms) {
 extern "C" int rt_kernel_times(rt_ctx* ctx, float* ms, int n) {
     if (!ctx || !ms || n < 0) return RT_E_ARG;
     HIPC(hipSetDevice(ctx->device));
+    if (int rc = comm_settle_ctx(ctx, "rt_kernel_times")) return rc;
     HIPC(hipStreamSynchronize(ctx->stream));
     long long avail = ctx->launches < rt_ctx::NEV ? ctx->launches : rt_ctx::NEV;
     if (n > avail) n = (int)avail;
@@ -2111,6 +2126,15 @@ struct rt_comm {
     hipStream_t side = nullptr;  // the exchange's stream: the host waits for the exchange only, not for renders
     hipEvent_t done = nullptr;   // after the last send / recv group: the next operation on the communicator waits
     bool issued = false;
+    // the issued send / recv groups not yet seen complete, oldest first: `pre` recorded on the source's stream before
+    // the group (after its render: the group's local part), `done` after it (rtc::settle: the deadline covers the
+    // collective, not the render before it); events reused from ev_pool
+    struct Pending {
+        hipEvent_t pre, done;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> ev_pool;
+    std::shared_ptr<CommLink> link = std::make_shared<CommLink>();
     bool aborted = false;     // a collective missed its deadline: the communicator was aborted (ncclCommAbort)
     double timeout_s = 120.0;  // host waits on a collective (rt_comm_set_timeout)
     rt_comm_info info{};
@@ -2169,12 +2193,13 @@ Rccl& rccl() {
 
 int comm_fail(rt_comm* cm, ncclResult_t r, const char* what) {
     cm->err = std::string(what) + ": " + (rccl().GetErrorString ? rccl().GetErrorString(r) : "RCCL error");
-    if (!cm->ctxs.empty() && cm->ctxs[0]) cm->ctxs[0]->err = cm->err;
+    if (!cm->ctxs.empty() && cm->ctxs[0]) cm->ctxs[0]->err = cm->err;  // (null: that context was destroyed)
     return RT_E_HIP;
 }
 int comm_arg(rt_comm* cm, const std::string& what) {
     cm->err = what;
-    for (rt_ctx* c : cm->ctxs) c->err = what;
+    for (rt_ctx* c : cm->ctxs)
+        if (c) c->err = what;
     return RT_E_ARG;
 }
 #define NCCLC(call)                                       \
@@ -2194,7 +2219,14 @@ int comm_abort(rt_comm* cm, const std::string& what) {
         }
     cm->aborted = true;
     cm->err = what;
-    for (rt_ctx* c : cm->ctxs) c->err = what;
+    for (rt_ctx* c : cm->ctxs)
+        if (c) c->err = what;
+    // (the aborted groups' kernels stop waiting, the streams drain: nothing outstanding is waited for again)
+    for (const rt_comm::Pending& p : cm->pending) {
+        cm->ev_pool.push_back(p.pre);
+        cm->ev_pool.push_back(p.done);
+    }
+    cm->pending.clear();
     return RT_E_TIMEOUT;
 }
 // A host wait on work behind a collective (a stream or an event), bounded by the communicator's timeout
@@ -2216,11 +2248,80 @@ int comm_wait(rt_comm* cm, Q query_hip, const char* what) {
     if (w == rtc::Wait::Done) return RT_OK;
     if (w == rtc::Wait::Error) {
         cm->err = std::string(what) + ": " + hipGetErrorString((hipError_t)(-err));
-        for (rt_ctx* c : cm->ctxs) c->err = cm->err;
+        for (rt_ctx* c : cm->ctxs)
+            if (c) c->err = cm->err;
         return RT_E_HIP;
     }
     return comm_abort(cm, std::string(what) + ": no completion within " + std::to_string(cm->timeout_s) +
                               " s (a peer rank never joined the collective); the communicator is aborted");
+}
+
+int event_state(hipEvent_t e) {  // rtc query convention: 0 complete, 1 not yet, < 0 -(hipError_t)
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) return 0;
+    if (q == hipErrorNotReady) {
+        (void)hipGetLastError();  // not an error: still running
+        return 1;
+    }
+    return -(int)q;
+}
+
+// Waits for every outstanding send / recv group of a multi-process communicator, in issue order (rtc::settle): each
+// group's render without a deadline, its collective within the communicator's timeout from the moment that render has
+// completed. RT_E_TIMEOUT (the communicator aborted) when a peer never joins.
+int comm_settle(rt_comm* cm, const char* what) {
+    if (cm->aborted) {
+        cm->err = std::string(what) + ": the communicator was aborted";
+        return RT_E_TIMEOUT;
+    }
+    if (cm->pending.empty()) return RT_OK;
+    (void)hipSetDevice(cm->devices[0]);
+    int err = 0, n_done = 0;
+    const rtc::Wait w = rtc::settle((int)cm->pending.size(), [&](int j) { return event_state(cm->pending[j].pre); },
+                                    [&](int j) { return event_state(cm->pending[j].done); }, cm->timeout_s, err, n_done);
+    for (int j = 0; j < n_done; j++) {
+        cm->ev_pool.push_back(cm->pending[j].pre);
+        cm->ev_pool.push_back(cm->pending[j].done);
+    }
+    cm->pending.erase(cm->pending.begin(), cm->pending.begin() + n_done);
+    if (w == rtc::Wait::Done) return RT_OK;
+    if (w == rtc::Wait::Error) {
+        cm->err = std::string(what) + ": " + hipGetErrorString((hipError_t)(-err));
+        for (rt_ctx* c : cm->ctxs)
+            if (c) c->err = cm->err;
+        return RT_E_HIP;
+    }
+    return comm_abort(cm, std::string(what) + ": a gather's collective did not complete within " +
+                              std::to_string(cm->timeout_s) +
+                              " s of its render (a peer rank never joined it); the communicator is aborted");
+}
+// the same for a context whose stream holds a group (sync_checked, rt_kernel_times, rt_destroy)
+int comm_settle_ctx(rt_ctx* ctx, const char* who) {
+    if (!ctx->comm_link || !ctx->comm_link->cm) return RT_OK;
+    rt_comm* cm = ctx->comm_link->cm;
+    if (cm->aborted) return RT_OK;  // (aborted: its groups no longer block the stream)
+    const int rc = comm_settle(cm, who);
+    (void)hipSetDevice(ctx->device);
+    if (rc) ctx->err = cm->err;
+    return rc;
+}
+// completed groups off the front of the list, without waiting (each gather: the list stays short)
+void comm_prune(rt_comm* cm) {
+    size_t k = 0;
+    while (k < cm->pending.size() && event_state(cm->pending[k].done) == 0) {
+        cm->ev_pool.push_back(cm->pending[k].pre);
+        cm->ev_pool.push_back(cm->pending[k].done);
+        k++;
+    }
+    cm->pending.erase(cm->pending.begin(), cm->pending.begin() + k);
+}
+hipError_t comm_event(rt_comm* cm, hipEvent_t* e) {
+    if (!cm->ev_pool.empty()) {
+        *e = cm->ev_pool.back();
+        cm->ev_pool.pop_back();
+        return hipSuccess;
+    }
+    return hipEventCreateWithFlags(e, hipEventDisableTiming);
 }
 }  // namespace
 
@@ -2324,6 +2425,9 @@ int comm_gather_multi(rt_comm* cm, rt_ctx* src, int root, void* d_dst) {
                             "(frame size, frame count, pixel kind): call rt_comm_relayout on every rank first");
     const bool fresh = step == rtc::Step::Exchange;
     if (fresh) {  // a new layout: exchange the 64-B descriptors (ncclAllGather) and check that they partition the frames
+        // (the groups before it first: their renders unbounded, their collectives bounded -- the exchange's own
+        // deadline then covers the AllGather only)
+        if (int rc = comm_settle(cm, "rt_comm_gather: the gathers before a row-set exchange")) return rc;
         cm->h_desc[cm->nranks] = mine;
         if (cm->issued) HIPC(hipStreamWaitEvent(cm->side, cm->done, 0));
         HIPC(hipMemcpyAsync(cm->d_desc + cm->nranks, cm->h_desc + cm->nranks, sizeof(Part), hipMemcpyHostToDevice, cm->side));
@@ -2360,6 +2464,16 @@ int comm_gather_multi(rt_comm* cm, rt_ctx* src, int root, void* d_dst) {
     const size_t full_px = (size_t)a.frames * a.W * a.H;
     if (is_root && fresh)  // coverage check of a layout's first gather: no render writes this value (k_count_unwritten)
         HIPC(hipMemsetAsync(dst, words == 1 ? 0 : 0xFF, full_px * 4 * words, ctx->stream));
+    comm_prune(cm);
+    rt_comm::Pending pend{};
+    HIPC(comm_event(cm, &pend.pre));
+    if (hipError_t e = comm_event(cm, &pend.done); e != hipSuccess) {
+        cm->ev_pool.push_back(pend.pre);
+        return fail(ctx, e, "rt_comm_gather: events");
+    }
+    cm->ev_pool.push_back(pend.pre);  // (back to the pool unless the group is issued below)
+    cm->ev_pool.push_back(pend.done);
+    HIPC(hipEventRecord(pend.pre, ctx->stream));  // the group's local part (the render) ends here
     NCCLC(rccl().GroupStart());
     if (!is_root) {
         NCCLC(rccl().Send(payload_of(ctx), part_px(ps[cm->rank0]) * words, ncclUint32, root, cm->comms[0], ctx->stream));
@@ -2370,6 +2484,11 @@ int comm_gather_multi(rt_comm* cm, rt_ctx* src, int root, void* d_dst) {
     }
     NCCLC(rccl().GroupEnd());
     HIPC(hipEventRecord(cm->done, ctx->stream));
+    cm->ev_pool.pop_back();
+    cm->ev_pool.pop_back();
+    HIPC(hipEventRecord(pend.done, ctx->stream));
+    cm->pending.push_back(pend);
+    ctx->comm_link = cm->link;
     cm->issued = true;
     cm->info.gathers++;
     if (!is_root) return RT_OK;
@@ -2386,6 +2505,8 @@ int comm_gather_multi(rt_comm* cm, rt_ctx* src, int root, void* d_dst) {
         rtd::k_count_unwritten<<<grid, 256, 0, ctx->stream>>>((const unsigned*)dst, full_px, words, cm->d_count);
         HIPC(hipGetLastError());
         HIPC(hipMemcpyAsync(&left, cm->d_count, sizeof left, hipMemcpyDeviceToHost, ctx->stream));
+        // the group (its render unbounded, its collective bounded), then the local unshuffle and count behind it
+        if (int rc2 = comm_settle(cm, "rt_comm_gather: coverage check")) return rc2;
         if (int rc2 = comm_wait(cm, [&] { return hipStreamQuery(ctx->stream); }, "rt_comm_gather: coverage check"))
             return rc2;
         cm->info.checked++;
@@ -2400,7 +2521,8 @@ extern "C" int rt_comm_gather_from(rt_comm* cm, rt_ctx* src, int root, void* d_d
     if (!cm || root < 0 || root >= cm->nranks) return RT_E_ARG;
     if (cm->multi) {
         if (!src) src = cm->ctxs[0];
-        if (src->device != cm->ctxs[0]->device)
+        if (!src) return comm_arg(cm, "rt_comm_gather_from: the communicator's context was destroyed");
+        if (src->device != cm->devices[0])
             return comm_arg(cm, "rt_comm_gather_from: the context is not on the communicator's device");
         return comm_gather_multi(cm, src, root, d_dst);
     }
@@ -2409,7 +2531,7 @@ extern "C" int rt_comm_gather_from(rt_comm* cm, rt_ctx* src, int root, void* d_d
     // one process: every rank's descriptor at hand
     std::vector<Part> ps(cm->nranks);
     for (rt_ctx* c : cm->ctxs)
-        if (!c->rendered) return comm_arg(cm, "rt_comm_gather: a context has not rendered");
+        if (!c || !c->rendered) return comm_arg(cm, "rt_comm_gather: a context has not rendered (or was destroyed)");
     for (int i = 0; i < nl; i++) ps[i] = part_of(cm->ctxs[i]);
     const std::string why = check_parts(ps);
     if (!why.empty()) return comm_arg(cm, "rt_comm_gather: " + why);
@@ -2475,6 +2597,7 @@ extern "C" int rt_comm_wait(rt_comm* cm) {
     if (cm->aborted) return RT_E_TIMEOUT;
     if (!cm->issued || !cm->done) return RT_OK;
     (void)hipSetDevice(cm->devices[0]);
+    if (cm->multi) return comm_settle(cm, "rt_comm_wait: the gathers issued");
     return comm_wait(cm, [&] { return hipEventQuery(cm->done); }, "rt_comm_wait: the last gather");
 }
 
@@ -2503,6 +2626,9 @@ extern "C" void rt_comm_destroy(rt_comm* cm) {
     if (cm->h_desc) (void)hipHostFree(cm->h_desc);
     if (cm->side) (void)hipStreamDestroy(cm->side);
     if (cm->done) (void)hipEventDestroy(cm->done);
+    for (const rt_comm::Pending& p : cm->pending) cm->ev_pool.insert(cm->ev_pool.end(), {p.pre, p.done});
+    for (hipEvent_t e : cm->ev_pool) (void)hipEventDestroy(e);
+    cm->link->cm = nullptr;  // (the contexts that still hold the link see the communicator gone)
     delete cm;
 }
 
@@ -2575,6 +2701,12 @@ extern "C" const char* rt_last_error(rt_ctx* ctx) { return ctx ? ctx->err.c_str(
 extern "C" void rt_destroy(rt_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    // a send / recv group on this stream: waited for through the communicator (bounded; aborted if a peer never
+    // joins), and the communicator forgets this context
+    (void)comm_settle_ctx(ctx, "rt_destroy");
+    if (ctx->comm_link && ctx->comm_link->cm)
+        for (rt_ctx*& c : ctx->comm_link->cm->ctxs)
+            if (c == ctx) c = nullptr;
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     free_scene(ctx);
     if (ctx->gather_ev) (void)hipEventDestroy(ctx->gather_ev);

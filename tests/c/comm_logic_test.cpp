@@ -91,6 +91,33 @@ int main() {
         CHECK(cm.wait([&] { return -700; }) == -700);
         CHECK(!cm.aborted);
     }
+    {  // settle: a render (the local part) far longer than the timeout does not abort; the collective after it is bounded
+        using ms = std::chrono::milliseconds;
+        const double timeout = 0.05;
+        const auto t0 = clk::now();
+        auto at = [&](double s) { return std::chrono::duration<double>(clk::now() - t0).count() >= s ? 0 : 1; };
+        int err = 0, n_done = -1;
+        // group 0: render done at 0.30 s (6x the timeout), collective 10 ms later; group 1: render at 0.35, done 0.36
+        const double pre_t[2] = {0.30, 0.35}, done_t[2] = {0.31, 0.36};
+        rtc::Wait w = rtc::settle(2, [&](int j) { return at(pre_t[j]); }, [&](int j) { return at(done_t[j]); }, timeout,
+                                  err, n_done);
+        const double el = std::chrono::duration<double>(clk::now() - t0).count();
+        CHECK(w == rtc::Wait::Done && n_done == 2);
+        CHECK(el >= 0.36 && el < 2.0);
+        std::printf("settle: a 0.30 s render under a %.2f s timeout completes (%.3f s)\n", timeout, el);
+        // a peer that never joins group 1: group 0 completes, group 1 times out one timeout after its render
+        const auto t1 = clk::now();
+        auto since = [&](double s) { return std::chrono::duration<double>(clk::now() - t1).count() >= s ? 0 : 1; };
+        w = rtc::settle(2, [&](int j) { return since(j == 0 ? 0.02 : 0.1); }, [&](int j) { return j == 0 ? since(0.03) : 1; },
+                        timeout, err, n_done);
+        const double el1 = std::chrono::duration<double>(clk::now() - t1).count();
+        CHECK(w == rtc::Wait::Timeout && n_done == 1);
+        CHECK(el1 >= 0.1 + timeout && el1 < 2.0);
+        // an error in a render: reported as such
+        w = rtc::settle(1, [&](int) { return -700; }, [&](int) { return 0; }, timeout, err, n_done);
+        CHECK(w == rtc::Wait::Error && err == -700 && n_done == 0);
+        (void)ms(0);
+    }
     {  // layout decisions of two ranks over a gather sequence; rank 1 toggles its hit output
         const int W = 64, H = 40;
         Part last[2] = {};

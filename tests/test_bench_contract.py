@@ -81,6 +81,13 @@ def test_bench_two_ranks_on_one_gpu_count_the_whole_frame(tmp_path):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 4
     assert d["config"]["gather"].startswith("torch.distributed")  # gloo: the native RCCL gather needs one GPU per rank
+    # the N > 1 diagnostics: each rank's kernel time, the render-only walls, the exposed gather, the gather that ran
+    rk = d["config"]["ranks"]
+    assert d["config"]["gather_mode"] == rk["gather_mode"] == "torch"
+    assert len(rk["kernel_ms_per_frame"]["per_rank"]) == 2 and rk["kernel_ms_per_frame"]["min"] > 0
+    assert rk["kernel_ms_per_frame"]["spread"] >= 0 and len(rk["render_wall_ms"]["per_rank"]) == 2
+    assert rk["wall_ms"] > 0 and abs(rk["exposed_gather_ms"] - (rk["wall_ms"] - rk["render_wall_ms"]["max"])) < 1e-6
+    assert len(rk["variant_per_rank"]) == 2
     one = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline"] + args,
                          capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert one.returncode == 0, one.stderr[-3000:]

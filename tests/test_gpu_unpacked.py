@@ -57,10 +57,12 @@ def render(name, W, H, kernel, flags, counters=False):
 
 
 def expected_bits(kernel, fl):
-    """the RT_BUILD_* bits persist_kernel must report for a forced variant under unpacked flags `fl`"""
+    """the RT_BUILD_* bits persist_kernel must report for a forced variant under unpacked flags `fl` (lds_paths aside:
+    the unpacked PERSIST4 keeps its path levels in LDS only where its two-word stack entries leave room for 4 workgroups
+    per CU, and otherwise in a global slab)"""
     if kernel == "persist":  # the 3-wave spp = 1 build: packed triangle tests unless they are refused
         return {"packed_tris"} if fl == "stack" else set()
-    return {"waves4", "lds_paths"}  # PERSIST4 / SHPOOL / SHDEFER: the unpacked PERSIST4 (the pools need both packings)
+    return {"waves4"}  # PERSIST4 / SHPOOL / SHDEFER: the unpacked PERSIST4 (the pools need both packings)
 
 
 @pytest.mark.parametrize("fl", ["stack", "tris", "both"])
@@ -69,7 +71,7 @@ def expected_bits(kernel, fl):
 @pytest.mark.parametrize("W,H", [(64, 36), (160, 90)])
 def test_unpacked_builds_vs_reference_fixture(name, W, H, kernel, fl):
     out = render(name, W, H, kernel, flag_sets()[fl])
-    assert set(out["launch"]["build_bits"]) == expected_bits(kernel, fl), out["launch"]
+    assert set(out["launch"]["build_bits"]) - {"lds_paths"} == expected_bits(kernel, fl), out["launch"]
     ref = np.load(os.path.join(GOLD, f"{name}_{W}x{H}_strict.npz"))
     np.testing.assert_array_equal(out["hit"], ref["hit"])
     assert same_bits(out["t"], ref["t"])
