@@ -487,9 +487,41 @@ __device__ __forceinline__ WNode wload(const DWide& W, int node, const float4* t
     const float4* N = (top && node < NTOP) ? top + 5 * node : W.nodes + 5 * node;
     return WNode{N[0], N[1], N[2], N[3], N[4]};
 }
+// The walks' node array as a value held in scalar registers for the whole walk (PRT_PIN_BASE): read from the kernel
+// arguments once. Without it the compiler, short of scalar registers, re-read W.nodes from the kernel arguments at
+// every step (an s_load rematerialised instead of a spill), and that load's s_waitcnt lgkmcnt(0) sat between the
+// stack pop and the next node's loads, waiting for every LDS operation of the step as well. The view of a walk is
+// the same for every lane of the wave (the bounce level or the pool's fixed view decides it).
+#ifndef PRT_PIN_BASE
+#define PRT_PIN_BASE 1
+#endif
+// (a global-address-space pointer: its loads stay global_load, which the compiler waits for by vmcnt alone; a generic
+// pointer's flat loads are waited for with lgkmcnt too)
+typedef const pin4 __attribute__((address_space(1))) * gnodes;
+__device__ __forceinline__ gnodes walk_base(const float4* p) {
+    unsigned long long v = (unsigned long long)p;
+    if (PRT_PIN_BASE) __asm__ volatile("" : "+s"(v));
+    return (gnodes)v;
+}
+__device__ __forceinline__ float4 f4(pin4 v) { return make_float4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ WNode wload_at(gnodes base, int node, const float4* top = nullptr) {
+    if (LDS_TOP && top && node < NTOP) {
+        const float4* N = top + 5 * node;
+        return WNode{N[0], N[1], N[2], N[3], N[4]};
+    }
+    gnodes N = base + 5 * node;
+    return WNode{f4(N[0]), f4(N[1]), f4(N[2]), f4(N[3]), f4(N[4])};
+}
 
 
-template <bool COUNT>
+// LATE (PRT_LATE_TRIS): th returns the hit leaf SLOTS (bits 0..7) and the walk forms the triangle bits from them with
+// leaf_tris after it has issued the next node's loads (the slot loop is off the dependent chain from this node's
+// loads to the next node's)
+#ifndef PRT_LATE_TRIS
+#define PRT_LATE_TRIS 1
+#endif
+constexpr bool LATE_TRIS = PRT_LATE_TRIS != 0;
+template <bool COUNT, bool LATE = false>
 __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsigned oct, float lim, unsigned& nh,
                                           unsigned& th, int& cbase, int& tbase, unsigned& imask, unsigned& nleaf,
                                           unsigned ord_xor = 0u) {
@@ -555,6 +587,10 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
     unsigned lh = hit8 & ~imask;
     th = 0;
     nleaf = 0;
+    if constexpr (LATE) {  // (the slots; leaf_tris later)
+        th = lh;
+        return;
+    }
     while (lh) {
         const unsigned sl = (unsigned)__builtin_ctz(lh);
         lh &= lh - 1u;
@@ -562,6 +598,22 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
         th |= ((1u << (meta >> 5)) - 1u) << (meta & 31u);
         if (COUNT) nleaf += meta ? 1u : 0u;
     }
+}
+
+// The triangle bits (relative to the node's tri base) of hit leaf slots lh, from the node's meta words m0 / m1 (f1.z,
+// f1.w): wide_node's loop, for the LATE walks
+template <bool COUNT>
+__device__ __forceinline__ unsigned leaf_tris(unsigned lh, unsigned m0, unsigned m1, unsigned& nleaf) {
+    unsigned th = 0;
+    nleaf = 0;
+    while (lh) {
+        const unsigned sl = (unsigned)__builtin_ctz(lh);
+        lh &= lh - 1u;
+        const unsigned meta = ((sl < 4u ? m0 : m1) >> (8u * (sl & 3u))) & 0xFFu;
+        th |= ((1u << (meta >> 5)) - 1u) << (meta & 31u);
+        if (COUNT) nleaf += meta ? 1u : 0u;
+    }
+    return th;
 }
 
 // The node visited after this one: the nearest remaining hit child of this node, else the top group
@@ -600,6 +652,71 @@ __device__ __forceinline__ int wide_next(unsigned nh, int cb, unsigned imask, un
         ++sp;
     }
     return cb + __popc(imask & ((1u << slot) - 1u));
+}
+
+// wide_next with the stack's top entry cached in registers (PRT_TOP_CACHE): (t0, t1) hold the LDS words of entry sp - 1
+// as the previous step left them, read back after every step's stack update, so that a pop takes its entry from
+// registers instead of waiting for an LDS read on the chain from this node's loads to the next node's. The read-back
+// is unconditional (its result is used only by a later pop, whose wait it has long passed) -- a load under a branch
+// merged into loop-carried registers would be waited for at the merge.
+#ifndef PRT_TOP_CACHE
+#define PRT_TOP_CACHE 0
+#endif
+constexpr bool TOP_CACHE = PRT_TOP_CACHE != 0;
+struct TopC {
+    unsigned t0 = 0, t1 = 0;
+};
+template <bool PK = false>
+__device__ __forceinline__ int wide_next_tc(unsigned nh, int cb, unsigned imask, unsigned oct, int& sp, TopC& tc,
+                                            int* __restrict__ stk, int wcap = WSTACK) {
+    if (!nh) {
+        if (sp == 0) return -1;
+        --sp;
+        if constexpr (PK) {
+            cb = (int)(tc.t0 >> 8);
+            nh = tc.t0 & 0xFFu;
+            imask = tc.t1 & 0xFFu;
+        } else {
+            cb = (int)tc.t0;
+            imask = tc.t1 >> 8;
+            nh = tc.t1 & 0xFFu;
+        }
+    }
+    const unsigned slot = (unsigned)__builtin_ctz(nh) ^ oct;
+    nh &= nh - 1u;
+    if (nh) {
+        if (sp >= wcap) return -2;
+        if constexpr (PK) {
+            stk[sp * BLOCK] = (int)(((unsigned)cb << 8) | nh);
+            reinterpret_cast<unsigned char*>(stk + (wcap + (sp >> 2)) * BLOCK)[sp & 3] = (unsigned char)imask;
+        } else {
+            stk[(2 * sp) * BLOCK] = cb;
+            stk[(2 * sp + 1) * BLOCK] = (int)((imask << 8) | nh);
+        }
+        ++sp;
+    }
+    return cb + __popc(imask & ((1u << slot) - 1u));
+}
+// the top entry's read-back (TOP_CACHE), placed after the next node's loads are issued: its LDS waits never delay them
+template <bool PK>
+__device__ __forceinline__ void top_reload(int sp, TopC& tc, const int* __restrict__ stk, int wcap) {
+    if constexpr (TOP_CACHE) {
+        const int ti = sp > 0 ? sp - 1 : 0;  // (sp == 0: a word no pop reads)
+        if constexpr (PK) {
+            tc.t0 = (unsigned)stk[ti * BLOCK];
+            tc.t1 = reinterpret_cast<const unsigned char*>(stk + (wcap + (ti >> 2)) * BLOCK)[ti & 3];
+        } else {
+            tc.t0 = (unsigned)stk[(2 * ti) * BLOCK];
+            tc.t1 = (unsigned)stk[(2 * ti + 1) * BLOCK];
+        }
+    }
+}
+// the walks' step: wide_next or wide_next_tc (then top_reload after the next node's loads)
+template <bool PK>
+__device__ __forceinline__ int wide_step_next(unsigned nh, int cb, unsigned imask, unsigned oct, int& sp, TopC& tc,
+                                              int* __restrict__ stk, int wcap) {
+    if constexpr (TOP_CACHE) return wide_next_tc<PK>(nh, cb, imask, oct, sp, tc, stk, wcap);
+    else return wide_next<PK>(nh, cb, imask, oct, sp, stk, wcap);
 }
 
 // A wave's LDS queue of packed triangle tests (TQ): TQ_CAP jobs (owner lane << 26 | triangle), then 128 words of
@@ -771,23 +888,28 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
     const RayPre p = ray_pre(o, d);
     const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
     int sp = 0;
-    WNode N = wload(W, 0, top);
+    TopC tc;
+    const gnodes nbase = walk_base(W.nodes);
+    WNode N = wload_at(nbase, 0, top);
     for (;;) {
         unsigned nh, th, imask, nl;
         int cb, tb;
         pin_node(N);
-        wide_node<COUNT>(N, p, oct, best * PRUNE_SLACK, nh, th, cb, tb, imask, nl);
+        wide_node<COUNT, LATE_TRIS>(N, p, oct, best * PRUNE_SLACK, nh, th, cb, tb, imask, nl);
+        const unsigned m0 = __float_as_uint(N.f1.z), m1 = __float_as_uint(N.f1.w);
+        const int next = wide_step_next<PK>(nh, cb, imask, oct, sp, tc, stk, wcap);
+        // the next node's loads go out before this node's triangle tests, unconditionally (a walk that has ended
+        // reloads the root): a load under a branch is copied into the merged register right after it, and that
+        // copy waits for the load (dragon 0.712 -> 0.689 ms per frame, sportscar 0.931 -> 0.901, car_boxed 0.870 -> 0.858)
+        N = wload_at(nbase, next >= 0 ? next : 0, top);
+        top_reload<PK>(sp, tc, stk, wcap);
+        if constexpr (LATE_TRIS) th = leaf_tris<COUNT>(th, m0, m1, nl);
         if (COUNT) {
             c.chi++;
             c.chl += nl;
             c.nb += 10;
             count_step(c, false);
         }
-        const int next = wide_next<PK>(nh, cb, imask, oct, sp, stk, wcap);
-        // the next node's loads go out before this node's triangle tests, unconditionally (a walk that has ended
-        // reloads the root): a load under a branch is copied into the merged register right after it, and that
-        // copy waits for the load (dragon 0.712 -> 0.689 ms per frame, sportscar 0.931 -> 0.901, car_boxed 0.870 -> 0.858)
-        N = wload(W, next >= 0 ? next : 0, top);
         if constexpr (TQ) {
             if (__builtin_amdgcn_readfirstlane((int)(__ballot(__builtin_popcount(th) >= TQ_MIN) != 0ull)) &&
                 closest_tris_packed<COUNT>(W, o, d, th, tb, best, hp, nd, tie, tq, c))
@@ -859,20 +981,26 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
     float best = FMAX;
     const float reach = shadow_reach(o, ld2);
     int sp = 0;
-    WNode N = wload(W, 0, top);
+    TopC tc;
+    const gnodes nbase = walk_base(W.nodes);
+    WNode N = wload_at(nbase, 0, top);
     for (;;) {
         unsigned nh, th, imask, nl;
         int cb, tb;
         pin_node(N);
-        wide_node<COUNT>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nl, SHADOW_ORDER_XOR);
+        wide_node<COUNT, LATE_TRIS>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nl,
+                                    SHADOW_ORDER_XOR);
+        const unsigned m0 = __float_as_uint(N.f1.z), m1 = __float_as_uint(N.f1.w);
+        const int next = wide_step_next<PK>(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, tc, stk, wcap);
+        N = wload_at(nbase, next >= 0 ? next : 0, top);  // unconditional (closest_wide)
+        top_reload<PK>(sp, tc, stk, wcap);
+        if constexpr (LATE_TRIS) th = leaf_tris<COUNT>(th, m0, m1, nl);
         if (COUNT) {
             c.shi++;
             c.shl += nl;
             c.nb += 10;
             count_step(c, true);
         }
-        const int next = wide_next<PK>(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
-        N = wload(W, next >= 0 ? next : 0, top);  // unconditional (closest_wide)
         if constexpr (TQ) {
             bool occ = false;
             if (__builtin_amdgcn_readfirstlane((int)(__ballot(__builtin_popcount(th) >= TQ_MIN) != 0ull)) &&

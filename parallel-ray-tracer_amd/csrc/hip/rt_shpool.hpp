@@ -97,6 +97,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
     const unsigned long long all = uni64(__ballot(1));
     const int nl = s.n_lights;
     const DWide& W = wide_for(s, true);  // |d| = 1: the unit-direction view
+    const gnodes nbase = walk_base(W.nodes);
     // the cursor (wave-uniform): level cl, light cj, and the owner lanes whose ray toward it is still unassigned
     int cl = 0, cj = -1;
     unsigned long long cm = 0;
@@ -120,6 +121,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
     unsigned oct = 0;
     float ld2 = 0.0f, reach = 0.0f, best = FMAX;
     int sp = 0;
+    TopC tc;
     WNode N = {};
     for (;;) {
         advance();
@@ -169,7 +171,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
                     best = FMAX;
                     reach = shadow_reach(o, ld2);
                     sp = 0;
-                    N = wload(W, 0, c.top[1]);
+                    N = wload_at(nbase, 0, c.top[1]);
                     busy = true;
                 }
             }
@@ -184,15 +186,19 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
                 unsigned nh, imask, nlf;
                 int cb;
                 pin_node(N);
-                wide_node<COUNT>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nlf, SHADOW_ORDER_XOR);
+                wide_node<COUNT, LATE_TRIS>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nlf,
+                                            SHADOW_ORDER_XOR);
+                const unsigned m0 = __float_as_uint(N.f1.z), m1 = __float_as_uint(N.f1.w);
+                next = wide_step_next<true>(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, tc, stk, wcap);
+                N = wload_at(nbase, next >= 0 ? next : 0, c.top[1]);  // unconditional (closest_wide)
+                top_reload<true>(sp, tc, stk, wcap);
+                if constexpr (LATE_TRIS) th = leaf_tris<COUNT>(th, m0, m1, nlf);
                 if (COUNT) {
                     c.shi++;
                     c.shl += nlf;
                     c.nb += 10;
                     count_step(c, true);
                 }
-                next = wide_next<true>(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, stk, wcap);
-                N = wload(W, next >= 0 ? next : 0, c.top[1]);  // unconditional (closest_wide)
             }
             bool occ = false, seq = true;
             if constexpr (TQ) {

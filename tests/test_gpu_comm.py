@@ -185,3 +185,31 @@ def test_rccl_rank_comm_refuses_a_partial_layout(dev, scene):
         comm.gather(0, torch.zeros((1, H, W), dtype=torch.int32, device="cuda"), src=r)
     comm.close()
     r.close()
+
+
+def test_rccl_rank_comm_deadline_does_not_cover_the_render(dev, scene):
+    """the deadline of the collective waits starts when the render before the gather has completed, so a
+    render much longer than the communicator's timeout (here car_boxed 1920x1080 at 16 spp, ~15 ms, under a 2 ms
+    timeout) gathers, waits (rt_comm_wait) and syncs (rt_sync, which settles the communicator first) without an abort;
+    the gathered frame equals the render"""
+    Wl, Hl = 1920, 1080
+    r = dev.Renderer(0)
+    r.upload(scene)
+    comm = dev.Comm([r], nranks=1, rank=0, uid=dev.comm_id())
+    comm.set_timeout(0.002)
+    px = torch.zeros((1, Hl, Wl), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    for g in range(3):  # the first gather exchanges and checks coverage (host waits); the others reuse the layout
+        r.render_frames([host.camera(Wl, Hl)], Wl, Hl, spp=16, bgra=px)
+        out = torch.zeros((1, Hl, Wl), dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        comm.gather(0, out, src=r)
+        if g == 1:
+            comm.wait()
+        ms = r.sync()
+        assert ms > 0.002 * 1e3, ms  # (the render did outlast the timeout)
+        assert torch.equal(out, px), g
+    info = comm.info()
+    assert info["gathers"] == 3 and info["exchanges"] == 1 and info["checked"] == 1, info
+    comm.close()
+    r.close()
