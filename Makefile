@@ -14,7 +14,7 @@ ARCH     ?= gfx950
 # -fno-slp-vectorize: the SLP vectoriser packed the triangle tests and shading into v_pk_{mul,add}_f32 pairs whose
 # operand shuffles cost as many moves as they saved, and its register pairs pushed the walks to the 128-VGPR cap
 # (same box: dragon 0.519 -> 0.511 ms per frame, car_boxed 0.746 -> 0.697, sportscar 0.787 -> 0.757).
-HOST_FLAGS := -O2 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -Wall -Wextra -Iinclude
+HOST_FLAGS := -O2 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -pthread -Wall -Wextra -Iinclude
 HIP_FLAGS  := -O3 -std=c++17 --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math -fno-slp-vectorize $(PRT_DEFS) \
               -fhip-fp32-correctly-rounded-divide-sqrt -fPIC -Wall -Iinclude -I$(CSRC)
 

@@ -698,6 +698,8 @@ def main():
                        "gather_comm": ng.info() if ng else None,
                        "gather_mode": gmode, "ranks": ranks_detail,
                        "launch": timed_launch, "accel_built": info["accel_built"], "accel_build_ms": info["build_ms"],
+                       # its stages over every view: GPU PLOC, host treelet passes, host layout + 8-wide collapse
+                       "accel_build_stages_ms": {k: info[k] for k in ("ploc_ms", "treelet_ms", "collapse_ms")},
                        "wide_depth": info["wide_depth"]},
             "frame_latency_ms": lat.item() if not args.no_latency else None,
             "frame_latency_detail": {"default_rule_ms": lat_default, "default_rule_mean_ms": sd["mean"],

@@ -91,6 +91,10 @@ typedef struct rt_scene_info {
                                    when every primary direction of a launch is that short (the reference camera's are
                                    1.87-2.77); 0: no such view (it would leave out < 2 % of the triangles) */
     int primary_nodes;
+    /* build_ms by stage, summed over the views: */
+    float ploc_ms;     /* the GPU tree builds (PLOC, incl. transfers) */
+    float treelet_ms;  /* the treelet restructuring of the GPU-built trees (host threads, rt_treelet.hpp) */
+    float collapse_ms; /* the layout and the 8-wide collapse with its quantisation (host threads, rt_wide.cpp) */
 } rt_scene_info;
 
 /* rt_frame.kernel */
@@ -267,7 +271,9 @@ enum {
     RT_BUILD_LDS_PATHS = 8,    /* the path levels in LDS (else a global slab, or registers at 3 waves) */
     RT_BUILD_POOL_LEVEL = 16,  /* the per-level shadow pool (RT_VARIANT_SHPOOL) */
     RT_BUILD_POOL_ALL = 32,    /* one shadow pool for all levels (RT_VARIANT_SHDEFER) */
-    RT_BUILD_TRACE = 64        /* the measuring build with per-tile times */
+    RT_BUILD_TRACE = 64,       /* the measuring build with per-tile times */
+    RT_BUILD_FEEDBACK = 128    /* a decided single-frame shape's frame dealt by the previous frame's per-tile times, its
+                                  tile lists built on the device (no measuring frames, no host round trip) */
 };
 int rt_get_launch_info(rt_ctx* ctx, rt_launch_info* info);
 /* load_from_gpu(): copies the last frame's compact rows to host (synchronous); nullable args. RT_E_KERNEL when the

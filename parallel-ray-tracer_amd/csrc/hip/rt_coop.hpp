@@ -307,6 +307,11 @@ __device__ __forceinline__ void flush_g(Ctr c, unsigned long long* g, unsigned q
     flush<COUNT>(c, g);
 }
 
+// The single-frame feedback (rt_feedback.hpp) ranks 8x8 tiles by the time their last render took; a tile rendered by
+// k_coop is priced at FB_COOP_SCALE times its longest group tile's time, so that a hot tile's cost stays comparable
+// with the cold tiles k_persist rendered (k_coop spends about twice k_persist's wave time per ray, over 2-4 tiles).
+constexpr unsigned FB_COOP_SCALE = 2;
+
 // Pixel tile of one wave: 64 / G pixels.
 template <int G> struct GTile;
 template <> struct GTile<2> { static constexpr int TW = 8, TH = 4; };
@@ -324,7 +329,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
     const int pi = lane / G;
     constexpr int TW = GTile<G>::TW;
     Ctr c = {};
-    const unsigned items = (unsigned)A.n_tiles * (unsigned)A.n_frames;  // frame batches: as k_persist
+    // frame batches: as k_persist; a list built on the device (the single-frame feedback) has its length there
+    const unsigned items =
+        (unsigned)(A.n_tiles_dev ? __builtin_amdgcn_readfirstlane(*A.n_tiles_dev) : A.n_tiles) * (unsigned)A.n_frames;
     for (;;) {
         unsigned t = 0;
         if (lane == 0) t = atomicAdd(A.work, 1u);
@@ -337,8 +344,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         const int x = tx * TW + pi % TW, k = ty * GTile<G>::TH + pi / TW;
         unsigned long long t0 = 0;
         const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
-        if (TRACE) t0 = __builtin_amdgcn_s_memrealtime();
+        if (TRACE || A.tile_cost) t0 = __builtin_amdgcn_s_memrealtime();
         if (x < A.W && k < A.n_rows) render_pixel<MAXB, false, COUNT, true, G>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, q);
+        if (A.tile_cost && lane == 0)  // the feedback's cost of the 8x8 tile this tile lies in (rt_feedback.hpp)
+            atomicMax(A.tile_cost + (ty * GTile<G>::TH / 8) * A.tiles_x8 + tx * TW / 8,
+                      (unsigned)(__builtin_amdgcn_s_memrealtime() - t0) * FB_COOP_SCALE);
         if (TRACE) {  // as k_persist's: {begin, end, wave | fallbacks << 32, wave steps | ray node visits << 32}
             const unsigned fb = wave_sum(q == 0 ? c.fb - fb0 : 0u), ws = wave_sum(c.ws - ws0),
                            nv = wave_sum(q == 0 ? c.chi + c.shi - nd0 : 0u);

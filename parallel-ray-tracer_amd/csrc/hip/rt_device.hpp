@@ -111,13 +111,21 @@ struct KArgs {
     // int offset slot_off (the host appends them to the launch's LDS layout), so that the per-sample sums never leave
     // the CU (64 spp at 4K: 530 M slot updates per frame)
     int slot_off;
+    // single frames under the default rule's feedback (RT_VARIANT_HYBRID, rt_feedback.hpp; nullable): every 8x8 tile's
+    // duration in s_memrealtime ticks (k_persist: stored; k_coop: the maximum of its tiles', scaled, by atomic max), from
+    // which the next frame's tile lists are built on the device
+    unsigned* tile_cost;
+    // nullable: the number of tiles to deal, in device memory (k_coop over a list whose length the device built)
+    const int* n_tiles_dev;
+    int tiles_x8;  // 8x8 tiles per row of the frame (k_coop's tile_cost index)
+    int pad_fb;
 };
 
 // Kernel arguments are laid out by the host compiler and read by the device compiler: both passes must
 // agree on every offset (an LDS pointer, 32-bit on gfx950 but 64-bit on the host, once shifted every
 // later field and hung a kernel). Pinned sizes catch such drift at compile time in whichever pass
 // disagrees; never put address-space-qualified pointers in these structs.
-static_assert(sizeof(DWide) == 32 && sizeof(DScene) == 216 && sizeof(KArgs) == 456,
+static_assert(sizeof(DWide) == 32 && sizeof(DScene) == 216 && sizeof(KArgs) == 480,
               "kernel-argument layout changed: update the pinned sizes only after checking both passes agree");
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

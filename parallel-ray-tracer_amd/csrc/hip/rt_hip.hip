@@ -16,6 +16,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -28,6 +29,7 @@
 #include "rt_build.hpp"
 #include "rt_comm_logic.hpp"
 #include "rt_treelet.hpp"
+#include "rt_feedback.hpp"
 #ifndef PRT_TREELET
 #define PRT_TREELET 2  // treelet-restructuring passes over the GPU-built binary tree (0: none)
 #endif
@@ -96,6 +98,7 @@ struct rt_ctx {
     float amb[3] = {0.5f, 0.5f, 0.5f};
     bool has_scene = false;
     rt_scene_info info{};  // what the last upload built (rt_get_scene_info)
+    float t_ploc = 0.0f, t_treelet = 0.0f, t_collapse = 0.0f;  // the upload's build stages (ms; rt_scene_info)
     // outputs / bookkeeping
     float* d_rgb_own = nullptr;
     size_t rgb_cap = 0;
@@ -185,8 +188,22 @@ struct rt_ctx {
         int* h_lists = nullptr;  // pinned staging of d_lists (stream-ordered copies)
         size_t lists_cap = 0, hl_cap = 0;
         bool cold_regions = false;
+        int cold_mode = 0;  // the cold lists' region layout (xcd_mode) when cold_regions
         hipEvent_t ev = nullptr, fork = nullptr, join = nullptr;
         hipStream_t s2 = nullptr;
+        // per-frame feedback (rt_feedback.hpp): every frame of the shape records its 8x8 tiles' durations in d_cost; a
+        // decided shape's frames build their lists from the previous frame's on the device (d_fb: [hot: 4 x n_tiles]
+        // [cold: 9 + n_tiles][counts: 4]); h_fb_cnt: a recent frame's hot count, read back without waiting (grid sizes)
+        unsigned* d_cost = nullptr;
+        int* d_fb = nullptr;
+        unsigned char* d_info = nullptr;  // rtd::fb_tile_info of every tile, for info_mode
+        int info_mode = -1;
+        size_t fb_cap = 0;
+        bool fb_ok = false;  // d_cost holds a whole frame of this shape (stream order)
+        int* h_fb_cnt = nullptr;
+        hipEvent_t fb_ev = nullptr;
+        bool fb_pending = false;
+        int fb_hot_est = -1;
     } hy;
 };
 
@@ -212,6 +229,11 @@ struct HotCand {
 constexpr HotCand HYBRID_CANDS[] = {{0, 0, RT_VARIANT_SHPOOL, true},   {0, 0, RT_VARIANT_PERSIST, true},
                                     {45, 4, RT_VARIANT_PERSIST, true}, {60, 4, RT_VARIANT_PERSIST, false},
                                     {60, 2, RT_VARIANT_PERSIST, false}};
+// Per-frame feedback (rt_feedback.hpp) for a decided shape: its frames deal their tiles by the previous frame's
+// per-tile durations, the lists built on the device, instead of a measuring frame's every REFRESH frames
+#ifndef PRT_FEEDBACK
+#define PRT_FEEDBACK 1
+#endif
 // pixel tile of a group kernel (rtd::GTile): k_coop<2> 8x4, k_coop<4> 4x4
 inline void hot_tile(int g, int& tw, int& th) {
     tw = g == 2 ? 8 : 4;
@@ -429,12 +451,19 @@ extern "C" int rt_create(const rt_opts* opts, rt_ctx** out) {
 
 // load_to_gpu (gpu/src/gpu.cu:129-201): reference layouts -> device layout (rt_device.hpp).
 namespace {
+// host threads of the acceleration build's CPU stages (the treelet passes, rt_treelet.hpp): the machine's, at most 16
+// (the GPU box's CPU quota; nproc there reports the whole host)
+int build_threads() {
+    const unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(16u, hc));
+}
 // GPU-built acceleration BVH (rt_build.hpp, PLOC) in the reference layout: children of a node at child and
 // child + 1, single-triangle leaves numbered depth-first (every subtree's triangles are one range of idx).
 // Returns RT_OK, or RT_E_STATE when the tree is unusable (the caller falls back to the host build).
 int gpu_ploc(rt_ctx* ctx, const rt_triangle* T, int n, int R, std::vector<rt_bvh_node>& out, std::vector<int>& idx,
              int& depth_out) {
     hipStream_t st = ctx->stream;
+    const auto t_gpu = std::chrono::steady_clock::now();
     std::vector<float> hv(9 * (size_t)n);
     for (int i = 0; i < n; i++)
         for (int k = 0; k < 3; k++) {
@@ -536,6 +565,10 @@ int gpu_ploc(rt_ctx* ctx, const rt_triangle* T, int n, int R, std::vector<rt_bvh
     PLOC(hipMemcpyAsync(hhi.data(), nhi, sizeof(float4) * nn2, hipMemcpyDeviceToHost, st));
     PLOC(hipStreamSynchronize(st));
 #undef PLOC
+    using clk = std::chrono::steady_clock;
+    auto since = [](clk::time_point t) { return std::chrono::duration<float, std::milli>(clk::now() - t).count(); };
+    ctx->t_ploc += since(t_gpu);
+    auto t_host = clk::now();
     if (PRT_TREELET > 0 && n >= 3) {  // treelet restructuring on the host (rt_treelet.hpp)
         rtt::Tree T;
         T.n = n;
@@ -545,7 +578,7 @@ int gpu_ploc(rt_ctx* ctx, const rt_triangle* T, int n, int R, std::vector<rt_bvh
         T.box.resize(2 * (size_t)n - 1);
         for (size_t i = 0; i < T.box.size(); i++)
             T.box[i] = rtt::Box{{hlo[i].x, hlo[i].y, hlo[i].z}, {hhi[i].x, hhi[i].y, hhi[i].z}};
-        for (int p = 0; p < PRT_TREELET; p++) rtt::optimize_pass(T);
+        for (int p = 0; p < PRT_TREELET; p++) rtt::optimize_pass(T, build_threads());
         std::copy(T.left.begin(), T.left.end(), hl.begin());
         std::copy(T.right.begin(), T.right.end(), hr.begin());
         for (size_t i = (size_t)n; i < T.box.size(); i++) {
@@ -553,6 +586,8 @@ int gpu_ploc(rt_ctx* ctx, const rt_triangle* T, int n, int R, std::vector<rt_bvh
             hhi[i] = make_float4(T.box[i].hi[0], T.box[i].hi[1], T.box[i].hi[2], hhi[i].w);
         }
     }
+    ctx->t_treelet += since(t_host);
+    t_host = clk::now();
     // reference layout, depth-first: children at consecutive indices, leaves numbered left to right
     out.clear();
     out.reserve(nn2);
@@ -586,6 +621,7 @@ int gpu_ploc(rt_ctx* ctx, const rt_triangle* T, int n, int R, std::vector<rt_bvh
         }
     }
     depth_out = depth;
+    ctx->t_collapse += since(t_host);
     return done();
 }
 }  // namespace
@@ -659,7 +695,10 @@ int wide_view(rt_ctx* ctx, const rt_triangle* T, int n, int method, int R, float
     int* order = nullptr;
     rth_wbvh_info wi{};
     int rc = RT_E_STATE;
-    if (rth_wbvh_build_cost(nodes, nlen, idx, T, n, inflate, cnode, &words, &order, &wi) == RT_OK && wi.depth <= rtd::WSTACK) {
+    const auto t_c = std::chrono::steady_clock::now();
+    const bool wide_ok = rth_wbvh_build_cost(nodes, nlen, idx, T, n, inflate, cnode, &words, &order, &wi) == RT_OK;
+    ctx->t_collapse += std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_c).count();
+    if (wide_ok && wi.depth <= rtd::WSTACK) {
         wn.resize(5 * (size_t)wi.n_nodes);
         std::memcpy(wn.data(), words, sizeof(uint32_t) * 20 * (size_t)wi.n_nodes);
         tri_records(T, order, n, wt, wo);
@@ -693,6 +732,7 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     bool own_acc = sc->accel != RT_ACCEL_REFERENCE;
     int built = sc->accel == RT_ACCEL_REFERENCE ? RT_ACCEL_REFERENCE : RT_ACCEL_HOST;
     float gpu_ms = 0.0f;
+    ctx->t_ploc = ctx->t_treelet = ctx->t_collapse = 0.0f;
     const auto t_build = std::chrono::steady_clock::now();
     std::vector<rt_bvh_node> gnodes;
     std::vector<int> gidx;
@@ -741,9 +781,11 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
         uint32_t* words = nullptr;
         int* order = nullptr;
         rth_wbvh_info wi{};
-        if (!rc && rth_wbvh_build_cost(nodes, nlen, idx, sc->triangles, n, inflate, sc->collapse_node_cost, &words, &order, &wi) ==
-                       RT_OK &&
-            wi.depth <= rtd::WSTACK) {
+        const auto t_c = std::chrono::steady_clock::now();
+        const bool wide_ok = !rc && rth_wbvh_build_cost(nodes, nlen, idx, sc->triangles, n, inflate,
+                                                        sc->collapse_node_cost, &words, &order, &wi) == RT_OK;
+        ctx->t_collapse += std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_c).count();
+        if (wide_ok && wi.depth <= rtd::WSTACK) {
             wide_nodes.resize(5 * (size_t)wi.n_nodes);
             std::memcpy(wide_nodes.data(), words, sizeof(uint32_t) * 20 * (size_t)wi.n_nodes);
             tri_records(sc->triangles, order, n, wide_tris, wide_orig);
@@ -910,6 +952,9 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     ctx->info.accel_built = built;
     ctx->info.build_ms = build_ms;
     ctx->info.gpu_build_ms = gpu_ms;
+    ctx->info.ploc_ms = ctx->t_ploc;
+    ctx->info.treelet_ms = ctx->t_treelet;
+    ctx->info.collapse_ms = ctx->t_collapse;
     return RT_OK;
 }
 
@@ -1136,6 +1181,8 @@ std::vector<int> region_layout(const std::vector<int>& ord, int tx, int ty, int 
 
 template <int MAXB>
 int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsigned* build = nullptr);  // below
+template <int MAXB>
+int launch_hybrid_fb(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsigned* build);  // below
 
 // A frame batch's cameras to d_cams when they differ from the set it holds. The copy runs in stream order (after the
 // renders in flight, which read the old set) from a ring of pinned slots; only a slot whose previous copy has not
@@ -1272,6 +1319,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     A.work = ctx->d_work;
     A.tiles_x = (f->width + 7) / 8;
     A.n_tiles = A.tiles_x * ((f->n_rows + 7) / 8);
+    A.tiles_x8 = A.tiles_x;
     const int kernel = f->kernel == RT_KERNEL_AUTO ? RT_KERNEL_FAST : f->kernel;
     if (n_frames > 1 && kernel != RT_KERNEL_FAST) {  // one launch per frame, outputs at frame offsets
         for (int i = 0; i < n_frames; i++) {
@@ -1569,9 +1617,31 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 if (e != hipSuccess) return err(e, "rt_render: hybrid tile times");
                 h.tr_cap = h.n_tiles;
             }
+            if (h.fb_cap < h.n_tiles) {  // the feedback's buffers (rt_feedback.hpp); no frame of the old shape runs now
+                if (h.fb_pending) (void)hipEventSynchronize(h.fb_ev);
+                if (h.d_cost) (void)hipFree(h.d_cost);
+                if (h.d_fb) (void)hipFree(h.d_fb);
+                if (h.d_info) (void)hipFree(h.d_info);
+                h.d_cost = nullptr;
+                h.d_fb = nullptr;
+                h.d_info = nullptr;
+                h.fb_cap = 0;
+                hipError_t e = hipMalloc((void**)&h.d_cost, sizeof(unsigned) * h.n_tiles);
+                if (e == hipSuccess) e = hipMalloc((void**)&h.d_fb, sizeof(int) * (5 * h.n_tiles + 13));
+                if (e == hipSuccess) e = hipMalloc((void**)&h.d_info, h.n_tiles);
+                if (e == hipSuccess && !h.h_fb_cnt) e = hipHostMalloc((void**)&h.h_fb_cnt, sizeof(int) * 4, hipHostMallocDefault);
+                if (e == hipSuccess && !h.fb_ev) e = hipEventCreateWithFlags(&h.fb_ev, hipEventDisableTiming);
+                if (e != hipSuccess) return err(e, "rt_render: hybrid feedback buffers");
+                h.fb_cap = h.n_tiles;
+            }
+            h.fb_ok = false;
+            h.fb_hot_est = -1;
+            h.info_mode = -1;
             h.state = 0;
         }
-        if (h.state == 2 && h.choice >= 0 && ++h.frames >= rt_ctx::Hybrid::REFRESH) h.state = 0;  // renew the lists
+        // renew a decided shape's lists with a measuring frame every REFRESH frames -- unless its frames feed their own
+        // tile times forward (PRT_FEEDBACK), which keeps the lists one frame old
+        if (!PRT_FEEDBACK && h.state == 2 && h.choice >= 0 && ++h.frames >= rt_ctx::Hybrid::REFRESH) h.state = 0;
         if (h.state == 0) return Pick{0, 0};
         if (h.state == 1) {
             bool done = false;
@@ -1589,6 +1659,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             if (!dealt_centre_out)
                 for (int t = 0; t < (int)ord.size(); t++) ord[t] = t;  // RT_DEAL_ROW_MAJOR
             h.cold_regions = xcd_mode >= 1 && xcd_mode <= 3 && dealt_centre_out;
+            h.cold_mode = h.cold_regions ? xcd_mode : 0;
             const bool keep = h.choice >= 0;  // a refresh: new lists, the same candidates and choice
             if (!keep) {
                 h.nc = 0;
@@ -1751,6 +1822,26 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             if (rc) return rc;
             // the frame's HIP-event time starts here, after the host work of the pick (the trials compare them)
             HIPC(hipEventRecord(ctx->ev0, ctx->stream));
+            rt_ctx::Hybrid& h = ctx->hy;
+            // every frame of the shape records its tiles' durations (rt_feedback.hpp); a decided shape's frames build
+            // their lists from the previous frame's first, on the device (the memset follows that build: k_coop's hot
+            // tiles combine their group tiles' times by atomic max)
+            const bool fb = PRT_FEEDBACK && pk.kind == 2 && h.choice >= 0 && h.fb_ok && pk.c == h.choice;
+            if (PRT_FEEDBACK && h.d_cost) {
+                if (fb) {
+                    li.hot_pct = h.pct[pk.c];
+                    li.hot_lanes = h.lanes[pk.c];
+                    li.cold_variant = h.cold[pk.c];
+                    const int r2 = f->bounces <= 4 ? launch_hybrid_fb<4>(ctx, A, count, pk.c, &li.build)
+                                                   : launch_hybrid_fb<8>(ctx, A, count, pk.c, &li.build);
+                    h.fb_ok = r2 == RT_OK;
+                    return r2;
+                }
+                HIPC(hipMemsetAsync(h.d_cost, 0, sizeof(unsigned) * h.n_tiles, ctx->stream));
+                P.tile_cost = h.d_cost;
+                A.tile_cost = h.d_cost;
+                h.fb_ok = true;  // (this frame, in stream order, fills it)
+            }
             if (pk.kind == 2) {
                 li.hot_pct = ctx->hy.pct[pk.c];
                 li.hot_lanes = ctx->hy.lanes[pk.c];
@@ -1758,7 +1849,6 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 return f->bounces <= 4 ? launch_hybrid<4>(ctx, A, count, pk.c, &li.build)
                                        : launch_hybrid<8>(ctx, A, count, pk.c, &li.build);
             }
-            rt_ctx::Hybrid& h = ctx->hy;
             if (pk.kind == 0) {  // measuring frame: k_persist with per-tile times, copied to the host behind it
                 li.variant = RT_VARIANT_PERSIST;
                 li.refresh = h.choice >= 0 ? 1 : 0;  // a decided shape's periodic list refresh (settled)
@@ -1960,6 +2050,87 @@ int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsigned*
     if (n_hot > 0) kc<<<nc, rtd::BLOCK, 0, h.s2>>>(B);
     HIPC(hipGetLastError());
     if (n_cold > 0) kp<<<np, rtd::BLOCK, dyn, ctx->stream>>>(with_slots(P, dyn));
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(h.join, h.s2));
+    HIPC(hipStreamWaitEvent(ctx->stream, h.join, 0));
+    return RT_OK;
+}
+
+// A decided shape's frame under the per-frame feedback (rt_feedback.hpp): candidate c's lists built on the device from
+// the previous frame's tile durations (k_fb_lists), the durations cleared, then c's kernels as launch_hybrid launches
+// them, every one reading its list and count from the device and recording this frame's durations. The grids are sized
+// by a recent frame's hot count, read back without a wait.
+template <int MAXB>
+int launch_hybrid_fb(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsigned* build) {
+    rt_ctx::Hybrid& h = ctx->hy;
+    const int g = h.lanes[c] == 2 ? 2 : 4;
+    const bool hot = h.pct[c] > 0;
+    int tw, th;
+    hot_tile(g, tw, th);
+    const int ctw = (A.W + tw - 1) / tw, cth = (A.n_rows + th - 1) / th;
+    int* d_hot = h.d_fb;
+    int* d_cold = h.d_fb + 4 * h.n_tiles;
+    int* d_cnt = d_cold + 9 + h.n_tiles;
+    const int tx = A.tiles_x, ty = A.n_tiles / A.tiles_x;
+    if (h.info_mode != h.cold_mode) {  // the shape's per-tile region and hot-kernel tile counts, once
+        std::vector<unsigned char> info(h.n_tiles);
+        for (int t = 0; t < A.n_tiles; t++) info[t] = rtd::fb_tile_info(t, tx, ty, h.cold_mode, A.W, A.n_rows);
+        HIPC(hipMemcpy(h.d_info, info.data(), info.size(), hipMemcpyHostToDevice));
+        h.info_mode = h.cold_mode;
+    }
+    // (hot set: at most half the 8x8 tiles, as the host's lists, counted in hot-kernel tiles)
+    const rtd::FbArgs F{h.d_cost, A.n_tiles, tx, ty, h.pct[c], (int)(h.n_tiles / 2) * (8 / tw) * (8 / th), tw, th, ctw, cth, h.cold_mode,
+                        h.d_info, d_hot, d_cold, d_cnt};
+    rtd::k_fb_lists<<<1, rtd::FB_THREADS, 0, ctx->stream>>>(F);
+    HIPC(hipGetLastError());
+    HIPC(hipMemsetAsync(h.d_cost, 0, sizeof(unsigned) * h.n_tiles, ctx->stream));
+    if (h.fb_pending) {  // a recent frame's hot count (grid size), if its copy has landed: a query, never a wait
+        const hipError_t q = hipEventQuery(h.fb_ev);
+        if (q == hipSuccess) {
+            h.fb_hot_est = h.h_fb_cnt[0];
+            h.fb_pending = false;
+        } else if (q == hipErrorNotReady) {
+            (void)hipGetLastError();
+        } else {
+            return fail(ctx, q, "rt_render: hybrid feedback count");
+        }
+    }
+    if (hot && !h.fb_pending) {
+        HIPC(hipMemcpyAsync(h.h_fb_cnt, d_cnt, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        HIPC(hipEventRecord(h.fb_ev, ctx->stream));
+        h.fb_pending = true;
+    }
+    const KFn kc = coop_kernel<MAXB>(g, count);
+    rtd::KArgs B = A;  // the hot kernel's tiles, hottest first, their number on the device
+    B.tiles_x = ctw;
+    B.n_tiles = 4 * (int)h.n_tiles;
+    B.n_tiles_dev = d_cnt;
+    B.tile_order = d_hot;
+    B.region_off = nullptr;
+    B.work = A.work + 224;
+    B.tile_cost = h.d_cost;
+    rtd::KArgs P = A;  // the cold 8x8 tiles by region, costliest first (the region offsets hold their number)
+    P.region_off = d_cold;
+    P.tile_order = d_cold + 9;
+    P.tile_cost = h.d_cost;
+    size_t dyn = 0;
+    const KFn kp = persist_kernel<MAXB>(P, h.cold[c], count, ctx->device, dyn, ctx->pk_ok, ctx->tq_ok, build);
+    if (build) *build |= RT_BUILD_FEEDBACK;
+    const int rp = resident(kp, ctx->device, 8, dyn);
+    const int rcp = resident(kc, ctx->device);
+    const int est = h.fb_hot_est >= 0 ? h.fb_hot_est : h.n_hot[c];
+    const int nc = hot ? std::max(1, std::min((est + 3) / 4, rcp / 2)) : 0;
+    const int np = std::max(1, std::min(rp - (int)((long long)nc * rp / rcp), (A.n_tiles + 3) / 4));
+    if (!hot) {  // (the whole frame, costliest first)
+        kp<<<np, rtd::BLOCK, dyn, ctx->stream>>>(with_slots(P, dyn));
+        HIPC(hipGetLastError());
+        return RT_OK;
+    }
+    HIPC(hipEventRecord(h.fork, ctx->stream));  // after the lists, the counters' and the durations' resets
+    HIPC(hipStreamWaitEvent(h.s2, h.fork, 0));
+    kc<<<nc, rtd::BLOCK, 0, h.s2>>>(B);
+    HIPC(hipGetLastError());
+    kp<<<np, rtd::BLOCK, dyn, ctx->stream>>>(with_slots(P, dyn));
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(h.join, h.s2));
     HIPC(hipStreamWaitEvent(ctx->stream, h.join, 0));
@@ -2730,6 +2901,11 @@ extern "C" void rt_destroy(rt_ctx* ctx) {
     }
     if (ctx->hy.s2) (void)hipStreamSynchronize(ctx->hy.s2);
     if (ctx->hy.d_tr) (void)hipFree(ctx->hy.d_tr);
+    if (ctx->hy.d_cost) (void)hipFree(ctx->hy.d_cost);
+    if (ctx->hy.d_fb) (void)hipFree(ctx->hy.d_fb);
+    if (ctx->hy.d_info) (void)hipFree(ctx->hy.d_info);
+    if (ctx->hy.h_fb_cnt) (void)hipHostFree(ctx->hy.h_fb_cnt);
+    if (ctx->hy.fb_ev) (void)hipEventDestroy(ctx->hy.fb_ev);
     if (ctx->hy.h_tr) (void)hipHostFree(ctx->hy.h_tr);
     if (ctx->hy.d_lists) (void)hipFree(ctx->hy.d_lists);
     if (ctx->hy.h_lists) (void)hipHostFree(ctx->hy.h_lists);

@@ -1663,13 +1663,15 @@ void k_persist(KArgs A) {
         const int x = tx * 8 + (int)(ln & 7u), k = ty * 8 + (int)(ln >> 3);
         unsigned long long t0 = 0;
         const unsigned fb0 = c.fb, ws0 = c.ws, nd0 = c.chi + c.shi;
-        if (TRACE) t0 = __builtin_amdgcn_s_memrealtime();
+        if (TRACE || A.tile_cost) t0 = __builtin_amdgcn_s_memrealtime();
         if constexpr (SHP == 1 || SHP == 2)
             render_pixel_shp<MAXB, COUNT, SPP1, SHP>(A, cam_of<BATCH>(A, frame), frame, x, k, x < A.W && k < A.n_rows,
                                                      stk, c, u, sstk, wcap);
         else if (x < A.W && k < A.n_rows)
             render_pixel<MAXB, STRICT, COUNT, REG, 1, PB, SPP1 ? 1 : 2, SHP == 3, SHP == 3 && DYN>(
                 A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, 0u, sstk, wcap);
+        if (A.tile_cost && lane == 0)  // the feedback's tile duration (single frames: tile = its 8x8 tile)
+            A.tile_cost[tile] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t0);
         if (TRACE) {  // {begin, end, wave | fallbacks << 32, wave steps | lane node visits << 32} (COUNT)
             const unsigned fb = wave_sum(c.fb - fb0), ws = wave_sum(c.ws - ws0), nv = wave_sum(c.chi + c.shi - nd0);
             if (lane == 0) {

@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "rt_host.h"
@@ -284,64 +285,60 @@ extern "C" int rth_wbvh_build_cost(const rt_bvh_node* bvh, int n_nodes, const in
     // DESIGN.md §3)
     w.sah_costs(c_node > 0.0f ? c_node : 2.0f);
 
-    // breadth-first: interior children of a wide node get consecutive indices
+    // breadth-first: interior children of a wide node get consecutive indices. Level by level: every node of a level
+    // is formed independently (its children, slots, quantised planes) on the build's threads, then the level's
+    // child / triangle bases follow by prefix sums in queue order -- the layout a one-node-at-a-time queue makes.
     struct Item {
         int b, depth;
     };
-    std::vector<Item> queue{{root, 1}};
-    std::vector<uint32_t> words;
-    std::vector<int> order;
-    order.reserve(n_tris);
-    int depth = 0, max_kids = 0;
-    for (size_t qi = 0; qi < queue.size(); qi++) {
-        const Item it = queue[qi];
-        depth = std::max(depth, it.depth);
+    struct Out {  // one wide node before its bases are known
+        uint32_t W[20];
+        int kid[WIDTH];      // per slot: the child's BNode (-1: empty)
+        char leaf[WIDTH];    // per slot: a leaf slot
+        int n_inner, n_tri;  // interior slots, leaf triangles
+    };
+    auto form = [&](const Item& it, Out& o) {
         const BNode& B = w.bn[it.b];
-        std::vector<int> kids;
-        std::vector<char> kid_leaf;
+        std::pair<int, bool> c2[WIDTH];
+        int k = 0;
         if (B.l < 0 || w.as_leaf[it.b]) {
-            kids.push_back(it.b);  // a leaf root
-            kid_leaf.push_back(1);
+            c2[k++] = {it.b, true};  // a leaf root
         } else {  // the cost-optimal distribution of this node's 8 slots
-            std::vector<std::pair<int, bool>> c2;
-            w.collect(B.l, w.split[it.b][WIDTH], c2);
-            w.collect(B.r, WIDTH - w.split[it.b][WIDTH], c2);
-            for (auto& pr : c2) {
-                kids.push_back(pr.first);
-                kid_leaf.push_back(pr.second ? 1 : 0);
-            }
+            std::vector<std::pair<int, bool>> tmp;
+            tmp.reserve(WIDTH);
+            w.collect(B.l, w.split[it.b][WIDTH], tmp);
+            w.collect(B.r, WIDTH - w.split[it.b][WIDTH], tmp);
+            for (auto& pr : tmp) c2[k++] = pr;
         }
-        const int k = (int)kids.size();
-        max_kids = std::max(max_kids, k);
         // octant slots: greedy on cost = -dot(centre offset, slot direction)
         Box all = empty_box();
-        for (int c : kids) grow(all, w.bn[c].b);
+        for (int c = 0; c < k; c++) grow(all, w.bn[c2[c].first].b);
         float pc[3];
         for (int a = 0; a < 3; a++) pc[a] = 0.5f * (all.lo[a] + all.hi[a]);
         int kid_in[WIDTH];
-        for (int s = 0; s < WIDTH; s++) kid_in[s] = -1;
-        std::vector<char> done(k, 0);
+        for (int s2 = 0; s2 < WIDTH; s2++) kid_in[s2] = -1;
+        bool done[WIDTH] = {false};
         for (int round = 0; round < k; round++) {
             float bc = INFINITY;
             int bk = -1, bs = -1;
             for (int c = 0; c < k; c++) {
                 if (done[c]) continue;
-                const Box& cb = w.bn[kids[c]].b;
-                for (int s = 0; s < WIDTH; s++) {
-                    if (kid_in[s] >= 0) continue;
+                const Box& cb = w.bn[c2[c].first].b;
+                for (int s2 = 0; s2 < WIDTH; s2++) {
+                    if (kid_in[s2] >= 0) continue;
                     float cost = 0.0f;
                     for (int a = 0; a < 3; a++) {
                         const float off = 0.5f * (cb.lo[a] + cb.hi[a]) - pc[a];
-                        cost -= ((s >> a) & 1) ? off : -off;
+                        cost -= ((s2 >> a) & 1) ? off : -off;
                     }
                     if (cost < bc) {
                         bc = cost;
                         bk = c;
-                        bs = s;
+                        bs = s2;
                     }
                 }
             }
-            done[bk] = 1;
+            done[bk] = true;
             kid_in[bs] = bk;
         }
         // quantise (grown boxes) per axis over the occupied slots
@@ -349,66 +346,118 @@ extern "C" int rth_wbvh_build_cost(const rt_bvh_node* bvh, int n_nodes, const in
         int qlo[3][WIDTH], qhi[3][WIDTH];
         int ks = 0;
         int slot_list[WIDTH];
-        for (int s = 0; s < WIDTH; s++)
-            if (kid_in[s] >= 0) {
-                const Box& cb = w.bn[kids[kid_in[s]]].b;
+        for (int s2 = 0; s2 < WIDTH; s2++)
+            if (kid_in[s2] >= 0) {
+                const Box& cb = w.bn[c2[kid_in[s2]].first].b;
                 for (int a = 0; a < 3; a++) {
                     lo[a][ks] = cb.lo[a] - inflate;
                     hi[a][ks] = cb.hi[a] + inflate;
                 }
-                slot_list[ks++] = s;
+                slot_list[ks++] = s2;
             }
         float p[3];
         int eb[3];
         for (int a = 0; a < 3; a++) eb[a] = quantise_axis(lo[a], hi[a], ks, p[a], qlo[a], qhi[a]);
-        // node words
-        const size_t base = words.size();
-        words.resize(base + 20, 0);
-        uint32_t* W = &words[base];
+        uint32_t* W = o.W;
+        std::memset(W, 0, sizeof o.W);
         W[0] = f2u(p[0]);
         W[1] = f2u(p[1]);
         W[2] = f2u(p[2]);
         uint32_t imask = 0;
-        for (int s = 0; s < WIDTH; s++)
-            if (kid_in[s] >= 0 && !kid_leaf[kid_in[s]]) imask |= 1u << s;
+        for (int s2 = 0; s2 < WIDTH; s2++)
+            if (kid_in[s2] >= 0 && !c2[kid_in[s2]].second) imask |= 1u << s2;
         // the exponents as signed bytes: the walks scale 1/d by them with one v_ldexp_f32 each
         W[3] = (uint32_t)(uint8_t)(int8_t)eb[0] | ((uint32_t)(uint8_t)(int8_t)eb[1] << 8) |
                ((uint32_t)(uint8_t)(int8_t)eb[2] << 16) | (imask << 24);
-        const int child_base = (int)queue.size();
-        const int tri_base = (int)order.size();
-        W[4] = (uint32_t)child_base;
-        W[5] = (uint32_t)tri_base;
-        uint8_t meta[WIDTH] = {0};
         uint8_t q8[6][WIDTH];
-        for (int s = 0; s < WIDTH; s++) {  // empty slots: an inverted box (never selected: meta 0, imask 0)
+        for (int s2 = 0; s2 < WIDTH; s2++) {  // empty slots: an inverted box (never selected: meta 0, imask 0)
             for (int a = 0; a < 3; a++) {
-                q8[a][s] = 255;
-                q8[3 + a][s] = 0;
+                q8[a][s2] = 255;
+                q8[3 + a][s2] = 0;
             }
+            o.kid[s2] = kid_in[s2] >= 0 ? c2[kid_in[s2]].first : -1;
+            o.leaf[s2] = kid_in[s2] >= 0 && c2[kid_in[s2]].second;
         }
+        o.n_inner = o.n_tri = 0;
         for (int j = 0; j < ks; j++) {
-            const int s = slot_list[j];
+            const int s2 = slot_list[j];
             for (int a = 0; a < 3; a++) {
-                q8[a][s] = (uint8_t)qlo[a][j];
-                q8[3 + a][s] = (uint8_t)qhi[a][j];
+                q8[a][s2] = (uint8_t)qlo[a][j];
+                q8[3 + a][s2] = (uint8_t)qhi[a][j];
             }
-            const BNode& c = w.bn[kids[kid_in[s]]];
-            if (!kid_leaf[kid_in[s]]) {
-                queue.push_back({kids[kid_in[s]], it.depth + 1});
-            } else {
-                const int off = (int)order.size() - tri_base;
-                meta[s] = (uint8_t)((c.cnt << 5) | off);
-                for (int i = c.first; i < c.first + c.cnt; i++) order.push_back(w.idx[i]);
-            }
+            if (o.leaf[s2]) o.n_tri += w.bn[o.kid[s2]].cnt;
+            else o.n_inner++;
         }
-        std::memcpy(&W[6], meta, 8);
         // per axis a, four words: word j = qlo[2j], qhi[2j], qlo[2j + 1], qhi[2j + 1] (one slot pair's two planes
         // side by side, so that a single byte permute picks a pair's near or far planes by the ray's sign)
         for (int a = 0; a < 3; a++)
             for (int j = 0; j < WIDTH / 2; j++)
                 W[8 + 4 * a + j] = (uint32_t)q8[a][2 * j] | ((uint32_t)q8[3 + a][2 * j] << 8) |
                                    ((uint32_t)q8[a][2 * j + 1] << 16) | ((uint32_t)q8[3 + a][2 * j + 1] << 24);
+    };
+    const int nthreads = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+    auto parallel = [&](size_t n, auto&& fn) {  // fn(i) for i < n, in contiguous chunks over the threads
+        const int nt = (int)std::min<size_t>((size_t)nthreads, (n + 255) / 256);
+        if (nt <= 1) {
+            for (size_t i = 0; i < n; i++) fn(i);
+            return;
+        }
+        std::vector<std::thread> pool;
+        for (int t = 0; t < nt; t++)
+            pool.emplace_back([&, t] {
+                for (size_t i = n * t / nt; i < n * (t + 1) / nt; i++) fn(i);
+            });
+        for (std::thread& th : pool) th.join();
+    };
+    std::vector<Item> level{{root, 1}};
+    std::vector<uint32_t> words;
+    std::vector<int> order(n_tris, -1);
+    size_t n_wide = 0, n_order = 0;
+    int depth = 0, max_kids = 0;
+    std::vector<Out> outs;
+    while (!level.empty()) {
+        depth = std::max(depth, level[0].depth);
+        outs.resize(level.size());
+        parallel(level.size(), [&](size_t i) { form(level[i], outs[i]); });
+        // bases in queue order: this level's children follow every node queued so far
+        size_t next_node = n_wide + level.size(), next_tri = n_order;
+        std::vector<size_t> cbase(level.size()), tbase(level.size());
+        std::vector<Item> nxt;
+        for (size_t i = 0; i < level.size(); i++) {
+            cbase[i] = next_node;
+            tbase[i] = next_tri;
+            next_node += (size_t)outs[i].n_inner;
+            next_tri += (size_t)outs[i].n_tri;
+            int kc = 0;
+            for (int s2 = 0; s2 < WIDTH; s2++)
+                if (outs[i].kid[s2] >= 0) {
+                    kc++;
+                    if (!outs[i].leaf[s2]) nxt.push_back({outs[i].kid[s2], level[i].depth + 1});
+                }
+            max_kids = std::max(max_kids, kc);
+        }
+        if (next_tri > (size_t)n_tris) return RT_E_ARG;  // a triangle referenced twice
+        words.resize(20 * (n_wide + level.size()));
+        parallel(level.size(), [&](size_t i) {
+            Out& o = outs[i];
+            o.W[4] = (uint32_t)cbase[i];
+            o.W[5] = (uint32_t)tbase[i];
+            uint8_t meta[WIDTH] = {0};
+            int off = 0;
+            for (int s2 = 0; s2 < WIDTH; s2++)
+                if (o.kid[s2] >= 0 && o.leaf[s2]) {
+                    const BNode& c = w.bn[o.kid[s2]];
+                    meta[s2] = (uint8_t)((c.cnt << 5) | off);
+                    for (int t = c.first; t < c.first + c.cnt; t++) order[tbase[i] + (size_t)off++] = w.idx[t];
+                }
+            std::memcpy(&o.W[6], meta, 8);
+            std::memcpy(&words[20 * (n_wide + i)], o.W, sizeof o.W);
+        });
+        n_wide += level.size();
+        n_order = next_tri;
+        level.swap(nxt);
     }
+    order.resize(n_order);
     if ((int)order.size() != n_tris) return RT_E_ARG;  // a triangle referenced twice or never
     uint32_t* nodes = (uint32_t*)std::malloc(sizeof(uint32_t) * words.size());
     int* ord = (int*)std::malloc(sizeof(int) * order.size());

@@ -81,7 +81,8 @@ class SceneInfo(ctypes.Structure):  # rt_scene_info
     _fields_ = [("n_triangles", ctypes.c_int), ("n_lights", ctypes.c_int), ("wide_nodes", ctypes.c_int),
                 ("wide_depth", ctypes.c_int), ("accel_built", ctypes.c_int), ("build_ms", ctypes.c_float),
                 ("gpu_build_ms", ctypes.c_float), ("unit_triangles", ctypes.c_int), ("unit_nodes", ctypes.c_int),
-                ("unit_depth", ctypes.c_int), ("primary_triangles", ctypes.c_int), ("primary_nodes", ctypes.c_int)]
+                ("unit_depth", ctypes.c_int), ("primary_triangles", ctypes.c_int), ("primary_nodes", ctypes.c_int),
+                ("ploc_ms", ctypes.c_float), ("treelet_ms", ctypes.c_float), ("collapse_ms", ctypes.c_float)]
 
 
 class LaunchInfo(ctypes.Structure):  # rt_launch_info
@@ -92,7 +93,7 @@ class LaunchInfo(ctypes.Structure):  # rt_launch_info
 
 # rt_launch_info.build bits (RT_BUILD_*)
 BUILD_BITS = {"waves4": 1, "packed_stack": 2, "packed_tris": 4, "lds_paths": 8, "pool_level": 16, "pool_all": 32,
-              "trace": 64}
+              "trace": 64, "feedback": 128}
 
 
 class CommInfo(ctypes.Structure):  # rt_comm_info

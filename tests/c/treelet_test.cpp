@@ -147,6 +147,12 @@ int main() {
         };
         T.root = build(0, n);
         check_tree(T);
+        {  // threads: disjoint subtrees in parallel, then the nodes above them -- the same tree as one thread makes
+            rtt::Tree A = T, B = T;
+            const double ca = rtt::optimize_pass(A, 1), cb = rtt::optimize_pass(B, 4);
+            CHECK(ca == cb && A.left == B.left && A.right == B.right);
+            for (size_t i = 0; i < A.box.size(); i++) CHECK(same(A.box[i], B.box[i]));
+        }
         double prev = rtt::tree_cost(T);
         for (int pass = 0; pass < 3; pass++) {
             const double c = rtt::optimize_pass(T);

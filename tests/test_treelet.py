@@ -12,7 +12,7 @@ def test_treelet(tmp_path):
     exe = tmp_path / "treelet_test"
     src = os.path.join(ROOT, "tests", "c", "treelet_test.cpp")
     inc = os.path.join(ROOT, "parallel-ray-tracer_amd", "csrc", "hip")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-I", inc, "-o", str(exe), src],
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-Wall", "-Wextra", "-Werror", "-I", inc, "-o", str(exe), src],
                    check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
