@@ -582,8 +582,8 @@ def main():
     # gpu/src/main.cu:110-115: one render_frame per iteration, each waited for) with the library's default rule.
     # RT_VARIANT_HYBRID measures and tries its candidates on the first frames of a shape (rt_get_launch_info: trial /
     # settled); the latency is the median HIP-event time of the frames after the rule has settled -- 72 of them for the
-    # fixed camera, so that one periodic tile-list refresh (a settled measuring frame every 64 frames, `refresh`) is
-    # among them and its cost is reported too. Measured for the reference's fixed camera (frame_latency_ms), for a
+    # fixed camera (with the per-frame feedback no refresh frame is among them; a build without it refreshes the
+    # lists with a settled measuring frame every 64 frames, `refresh`, reported on its own). Measured for the reference's fixed camera (frame_latency_ms), for a
     # walkthrough (every frame's camera moved: the rule is keyed by the frame's shape, so a moving camera settles the
     # same way), and for the fixed camera at the walkthrough's middle measured camera (fixed_at_walk_ms: the walk's
     # cameras see more of the reflective knot, so the walk is compared with a fixed camera where the walk is).
@@ -607,7 +607,7 @@ def main():
         srt = sorted(ts)
         return {"median": srt[len(srt) // 2] if ts else float("nan"), "mean": sum(ts) / len(ts) if ts else float("nan"),
                 "settle": n - len(ts), "info": info, "mid_camera": idx[len(idx) // 2] if idx else 0,
-                "refresh_ms": refresh, "frames": len(ts)}
+                "refresh_ms": refresh, "frames": len(ts), "ts": ts, "idx": idx}
 
     def walk(i):
         c = host.camera(W, H)
@@ -618,10 +618,24 @@ def main():
     if not args.no_latency:
         sd = seam(lambda i: cam, n_after=72)
         sw = seam(walk, n_after=16)
-        sf = seam(lambda i, k=sw["mid_camera"]: walk(k))
+        # the walk against fixed cameras where it was: at 3 of its measured cameras (its quartiles), the fixed camera's
+        # settled median vs the walk's frames at and beside that camera (the walk's cameras differ in cost -- one may
+        # look past the model -- so a frame is compared with its own camera, not with the walk's median)
+        wcams, wat, wfix = [], [], []
+        for q in (1, 2, 3):
+            j = min(len(sw["idx"]) - 1, q * len(sw["idx"]) // 4)
+            if j < 0:
+                break
+            k = sw["idx"][j]
+            near = sorted(sw["ts"][max(0, j - 1):j + 2])
+            wcams.append(k)
+            wat.append(near[len(near) // 2])
+            wfix.append(seam(lambda i, k=k: walk(k))["median"])
+        sf = {"median": wfix[1] if len(wfix) > 1 else nan}
     else:
         sd = sw = sf = {"median": nan, "mean": nan, "settle": None, "info": None, "mid_camera": None, "refresh_ms": [],
                         "frames": 0}
+        wcams, wat, wfix = [], [], []
     lat_default, settle_frames, seam_info = sd["median"], sd["settle"], sd["info"]
     lat_walk, settle_walk = sw["median"], sw["settle"]
     lat = torch.tensor([lat_default], dtype=torch.float64, device="cuda")
@@ -706,18 +720,24 @@ def main():
                                      "refresh_frame_ms": sd["refresh_ms"], "walkthrough_ms": lat_walk,
                                      "walkthrough_mean_ms": sw["mean"], "walkthrough_refresh_ms": sw["refresh_ms"],
                                      "fixed_at_walk_ms": sf["median"], "walk_mid_camera": sw["mid_camera"],
+                                     "walk_cameras": wcams, "walk_at_cameras_ms": wat, "fixed_at_cameras_ms": wfix,
+                                     "walk_vs_fixed": (sum(a / b for a, b in zip(wat, wfix)) / len(wat)) if wat else None,
                                      "settle_frames": settle_frames, "settle_frames_walkthrough": settle_walk,
                                      "choice": seam_info,
                                      "rule": "frame_latency_ms = the default rule (rt_render with rt_frame's launch fields "
                                              "zeroed, render + sync per frame as the reference's loop): median HIP-event "
                                              "time of the 72 frames after rt_get_launch_info reports the rule settled (its "
-                                             "measuring and trial frames excluded; its periodic tile-list refresh, one "
-                                             "settled measuring frame per 64, included: refresh_frame_ms, and in "
-                                             "default_rule_mean_ms), fixed reference camera; walkthrough_ms: the median of 16 "
-                                             "settled frames with the camera moved every frame (their mean, and the tile-list "
-                                             "refresh frames among them: walkthrough_mean_ms, walkthrough_refresh_ms); "
+                                             "measuring and trial frames excluded; every later frame's tile lists are "
+                                             "built on the device from the frame before it, RT_BUILD_FEEDBACK -- a "
+                                             "measuring refresh frame only without it: refresh_frame_ms), fixed reference "
+                                             "camera; default_rule_mean_ms: their mean; walkthrough_ms: the median of 16 "
+                                             "settled frames with the camera moved every frame (walkthrough_mean_ms: their "
+                                             "mean); "
                                              "fixed_at_walk_ms: the fixed "
-                                             "camera placed at the walkthrough's middle measured camera (walk_mid_camera)"},
+                                             "camera placed at the walkthrough's middle measured camera (walk_mid_camera); "
+                                             "walk_vs_fixed: the mean over walk_cameras (the walk's measured quartiles) of "
+                                             "the walk's median frame at and beside that camera (walk_at_cameras_ms) / "
+                                             "the settled median of a fixed camera there (fixed_at_cameras_ms)"},
             "roofline": {**roof, "traffic": traffic,
                          "kernel_ms": k_avg_ms, "alg_bytes_per_launch": bytes_launch, "frames_per_launch": F,
                          # the algorithmic bytes per second and against the HBM peak: not a bound (the

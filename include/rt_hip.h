@@ -126,10 +126,11 @@ enum {
     RT_VARIANT_HYBRID = 11,  /* single 1-spp frames: the tiles a measuring frame of the same SHAPE found costliest through
                                 k_coop (2 or 4 lanes per ray) on a second stream while k_persist or the shadow pool renders
                                 the rest. The first frame of a shape measures (k_persist with per-tile times), the next
-                                ones try the candidates -- including the whole-frame kernels -- three times each, and the
-                                best median renders from then on; every 64 frames a measuring frame renews the tile lists
-                                for a moving camera. Nothing waits on the host: measurements and trials are read by event
-                                queries (rt_frame.hot_pct > 0: that threshold and rt_frame.hot_kernel, no trials) */
+                                ones try the candidates -- including the whole-frame kernels -- four frames each, back
+                                to back, and the best median of the last three renders from then on, each frame's tile lists built on the device from the
+                                previous frame's per-tile times (RT_BUILD_FEEDBACK: a moving camera's lists stay one
+                                frame old). Nothing waits on the host: measurements and trials are read by event queries
+                                (rt_frame.hot_pct > 0: that threshold and rt_frame.hot_kernel, no trials) */
     /* 12: k_relay (1 + lights waves per tile, LDS hand-off), measured slower, removed in round 4: refused */
     RT_VARIANT_SHPOOL = 13,  /* k_persist at 4 waves per SIMD with each bounce level's shadow rays (every pixel's, every
                                 light's) walked as ONE per-wave pool: a lane whose walk ends takes the next unassigned ray,
@@ -256,10 +257,10 @@ typedef struct rt_launch_info {
     int hot_lanes;    /* its lanes per ray (k_coop) or per pixel (k_fan) */
     int cold_variant; /* its kernel of the cold tiles (RT_VARIANT_PERSIST or RT_VARIANT_SHPOOL) */
     int trial;        /* 1: a measuring or trial frame of the default rule */
-    int settled;      /* 1: the configuration of this shape is decided: no trial frames follow (the hybrid rule's
-                         periodic list refresh, every 64 frames of a shape, is reported by `refresh`) */
+    int settled;      /* 1: the configuration of this shape is decided: no trial frames follow */
     int refresh;      /* 1: a decided hybrid shape's measuring frame that renews its tile lists (k_persist with per-tile
-                         times; part of the rule's steady cost, settled = 1) */
+                         times; settled = 1) -- only where the per-frame feedback is off (PRT_FEEDBACK=0 at build time:
+                         a measuring frame every 64 frames of a shape); 0 with it */
     unsigned build;   /* the k_persist instantiation that ran (of the cold tiles, for a hybrid launch): RT_BUILD_* bits;
                          0 for the other kernels (strict, k_coop alone) */
 } rt_launch_info;

@@ -308,9 +308,12 @@ __device__ __forceinline__ void flush_g(Ctr c, unsigned long long* g, unsigned q
 }
 
 // The single-frame feedback (rt_feedback.hpp) ranks 8x8 tiles by the time their last render took; a tile rendered by
-// k_coop is priced at FB_COOP_SCALE times its longest group tile's time, so that a hot tile's cost stays comparable
-// with the cold tiles k_persist rendered (k_coop spends about twice k_persist's wave time per ray, over 2-4 tiles).
-constexpr unsigned FB_COOP_SCALE = 2;
+// k_coop is priced as k_persist would have taken for it, so that hot and cold tiles compare: k_coop spends about twice
+// k_persist's wave time per ray, and its tile holds 64 / G of the 8x8 tile's 64 rays, so a group tile's time t is
+// ~2 T / G of the 8x8 tile's T -- priced at t G / 2 (the longest of the tile's G group tiles). A biased price makes the
+// hot set sticky: priced 2x (G = 2 at a fixed 2x), last frame's hot tiles stayed over the cut and no other tile could
+// reach it, so a moving camera's hot set froze where it had been (a car_boxed walkthrough ~20 % slower than persist).
+template <int G> constexpr unsigned fb_coop_scale() { return G / 2; }
 
 // Pixel tile of one wave: 64 / G pixels.
 template <int G> struct GTile;
@@ -348,7 +351,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, BLOCK), amdgpu_waves_pe
         if (x < A.W && k < A.n_rows) render_pixel<MAXB, false, COUNT, true, G>(A, cam_of<BATCH>(A, frame), frame, x, k, stk, c, q);
         if (A.tile_cost && lane == 0)  // the feedback's cost of the 8x8 tile this tile lies in (rt_feedback.hpp)
             atomicMax(A.tile_cost + (ty * GTile<G>::TH / 8) * A.tiles_x8 + tx * TW / 8,
-                      (unsigned)(__builtin_amdgcn_s_memrealtime() - t0) * FB_COOP_SCALE);
+                      (unsigned)(__builtin_amdgcn_s_memrealtime() - t0) * fb_coop_scale<G>());
         if (TRACE) {  // as k_persist's: {begin, end, wave | fallbacks << 32, wave steps | ray node visits << 32}
             const unsigned fb = wave_sum(q == 0 ? c.fb - fb0 : 0u), ws = wave_sum(c.ws - ws0),
                            nv = wave_sum(q == 0 ? c.chi + c.shi - nd0 : 0u);

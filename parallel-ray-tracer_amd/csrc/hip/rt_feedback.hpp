@@ -17,7 +17,8 @@
 namespace rtd {
 
 struct FbArgs {
-    const unsigned* cost;  // [n_tiles]: the last frame's 8x8 tile durations (KArgs::tile_cost)
+    unsigned* cost;        // [n_tiles + 1]: the last frame's 8x8 tile durations (KArgs::tile_cost), then their maximum
+                           // (k_fb_max; cleared with the durations)
     int n_tiles, tx, ty;   // the 8x8 tile grid of the frame's compact rows
     int pct;               // hot tiles: cost > pct % of the costliest (0: none)
     int hot_cap;           // at most this many hot-kernel tiles (the hottest; k_coop spends ~2x the wave time per ray)
@@ -29,16 +30,22 @@ struct FbArgs {
     int* hot;              // the hot kernel's tiles, hottest first
     int* cold;             // [9 region offsets into the tile part][the cold 8x8 tiles, region by region, costliest first]
     int* counts;           // [0]: the hot kernel's tiles
+    unsigned* table;       // [FB_G][FB_TK]: each workgroup's key counts (k_fb_count -> k_fb_place)
+    int moved;             // the camera differs from the last frame's: the costs have moved with the image by up to
+                           // about a tile, so each tile is priced as the costliest of itself and its 4 neighbours (a
+                           // car_boxed walkthrough -7 %; kept off for a fixed camera, where it costs +5 %)
 };
 
 constexpr int FB_NB = 64;  // cost buckets: 8 per octave below the costliest tile, 8 octaves (cheaper: the last)
 constexpr int FB_THREADS = 1024;
-constexpr int FB_WAVES = FB_THREADS / 64;
-constexpr int FB_GROUPS = 9;  // hot, then the 8 regions' cold tiles
-constexpr int FB_KEYS = FB_GROUPS * FB_NB;
+constexpr int FB_G = 16;      // workgroups (CUs) of each builder kernel: LDS atomics run ~1 lane per clock per CU, and
+                              // one CU for a 1080p frame's 32400 tiles took ~35 us
+constexpr int FB_KEYS = 9 * FB_NB;          // list keys: hot bucket b; cold (region r, bucket b): FB_NB (1 + r) + b
+constexpr int FB_TK = FB_KEYS + 8 * FB_NB;  // + the hot tiles again as cold keys (region r, bucket b): a hot set over
+                                            // hot_cap drops its cheapest buckets to the cold lists (k_fb_place)
 
 // log2(c) in 1/8 octaves (exponent and the mantissa's top 3 bits)
-__device__ __forceinline__ int fb_log8(unsigned c) {
+__host__ __device__ inline int fb_log8(unsigned c) {
     if (c == 0u) return 0;
     const int e = 31 - __builtin_clz(c);
     const unsigned frac = e >= 3 ? (c >> (e - 3)) & 7u : (c << (3 - e)) & 7u;
@@ -57,159 +64,151 @@ __host__ __device__ inline unsigned char fb_tile_info(int t, int tx, int ty, int
     return (unsigned char)(reg | nsub(4, 4) << 3 | nsub(8, 4) << 6);
 }
 
-// One workgroup of 16 waves, wave w owning a contiguous 1/16 of the tiles: the costliest tile (reduction), the hot set
-// (capped at hot_cap, costliest buckets first), then a counting sort by (group, bucket) -- per-wave counts in LDS (no
-// wave contends with another), one exclusive scan in (group, bucket, wave) order, a scatter through the per-wave
-// cursors. The order is costliest bucket first, then tile order within a bucket. The durations come from the other
-// XCDs' kernels (memory, not this L2): each pass loads FB_PER of a lane's tiles at once, so that their latencies overlap
-// (one load at a time made this kernel ~45 us of a 0.95-ms frame).
-constexpr int FB_PER = 32;
-__global__ __launch_bounds__(FB_THREADS) void k_fb_lists(FbArgs F) {
-    __shared__ unsigned cnt[FB_KEYS * FB_WAVES];  // [key][wave]
-    __shared__ unsigned part[FB_WAVES];
-    __shared__ unsigned s_max, s_nhot, s_cut;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nt = F.n_tiles, chunk = (nt + FB_WAVES - 1) / FB_WAVES;
-    const int t0 = wave * chunk, t1 = min(nt, t0 + chunk);
-    for (int i = tid; i < FB_KEYS * FB_WAVES; i += FB_THREADS) cnt[i] = 0u;
-    // the lane's tiles t0 + lane + 64 i, FB_PER at a time: cost (0 past the wave's tiles) and info
-    unsigned c[FB_PER];
-    unsigned char inf[FB_PER];
-    auto load = [&](int base) {
-#pragma unroll
-        for (int i = 0; i < FB_PER; i++) {
-            const int t = t0 + lane + 64 * (base + i);
-            c[i] = t < t1 ? F.cost[t] : 0u;
-            inf[i] = t < t1 ? F.info[t] : (unsigned char)0;
-        }
-    };
-    const int iters = (chunk + 63) / 64;
+// The three kernels (FB_G workgroups of FB_THREADS each, workgroup g owning a contiguous 1/FB_G of the tiles, tile
+// t = t0 + thread + FB_THREADS j) form a counting sort by (group, bucket) -- hot tiles by bucket, costliest first, then
+// each region's cold tiles by bucket; tile order within a bucket does not matter (any order renders the same frame):
+//   k_fb_max   the costliest tile (the buckets are relative to it)
+//   k_fb_count each workgroup's key counts, in its LDS, to table
+//   k_fb_place every workgroup sums the table (its cursors: the keys before, the workgroups before it), caps the hot
+//              set at hot_cap (cheapest hot buckets to the cold lists), and scatters its tiles through LDS cursors.
+struct FbTile {  // a tile's key and weight under the frame's costliest tile
+    int b, grp;  // bucket; group: -1 past the tiles, 0 hot, 1 + region cold
+    unsigned w;  // hot: its hot-kernel tiles
+};
+__device__ __forceinline__ FbTile fb_tile(const FbArgs& F, int t, unsigned cmax) {
+    FbTile r{0, -1, 1u};
+    if (t >= F.n_tiles) return r;
+    unsigned v = F.cost[t];
+    if (F.moved) {  // the camera moved: a tile priced as the costliest of itself and its 4 neighbours
+        const int x = t % F.tx;
+        if (x > 0) v = max(v, F.cost[t - 1]);
+        if (x + 1 < F.tx) v = max(v, F.cost[t + 1]);
+        if (t >= F.tx) v = max(v, F.cost[t - F.tx]);
+        if (t + F.tx < F.n_tiles) v = max(v, F.cost[t + F.tx]);
+    }
+    const int inf = F.info[t];
+    r.b = v == 0u ? FB_NB - 1 : min(FB_NB - 1, fb_log8(cmax) - fb_log8(v));
+    if (F.pct > 0 && (unsigned long long)v * 100ull > (unsigned long long)F.pct * cmax) {
+        r.grp = 0;
+        r.w = (unsigned)(F.tw == 4 ? (inf >> 3) & 7 : inf >> 6);
+    } else {
+        r.grp = 1 + (inf & 7);
+    }
+    return r;
+}
+__device__ __forceinline__ int fb_t0(const FbArgs& F) { return blockIdx.x * ((F.n_tiles + FB_G - 1) / FB_G); }
+__device__ __forceinline__ int fb_t1(const FbArgs& F) { return min(F.n_tiles, fb_t0(F) + (F.n_tiles + FB_G - 1) / FB_G); }
+
+__global__ __launch_bounds__(FB_THREADS) void k_fb_max(FbArgs F) {
+    __shared__ unsigned part[FB_THREADS / 64];
+    const int t1 = fb_t1(F);
     unsigned m = 0u;
-    for (int base = 0; base < iters; base += FB_PER) {
-        load(base);
-#pragma unroll
-        for (int i = 0; i < FB_PER; i++) m = max(m, c[i]);
-    }
+    for (int t = fb_t0(F) + (int)threadIdx.x; t < t1; t += FB_THREADS) m = max(m, F.cost[t]);
     for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
-    if (lane == 0) part[wave] = m;
-    if (tid == 0) {
-        s_nhot = 0u;
-        s_cut = FB_NB;
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        m = threadIdx.x < FB_THREADS / 64 ? part[threadIdx.x] : 0u;
+        for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
+        if (threadIdx.x == 0 && m) atomicMax(F.cost + F.n_tiles, m);
+    }
+}
+
+__global__ __launch_bounds__(FB_THREADS) void k_fb_count(FbArgs F) {
+    __shared__ unsigned h[FB_TK];
+    for (int k = threadIdx.x; k < FB_TK; k += FB_THREADS) h[k] = 0u;
+    __syncthreads();
+    const unsigned cmax = max(1u, F.cost[F.n_tiles]);
+    const int t1 = fb_t1(F);
+    for (int t = fb_t0(F) + (int)threadIdx.x; t < t1; t += FB_THREADS) {
+        const FbTile q = fb_tile(F, t, cmax);
+        if (q.grp == 0) {
+            atomicAdd(&h[q.b], q.w);
+            atomicAdd(&h[FB_KEYS + (F.info[t] & 7) * FB_NB + q.b], 1u);
+        } else {
+            atomicAdd(&h[q.grp * FB_NB + q.b], 1u);
+        }
     }
     __syncthreads();
-    if (tid == 0) {
-        unsigned mm = 1u;
-        for (int w = 0; w < FB_WAVES; w++) mm = max(mm, part[w]);
-        s_max = mm;
+    for (int k = threadIdx.x; k < FB_TK; k += FB_THREADS) F.table[blockIdx.x * FB_TK + k] = h[k];
+}
+
+__global__ __launch_bounds__(FB_THREADS) void k_fb_place(FbArgs F) {
+    __shared__ unsigned tot[FB_TK], mine[FB_TK], cur[FB_KEYS];
+    __shared__ unsigned part[FB_THREADS / 64];
+    __shared__ int s_cut;
+    __shared__ unsigned s_nhot;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = blockIdx.x;
+    for (int k = tid; k < FB_TK; k += FB_THREADS) {  // the key's total, and its count in the workgroups before this one
+        unsigned a = 0u, b = 0u;
+#pragma unroll
+        for (int q = 0; q < FB_G; q++) {
+            const unsigned v = F.table[q * FB_TK + k];
+            a += v;
+            b += q < g ? v : 0u;
+        }
+        tot[k] = a;
+        mine[k] = b;
     }
     __syncthreads();
-    const unsigned cmax = s_max;
-    const int lmax = fb_log8(cmax);
-    const unsigned long long thr = (unsigned long long)F.pct * cmax;
-    auto is_hot = [&](unsigned v) { return F.pct > 0 && (unsigned long long)v * 100ull > thr; };
-    auto bucket = [&](unsigned v) { return v == 0u ? FB_NB - 1 : min(FB_NB - 1, lmax - fb_log8(v)); };
-    int cut = FB_NB;
-    auto key_of = [&](int i, unsigned& w) -> int {  // group * FB_NB + bucket; w: hot-kernel tiles (hot) or 1
-        const int b = bucket(c[i]);
-        if (is_hot(c[i]) && b < cut) {
-            w = (unsigned)(F.tw == 4 ? (inf[i] >> 3) & 7 : inf[i] >> 6);
-            return b;
+    if (wave == 0) {  // the hot buckets, costliest first, while they fit hot_cap (one per lane)
+        unsigned inc = tot[lane];
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned u = (unsigned)__shfl_up((int)inc, o, 64);
+            if (lane >= o) inc += u;
         }
-        w = 1u;
-        return (1 + (inf[i] & 7)) * FB_NB + b;
-    };
-    for (int pass = 0; pass < 2; pass++) {  // the histogram; again with a cut when the hot set exceeds hot_cap (rare)
-        unsigned nh = 0u;
-        for (int base = 0; base < iters; base += FB_PER) {
-            load(base);
-#pragma unroll
-            for (int i = 0; i < FB_PER; i++) {
-                const int t = t0 + lane + 64 * (base + i);
-                if (t >= t1) continue;
-                unsigned w;
-                const int k = key_of(i, w);
-                if (k < FB_NB) nh += w;
-                atomicAdd(&cnt[k * FB_WAVES + wave], w);
-            }
-        }
-        for (int o = 32; o > 0; o >>= 1) nh += (unsigned)__shfl_xor((int)nh, o, 64);
-        if (lane == 0 && nh) atomicAdd(&s_nhot, nh);
-        __syncthreads();
-        if (pass == 1 || s_nhot <= (unsigned)F.hot_cap) break;
-        if (wave == 0) {  // the hot buckets, costliest first, while they fit hot_cap (64 buckets: one per lane)
-            unsigned v = 0u;
-            for (int w = 0; w < FB_WAVES; w++) v += cnt[lane * FB_WAVES + w];  // (hot tiles' k_coop tiles: >= 1 each)
-            unsigned inc = v;
-            for (int o = 1; o < 64; o <<= 1) {
-                const unsigned u = (unsigned)__shfl_up((int)inc, o, 64);
-                if (lane >= o) inc += u;
-            }
-            const unsigned long long over = __ballot(inc > (unsigned)F.hot_cap);
-            if (lane == 0) s_cut = over ? (unsigned)__builtin_ctzll(over) : (unsigned)FB_NB;
-        }
-        __syncthreads();
-        cut = (int)s_cut;
-        for (int i = tid; i < FB_KEYS * FB_WAVES; i += FB_THREADS) cnt[i] = 0u;
-        __syncthreads();
+        const unsigned long long over = __ballot(inc > (unsigned)F.hot_cap);
+        if (lane == 0) s_cut = over ? __builtin_ctzll(over) : FB_NB;
     }
-    // exclusive scan of the [key][wave] counts in place: PER consecutive counts per thread, then the threads' sums
-    constexpr int PER = FB_KEYS * FB_WAVES / FB_THREADS;
-    static_assert(PER * FB_THREADS == FB_KEYS * FB_WAVES, "scan layout");
-    unsigned loc[PER], sum = 0u;
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-        loc[k] = cnt[tid * PER + k];
-        sum += loc[k];
+    __syncthreads();
+    const int cut = s_cut;
+    // the list keys' counts under the cut, exclusive scan over the keys (FB_KEYS <= FB_THREADS: one per thread)
+    unsigned e = 0u, em = 0u;
+    if (tid < FB_KEYS) {
+        const int b = tid % FB_NB;
+        if (tid < FB_NB) {
+            e = b < cut ? tot[tid] : 0u;
+            em = b < cut ? mine[tid] : 0u;
+        } else {
+            const int dk = FB_KEYS + tid - FB_NB;  // the same (region, bucket) among the hot tiles
+            e = tot[tid] + (b >= cut ? tot[dk] : 0u);
+            em = mine[tid] + (b >= cut ? mine[dk] : 0u);
+        }
     }
-    unsigned inc = sum;
+    unsigned inc = e;
     for (int o = 1; o < 64; o <<= 1) {
-        const unsigned v = (unsigned)__shfl_up((int)inc, o, 64);
-        if (lane >= o) inc += v;
+        const unsigned u = (unsigned)__shfl_up((int)inc, o, 64);
+        if (lane >= o) inc += u;
     }
     if (lane == 63) part[wave] = inc;
     __syncthreads();
-    if (tid == 0) {
-        unsigned run = 0u;
-        for (int w = 0; w < FB_WAVES; w++) {
-            const unsigned v = part[w];
-            part[w] = run;
-            run += v;
+    unsigned before = 0u;
+    for (int w = 0; w < wave; w++) before += part[w];
+    const unsigned start = before + inc - e;  // the key's first slot in the lists (hot part, then cold part)
+    if (tid < FB_KEYS) cur[tid] = start + em;
+    if (tid == FB_NB) s_nhot = start;  // (the first cold key's start: the hot total)
+    __syncthreads();
+    const unsigned nhot = s_nhot;
+    if (g == 0) {  // (thread FB_KEYS: e = 0, start = the lists' total)
+        if (tid == 0) F.counts[0] = (int)nhot;
+        if (tid >= FB_NB && tid < FB_KEYS && tid % FB_NB == 0) F.cold[tid / FB_NB - 1] = (int)(start - nhot);
+        if (tid == FB_KEYS) F.cold[8] = (int)(start - nhot);
+    }
+    const unsigned cmax = max(1u, F.cost[F.n_tiles]);
+    const int t1 = fb_t1(F);
+    for (int t = fb_t0(F) + tid; t < t1; t += FB_THREADS) {
+        const FbTile q = fb_tile(F, t, cmax);
+        if (q.grp == 0 && q.b < cut) {  // a hot tile: its hot-kernel tiles
+            int p = (int)atomicAdd(&cur[q.b], q.w);
+            const int sx = 8 / F.tw, sy = 8 / F.th, x0 = (t % F.tx) * sx, y0 = (t / F.tx) * sy;
+            for (int qy = 0; qy < sy; qy++)
+                for (int qx = 0; qx < sx; qx++)
+                    if (x0 + qx < F.ctw && y0 + qy < F.cth) F.hot[p++] = (y0 + qy) * F.ctw + x0 + qx;
+        } else {
+            const int k = (q.grp == 0 ? 1 + (F.info[t] & 7) : q.grp) * FB_NB + q.b;
+            F.cold[9 + (int)(atomicAdd(&cur[k], 1u) - nhot)] = t;
         }
     }
-    __syncthreads();
-    unsigned at = part[wave] + inc - sum;
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-        cnt[tid * PER + k] = at;
-        at += loc[k];
-    }
-    __syncthreads();
-    const unsigned nhot = cnt[FB_NB * FB_WAVES];  // the hot group's total (the first cold key's start)
-    if (tid == 0) F.counts[0] = (int)nhot;
-    if (tid < 8) F.cold[tid] = (int)(cnt[(1 + tid) * FB_NB * FB_WAVES] - nhot);  // region r's start in the tile part
-    __syncthreads();  // (the region starts read before the scatter moves the cursors)
-    for (int base = 0; base < iters; base += FB_PER) {  // scatter through the wave's cursors
-        load(base);
-#pragma unroll
-        for (int i = 0; i < FB_PER; i++) {
-            const int t = t0 + lane + 64 * (base + i);
-            if (t >= t1) continue;
-            unsigned w;
-            const int k = key_of(i, w);
-            const unsigned pos = atomicAdd(&cnt[k * FB_WAVES + wave], w);
-            if (k < FB_NB) {  // a hot tile: its hot-kernel tiles
-                const int sx = 8 / F.tw, sy = 8 / F.th, x0 = (t % F.tx) * sx, y0 = (t / F.tx) * sy;
-                int p = (int)pos;
-                for (int qy = 0; qy < sy; qy++)
-                    for (int qx = 0; qx < sx; qx++)
-                        if (x0 + qx < F.ctw && y0 + qy < F.cth) F.hot[p++] = (y0 + qy) * F.ctw + x0 + qx;
-            } else {
-                F.cold[9 + (int)(pos - nhot)] = t;
-            }
-        }
-    }
-    __syncthreads();
-    if (tid == 0) F.cold[8] = (int)(cnt[FB_KEYS * FB_WAVES - 1] - nhot);  // the last cursor: the cold total
 }
 
 }  // namespace rtd

@@ -170,8 +170,14 @@ struct rt_ctx {
         int state = 0;  // 0: measure next; 1: a measuring frame's tile times are on their way to h_tr; 2: lists ready
         long long frames = 0;  // frames since the choice or the last list refresh
         static constexpr int NCAND = 12;
-        static constexpr int ROUNDS = 3;    // trials per candidate, chosen by their median (single frames are noisy, and
-                                            // some two-stream launches bimodal)
+        static constexpr int ROUNDS = 4;    // trial frames per candidate, back to back: the first untimed (its per-tile
+                                            // times feed the next one's lists), the best median of the other three
+                                            // chosen (single frames are noisy, and some two-stream launches bimodal).
+                                            // Back to back, not round robin: a hybrid candidate's lists are built from
+                                            // the frame before it, and after another candidate's frame they are not the
+                                            // lists it renders with once chosen (a car_boxed walkthrough priced its hot
+                                            // candidates 30-60 % slow and settled on none of them)
+        static constexpr int WARM = 1;
         static constexpr int REFRESH = 64;  // frames of a shape between measuring frames once it is decided
         // candidates: hot threshold (0 = the cold kernel over the whole frame), lanes per ray of k_coop for the hot
         // tiles, the cold tiles' kernel (RT_VARIANT_PERSIST / SHPOOL); their lists at d_lists + at[c]
@@ -191,9 +197,10 @@ struct rt_ctx {
         int cold_mode = 0;  // the cold lists' region layout (xcd_mode) when cold_regions
         hipEvent_t ev = nullptr, fork = nullptr, join = nullptr;
         hipStream_t s2 = nullptr;
-        // per-frame feedback (rt_feedback.hpp): every frame of the shape records its 8x8 tiles' durations in d_cost; a
-        // decided shape's frames build their lists from the previous frame's on the device (d_fb: [hot: 4 x n_tiles]
-        // [cold: 9 + n_tiles][counts: 4]); h_fb_cnt: a recent frame's hot count, read back without waiting (grid sizes)
+        // per-frame feedback (rt_feedback.hpp): every frame of the shape records its 8x8 tiles' durations in d_cost (and
+        // their maximum after them); a decided shape's frames build their lists from the previous frame's on the device
+        // (d_fb: [hot: 4 x n_tiles][cold: 9 + n_tiles][counts: 4][the builder's table: FB_G x FB_TK]); h_fb_cnt: a
+        // recent frame's hot count, read back without waiting (grid sizes)
         unsigned* d_cost = nullptr;
         int* d_fb = nullptr;
         unsigned char* d_info = nullptr;  // rtd::fb_tile_info of every tile, for info_mode
@@ -203,6 +210,9 @@ struct rt_ctx {
         int* h_fb_cnt = nullptr;
         hipEvent_t fb_ev = nullptr;
         bool fb_pending = false;
+        int fb_est_c = -1, fb_pend_c = -1;  // the candidates whose hot counts fb_hot_est / the pending copy hold
+        float fb_cam[12] = {};  // the last feedback frame's camera (pos, ul, ix, iy)
+        bool fb_cam_ok = false;
         int fb_hot_est = -1;
     } hy;
 };
@@ -1626,8 +1636,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 h.d_fb = nullptr;
                 h.d_info = nullptr;
                 h.fb_cap = 0;
-                hipError_t e = hipMalloc((void**)&h.d_cost, sizeof(unsigned) * h.n_tiles);
-                if (e == hipSuccess) e = hipMalloc((void**)&h.d_fb, sizeof(int) * (5 * h.n_tiles + 13));
+                hipError_t e = hipMalloc((void**)&h.d_cost, sizeof(unsigned) * (h.n_tiles + 1));
+                if (e == hipSuccess) e = hipMalloc((void**)&h.d_fb, sizeof(int) * (5 * h.n_tiles + 13 + rtd::FB_G * rtd::FB_TK));
                 if (e == hipSuccess) e = hipMalloc((void**)&h.d_info, h.n_tiles);
                 if (e == hipSuccess && !h.h_fb_cnt) e = hipHostMalloc((void**)&h.h_fb_cnt, sizeof(int) * 4, hipHostMallocDefault);
                 if (e == hipSuccess && !h.fb_ev) e = hipEventCreateWithFlags(&h.fb_ev, hipEventDisableTiming);
@@ -1635,6 +1645,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 h.fb_cap = h.n_tiles;
             }
             h.fb_ok = false;
+            h.fb_cam_ok = false;
             h.fb_hot_est = -1;
             h.info_mode = -1;
             h.state = 0;
@@ -1748,8 +1759,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             li.trial = 0;
             return pick_of(h.choice);
         }
-        for (int r = 0; r < rt_ctx::Hybrid::ROUNDS; r++)
-            for (int c = 0; c < h.nc; c++)
+        for (int c = 0; c < h.nc; c++)
+            for (int r = 0; r < rt_ctx::Hybrid::ROUNDS; r++)
                 if (h.launch[c][r] < 0 || ctx->launches - h.launch[c][r] >= rt_ctx::NEV) {  // untried (or events reused)
                     h.launch[c][r] = ctx->launches;
                     return pick_of(c);
@@ -1762,14 +1773,15 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
         if (!done) return Pick{1, single_rule};  // the trials are still running
         int best = 0;
         for (int c = 0; c < h.nc; c++) {
-            float t[rt_ctx::Hybrid::ROUNDS];
-            for (int r = 0; r < rt_ctx::Hybrid::ROUNDS; r++) {
-                const int sl = (int)(h.launch[c][r] % rt_ctx::NEV);
+            constexpr int W = rt_ctx::Hybrid::WARM, NT = rt_ctx::Hybrid::ROUNDS - W;
+            float t[NT];
+            for (int r = 0; r < NT; r++) {
+                const int sl = (int)(h.launch[c][W + r] % rt_ctx::NEV);
                 const hipError_t e = hipEventElapsedTime(&t[r], ctx->ev0s[sl], ctx->ev1s[sl]);
                 if (e != hipSuccess) return err(e, "rt_render: hybrid trials");
             }
-            std::sort(t, t + rt_ctx::Hybrid::ROUNDS);
-            h.ms[c] = t[rt_ctx::Hybrid::ROUNDS / 2];  // the median
+            std::sort(t, t + NT);
+            h.ms[c] = t[NT / 2];  // the median of the timed trials
             if (h.ms[c] < h.ms[best]) best = c;
         }
         h.choice = best;
@@ -1823,10 +1835,12 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             // the frame's HIP-event time starts here, after the host work of the pick (the trials compare them)
             HIPC(hipEventRecord(ctx->ev0, ctx->stream));
             rt_ctx::Hybrid& h = ctx->hy;
-            // every frame of the shape records its tiles' durations (rt_feedback.hpp); a decided shape's frames build
-            // their lists from the previous frame's first, on the device (the memset follows that build: k_coop's hot
-            // tiles combine their group tiles' times by atomic max)
-            const bool fb = PRT_FEEDBACK && pk.kind == 2 && h.choice >= 0 && h.fb_ok && pk.c == h.choice;
+            // every frame of the shape records its tiles' durations (rt_feedback.hpp); a hybrid candidate's frame --
+            // tried or chosen -- builds its lists from the previous frame's first, on the device (the memset follows
+            // that build: k_coop's hot tiles combine their group tiles' times by atomic max). The trials too: with a
+            // moving camera the measuring frame's lists age frame by frame, and a candidate tried later would be
+            // priced with older lists than one tried first (a car_boxed walkthrough settled on the wrong candidate).
+            const bool fb = PRT_FEEDBACK && pk.kind == 2 && h.fb_ok;
             if (PRT_FEEDBACK && h.d_cost) {
                 if (fb) {
                     li.hot_pct = h.pct[pk.c];
@@ -1837,7 +1851,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                     h.fb_ok = r2 == RT_OK;
                     return r2;
                 }
-                HIPC(hipMemsetAsync(h.d_cost, 0, sizeof(unsigned) * h.n_tiles, ctx->stream));
+                HIPC(hipMemsetAsync(h.d_cost, 0, sizeof(unsigned) * (h.n_tiles + 1), ctx->stream));
                 P.tile_cost = h.d_cost;
                 A.tile_cost = h.d_cost;
                 h.fb_ok = true;  // (this frame, in stream order, fills it)
@@ -2057,7 +2071,7 @@ int launch_hybrid(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsigned*
 }
 
 // A decided shape's frame under the per-frame feedback (rt_feedback.hpp): candidate c's lists built on the device from
-// the previous frame's tile durations (k_fb_lists), the durations cleared, then c's kernels as launch_hybrid launches
+// the previous frame's tile durations (k_fb_max, k_fb_count, k_fb_place), the durations cleared, then c's kernels as launch_hybrid launches
 // them, every one reading its list and count from the device and recording this frame's durations. The grids are sized
 // by a recent frame's hot count, read back without a wait.
 template <int MAXB>
@@ -2079,15 +2093,29 @@ int launch_hybrid_fb(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsign
         h.info_mode = h.cold_mode;
     }
     // (hot set: at most half the 8x8 tiles, as the host's lists, counted in hot-kernel tiles)
-    const rtd::FbArgs F{h.d_cost, A.n_tiles, tx, ty, h.pct[c], (int)(h.n_tiles / 2) * (8 / tw) * (8 / th), tw, th, ctw, cth, h.cold_mode,
-                        h.d_info, d_hot, d_cold, d_cnt};
-    rtd::k_fb_lists<<<1, rtd::FB_THREADS, 0, ctx->stream>>>(F);
+    // (d_cost holds n_tiles + 1 words: A.n_tiles is this shape's n_tiles, the maximum's word right after the tiles)
+    rtd::FbArgs F{h.d_cost, A.n_tiles, tx, ty, h.pct[c], (int)(h.n_tiles / 2) * (8 / tw) * (8 / th), tw, th, ctw, cth, h.cold_mode,
+                        h.d_info, d_hot, d_cold, d_cnt, (unsigned*)(d_cnt + 4), 0};
+    {  // the camera against the last feedback frame's (rt_feedback.hpp FbArgs::moved)
+        float cam[12];
+        std::memcpy(cam, A.pos, sizeof(float) * 3);
+        std::memcpy(cam + 3, A.ul, sizeof(float) * 3);
+        std::memcpy(cam + 6, A.ix, sizeof(float) * 3);
+        std::memcpy(cam + 9, A.iy, sizeof(float) * 3);
+        F.moved = h.fb_cam_ok && std::memcmp(cam, h.fb_cam, sizeof cam) != 0;
+        std::memcpy(h.fb_cam, cam, sizeof cam);
+        h.fb_cam_ok = true;
+    }
+    rtd::k_fb_max<<<rtd::FB_G, rtd::FB_THREADS, 0, ctx->stream>>>(F);
+    rtd::k_fb_count<<<rtd::FB_G, rtd::FB_THREADS, 0, ctx->stream>>>(F);
+    rtd::k_fb_place<<<rtd::FB_G, rtd::FB_THREADS, 0, ctx->stream>>>(F);
     HIPC(hipGetLastError());
-    HIPC(hipMemsetAsync(h.d_cost, 0, sizeof(unsigned) * h.n_tiles, ctx->stream));
+    HIPC(hipMemsetAsync(h.d_cost, 0, sizeof(unsigned) * (h.n_tiles + 1), ctx->stream));
     if (h.fb_pending) {  // a recent frame's hot count (grid size), if its copy has landed: a query, never a wait
         const hipError_t q = hipEventQuery(h.fb_ev);
         if (q == hipSuccess) {
             h.fb_hot_est = h.h_fb_cnt[0];
+            h.fb_est_c = h.fb_pend_c;
             h.fb_pending = false;
         } else if (q == hipErrorNotReady) {
             (void)hipGetLastError();
@@ -2099,6 +2127,7 @@ int launch_hybrid_fb(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsign
         HIPC(hipMemcpyAsync(h.h_fb_cnt, d_cnt, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
         HIPC(hipEventRecord(h.fb_ev, ctx->stream));
         h.fb_pending = true;
+        h.fb_pend_c = c;
     }
     const KFn kc = coop_kernel<MAXB>(g, count);
     rtd::KArgs B = A;  // the hot kernel's tiles, hottest first, their number on the device
@@ -2118,7 +2147,7 @@ int launch_hybrid_fb(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsign
     if (build) *build |= RT_BUILD_FEEDBACK;
     const int rp = resident(kp, ctx->device, 8, dyn);
     const int rcp = resident(kc, ctx->device);
-    const int est = h.fb_hot_est >= 0 ? h.fb_hot_est : h.n_hot[c];
+    const int est = h.fb_hot_est >= 0 && h.fb_est_c == c ? h.fb_hot_est : h.n_hot[c];  // (another candidate's: its own)
     const int nc = hot ? std::max(1, std::min((est + 3) / 4, rcp / 2)) : 0;
     const int np = std::max(1, std::min(rp - (int)((long long)nc * rp / rcp), (A.n_tiles + 3) / 4));
     if (!hot) {  // (the whole frame, costliest first)

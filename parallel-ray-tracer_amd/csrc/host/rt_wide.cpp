@@ -17,11 +17,13 @@
 // for k = 0..7 meets them roughly front to back without sorting.
 #include <algorithm>
 #include <array>
-#include <cstdlib>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "rt_host.h"
@@ -81,16 +83,17 @@ struct WBuilder {
         return b;
     }
 
-    // a leaf range, cut by object median on the widest centroid axis until <= LEAF_MAX triangles
-    int leaf(int first, int cnt) {
+    // a leaf range, cut by object median on the widest centroid axis until <= LEAF_MAX triangles (nodes into out:
+    // bn, or a subtree's own vector when subtrees are made in parallel -- they sort disjoint ranges of idx)
+    int leaf(std::vector<BNode>& out, int first, int cnt) {
         if (cnt <= LEAF_MAX) {
             BNode x;
             x.first = first;
             x.cnt = cnt;
             x.b = empty_box();
             for (int i = first; i < first + cnt; i++) grow(x.b, tri_box(idx[i]));
-            bn.push_back(x);
-            return (int)bn.size() - 1;
+            out.push_back(x);
+            return (int)out.size() - 1;
         }
         float cl[3] = {INFINITY, INFINITY, INFINITY}, ch[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (int i = first; i < first + cnt; i++)
@@ -104,11 +107,11 @@ struct WBuilder {
         std::stable_sort(idx.begin() + first, idx.begin() + first + cnt,
                          [&](int u, int v) { return T[u].centroid[ax] < T[v].centroid[ax]; });
         const int h = cnt / 2;
-        const int l = leaf(first, h), r = leaf(first + h, cnt - h);
-        return inner(l, r);
+        const int l = leaf(out, first, h), r = leaf(out, first + h, cnt - h);
+        return inner(out, l, r);
     }
 
-    int inner(int l, int r) {
+    int inner(std::vector<BNode>& bn, int l, int r) {
         BNode x;
         x.l = l;
         x.r = r;
@@ -131,60 +134,67 @@ struct WBuilder {
     // off a parent using at most i slots — as one leaf slot (<= LEAF_MAX triangles), as one wide node,
     // or by distributing the slots over n's two children. Costs are surface area x (C_node per wide-node
     // visit, 1 per triangle test).
-    std::vector<std::array<float, WIDTH + 1>> cost;
-    std::vector<std::array<signed char, WIDTH + 1>> split;  // dist(n, i): slots given to the left child
-    std::vector<char> as_leaf;                               // cost(n, 1) is the leaf form
-    void sah_costs(float c_node) {
-        const size_t N = bn.size();
-        cost.assign(N, {});
-        split.assign(N, {});
-        as_leaf.assign(N, 0);
-        std::vector<std::array<float, WIDTH + 1>> dist(N);
-        for (size_t n = 0; n < N; n++) {  // children precede parents in bn
+    struct Dp {  // one node's costs, side by side (the collapse reads them node by node, in no memory order)
+        float cost[WIDTH + 1];
+        signed char split[WIDTH + 1];  // dist(n, i): slots given to the left child
+        char as_leaf;                  // cost(n, 1) is the leaf form
+    };
+    std::unique_ptr<Dp[]> dp;  // (uninitialised: every node's entry is written before it is read)
+    void sah_begin() { dp.reset(new Dp[bn.size()]); }
+    // nodes [n0, n1) of bn, whose children precede them within the range or in ranges already costed
+    void sah_costs(size_t n0, size_t n1, float c_node) {
+        for (size_t n = n0; n < n1; n++) {  // children precede parents in bn
             const BNode& B = bn[n];
+            Dp& D = dp[n];
             const float A = area(B.b);
             const float leaf = (B.cnt > 0 && B.cnt <= LEAF_MAX) ? A * (float)B.cnt : INFINITY;
             if (B.l < 0) {
-                for (int i = 1; i <= WIDTH; i++) {
-                    cost[n][i] = leaf;
-                    dist[n][i] = leaf;
-                }
-                as_leaf[n] = 1;
+                for (int i = 1; i <= WIDTH; i++) D.cost[i] = leaf;
+                D.as_leaf = 1;
                 continue;
             }
+            const Dp &L = dp[B.l], &R = dp[B.r];
+            float dist[WIDTH + 1];
             for (int j = 2; j <= WIDTH; j++) {
                 float best = INFINITY;
                 int bk = 1;
                 for (int k = 1; k < j; k++) {
-                    const float c = cost[B.l][k] + cost[B.r][j - k];
+                    const float c = L.cost[k] + R.cost[j - k];
                     if (c < best) {
                         best = c;
                         bk = k;
                     }
                 }
-                dist[n][j] = best;
-                split[n][j] = (signed char)bk;
+                dist[j] = best;
+                D.split[j] = (signed char)bk;
             }
-            const float node = c_node * A + dist[n][WIDTH];
-            as_leaf[n] = leaf <= node;
-            cost[n][1] = std::min(leaf, node);
-            for (int i = 2; i <= WIDTH; i++) cost[n][i] = std::min(cost[n][1], dist[n][i]);
+            const float node = c_node * A + dist[WIDTH];
+            D.as_leaf = leaf <= node;
+            D.cost[1] = std::min(leaf, node);
+            for (int i = 2; i <= WIDTH; i++) D.cost[i] = std::min(D.cost[1], dist[i]);
         }
     }
     // the slots of subtree n given i of them: (bnode, as-leaf) pairs
     void collect(int n, int i, std::vector<std::pair<int, bool>>& out) const {
         const BNode& B = bn[n];
-        if (B.l < 0 || i == 1 || cost[n][i] == cost[n][1]) {
-            out.push_back({n, B.l < 0 || as_leaf[n] != 0});
+        const Dp& D = dp[n];
+        if (B.l < 0 || i == 1 || D.cost[i] == D.cost[1]) {
+            out.push_back({n, B.l < 0 || D.as_leaf != 0});
             return;
         }
-        const int k = split[n][i];
+        const int k = D.split[i];
         collect(B.l, k, out);
         collect(B.r, i - k, out);
     }
 
-    // reference-layout node i -> BNode index (-1: empty subtree)
-    int make(const rt_bvh_node* B, int nn, int i, int depth, bool& bad) {
+    // reference-layout node i -> BNode index in out (-1: empty subtree); top: the subtrees already made, by their
+    // reference node (made in parallel, then appended to bn)
+    int make(std::vector<BNode>& out, const rt_bvh_node* B, int nn, int i, int depth, bool& bad,
+             const std::unordered_map<int, int>* top = nullptr) {
+        if (top) {
+            const auto f = top->find(i);
+            if (f != top->end()) return f->second;
+        }
         if (i < 0 || i >= nn || depth > 64) {
             bad = true;
             return -1;
@@ -195,14 +205,14 @@ struct WBuilder {
                 bad = true;
                 return -1;
             }
-            return leaf(p.child, p.tr_len);
+            return leaf(out, p.child, p.tr_len);
         }
         if (p.child == 0) return -1;
-        const int l = make(B, nn, p.child, depth + 1, bad);
-        const int r = make(B, nn, p.child + 1, depth + 1, bad);
+        const int l = make(out, B, nn, p.child, depth + 1, bad, top);
+        const int r = make(out, B, nn, p.child + 1, depth + 1, bad, top);
         if (l < 0) return r;
         if (r < 0) return l;
-        return inner(l, r);
+        return inner(out, l, r);
     }
 };
 
@@ -277,13 +287,91 @@ extern "C" int rth_wbvh_build_cost(const rt_bvh_node* bvh, int n_nodes, const in
     for (int t : w.idx)
         if (t < 0 || t >= n_tris) return RT_E_ARG;
     w.bn.reserve(2 * (size_t)n_tris + 2);
+    const int nthreads = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+    // the binary tree in parallel: the reference layout's top levels, breadth first, down to ~8 subtrees per thread
+    // (leaves and empty slots stay in the frontier); each subtree into its own vector on the threads, appended to bn
+    // in frontier order (children still precede parents), then the top above them -- the tree a one-thread make()
+    // makes, node for node, in another order of bn
+    struct Front {
+        int i, depth;
+    };
+    std::vector<Front> front{{0, 0}};
+    if (n_tris >= 4096 && nthreads > 1) {
+        for (size_t q = 0; q < front.size() && front.size() < 8 * (size_t)nthreads;) {
+            const Front f = front[q];
+            const bool inner_node = f.i >= 0 && f.i < n_nodes && bvh[f.i].tr_len <= 0 && bvh[f.i].child > 0 &&
+                                    bvh[f.i].child < n_nodes - 1 && f.depth < 64;
+            if (!inner_node) {
+                q++;
+                continue;
+            }
+            front.erase(front.begin() + (long)q);
+            front.push_back({bvh[f.i].child, f.depth + 1});
+            front.push_back({bvh[f.i].child + 1, f.depth + 1});
+        }
+    }
+    {  // (a malformed layout naming one node twice: one thread, as before)
+        std::vector<int> ids;
+        for (const Front& f : front) ids.push_back(f.i);
+        std::sort(ids.begin(), ids.end());
+        if (std::adjacent_find(ids.begin(), ids.end()) != ids.end()) front.assign(1, Front{0, 0});
+    }
+    std::vector<std::vector<BNode>> part(front.size());
+    std::vector<int> proot(front.size(), -1);
+    std::vector<char> pbad(front.size(), 0);
+    auto run_tasks = [&](size_t n, auto&& fn) {  // fn(k) for k < n, taken one at a time by the threads
+        std::atomic<size_t> next{0};
+        auto worker = [&] {
+            for (size_t k; (k = next.fetch_add(1)) < n;) fn(k);
+        };
+        const int nt = (int)std::min<size_t>((size_t)nthreads, n);
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; t++) pool.emplace_back(worker);
+        worker();
+        for (std::thread& th : pool) th.join();
+    };
     bool bad = false;
-    const int root = w.make(bvh, n_nodes, 0, 0, bad);
+    int root;
+    std::vector<size_t> pbase(front.size() + 1, 0);
+    if (front.size() == 1) {
+        root = w.make(w.bn, bvh, n_nodes, 0, 0, bad);
+    } else {
+        run_tasks(front.size(), [&](size_t k) {
+            bool b = false;
+            proot[k] = w.make(part[k], bvh, n_nodes, front[k].i, front[k].depth, b);
+            pbad[k] = b;
+        });
+        std::unordered_map<int, int> top;
+        for (size_t k = 0; k < front.size(); k++) {
+            bad = bad || pbad[k];
+            pbase[k + 1] = pbase[k] + part[k].size();
+            top[front[k].i] = proot[k] >= 0 ? proot[k] + (int)pbase[k] : -1;
+        }
+        w.bn.resize(pbase[front.size()]);
+        run_tasks(front.size(), [&](size_t k) {  // (the subtrees' nodes into place, their children's indices moved)
+            const int off = (int)pbase[k];
+            BNode* dst = w.bn.data() + pbase[k];
+            for (const BNode& x : part[k]) {
+                *dst = x;
+                if (x.l >= 0) {
+                    dst->l += off;
+                    dst->r += off;
+                }
+                dst++;
+            }
+            std::vector<BNode>().swap(part[k]);
+        });
+        root = w.make(w.bn, bvh, n_nodes, 0, 0, bad, &top);
+    }
     if (bad || root < 0) return RT_E_ARG;
     // collapse policy: SAH-optimal, a wide-node visit priced at 2 triangle tests (the best of 2 / 3 / 4 in the
     // measured sweep — dragon -3.5 % vs 4, car_boxed even; the greedy largest-area collapse: +1.6 % / +3 %;
-    // DESIGN.md §3)
-    w.sah_costs(c_node > 0.0f ? c_node : 2.0f);
+    // DESIGN.md §3). The subtrees' ranges of bn on the threads, then the top.
+    const float cn = c_node > 0.0f ? c_node : 2.0f;
+    w.sah_begin();
+    if (front.size() > 1)
+        run_tasks(front.size(), [&](size_t k) { w.sah_costs(pbase[k], pbase[k + 1], cn); });
+    w.sah_costs(pbase[front.size()], w.bn.size(), cn);
 
     // breadth-first: interior children of a wide node get consecutive indices. Level by level: every node of a level
     // is formed independently (its children, slots, quantised planes) on the build's threads, then the level's
@@ -301,13 +389,13 @@ extern "C" int rth_wbvh_build_cost(const rt_bvh_node* bvh, int n_nodes, const in
         const BNode& B = w.bn[it.b];
         std::pair<int, bool> c2[WIDTH];
         int k = 0;
-        if (B.l < 0 || w.as_leaf[it.b]) {
+        if (B.l < 0 || w.dp[it.b].as_leaf) {
             c2[k++] = {it.b, true};  // a leaf root
         } else {  // the cost-optimal distribution of this node's 8 slots
             std::vector<std::pair<int, bool>> tmp;
             tmp.reserve(WIDTH);
-            w.collect(B.l, w.split[it.b][WIDTH], tmp);
-            w.collect(B.r, WIDTH - w.split[it.b][WIDTH], tmp);
+            w.collect(B.l, w.dp[it.b].split[WIDTH], tmp);
+            w.collect(B.r, WIDTH - w.dp[it.b].split[WIDTH], tmp);
             for (auto& pr : tmp) c2[k++] = pr;
         }
         // octant slots: greedy on cost = -dot(centre offset, slot direction)
@@ -395,7 +483,6 @@ extern "C" int rth_wbvh_build_cost(const rt_bvh_node* bvh, int n_nodes, const in
                 W[8 + 4 * a + j] = (uint32_t)q8[a][2 * j] | ((uint32_t)q8[3 + a][2 * j] << 8) |
                                    ((uint32_t)q8[a][2 * j + 1] << 16) | ((uint32_t)q8[3 + a][2 * j + 1] << 24);
     };
-    const int nthreads = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
     auto parallel = [&](size_t n, auto&& fn) {  // fn(i) for i < n, in contiguous chunks over the threads
         const int nt = (int)std::min<size_t>((size_t)nthreads, (n + 255) / 256);
         if (nt <= 1) {

@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--walk", type=float, default=0.0, help="camera moved by i * WALK along x in frame i (a walkthrough)")
+    ap.add_argument("--frames", action="store_true", help="also print every settled frame's kernel ms")
+    ap.add_argument("--start", type=int, default=0, help="walk: the first frame's camera index")
+    ap.add_argument("--hold", action="store_true", help="walk: every frame at the --start camera (a fixed camera there)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import numpy as np
@@ -42,8 +45,9 @@ def main():
             c = cam
             if a.walk:
                 c = host.camera(W, H)
-                c.pos.x += i * a.walk
-                c.ul.x += i * a.walk
+                j = a.start + (0 if a.hold else i)
+                c.pos.x += j * a.walk
+                c.ul.x += j * a.walk
             r.render(c, W, H, kernel=name, rgb=rgb, **kw)
             ms = r.sync()
             info = r.launch_info()
@@ -59,6 +63,8 @@ def main():
         print(f"{a.scene:10s} {spec:22s} bit-exact {same!s:5s} kernel ms median {statistics.median(ks):.3f} "
               f"min {min(ks):.3f} max {max(ks):.3f} ({len(ks)} frames after settling at frame {settled})  wall ms median "
               f"{statistics.median(ws):.3f}  ran {info}", flush=True)
+        if a.frames:
+            print("   frames (settled, kernel ms):", " ".join(f"{k:.3f}" for k in ks), flush=True)
 
 
 if __name__ == "__main__":

@@ -23,6 +23,10 @@ for step in "$@"; do
     parity) run parity 1200 $PT tests/test_gpu_parity.py tests/test_gpu_build.py tests/test_gpu_stress.py ;;
     new)   run new 900 $PT tests/test_gpu_unpacked.py tests/test_gpu_comm.py tests/test_gpu_configs.py -k "unpacked or rccl or dragon-1920" ;;
     suite) run suite 1500 $PT tests ;;
+    seam)  run seam 900 $PT tests/test_gpu_seam.py tests/test_gpu_parity.py -k "seam or hybrid or walkthrough or settles" ;;
+    lat)   run lat_dragon 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline
+           run lat_car 300 python bench.py --scene car_boxed --steps 20 --warmup 5 --no-cpu-baseline
+           run lat_871k 300 python bench.py --scene dragon871k --steps 20 --warmup 5 --no-cpu-baseline ;;
     ab)    run ab 1200 bash tools/ab3.sh "${AB_LIBS:-ab_base tree}" "${AB_CASES:-dragon:shdefer car_boxed:persist4}" ${AB_ROUNDS:-2} ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     benchq) run bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
