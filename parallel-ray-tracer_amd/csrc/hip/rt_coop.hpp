@@ -268,11 +268,11 @@ __device__ __forceinline__ int closest_g(const DScene& s, v3 o, v3 d, float& bes
         if (!tie) return hp >= 0 ? W.tri_orig[hp] : -1;
         CTR_INC(c, fb, C_FALLBACK);  // strict re-walk, redundantly in every lane of the group
         if (TIE_BOUNDED) {  // (bounded just past the tie: closest)
-            const float tb = tie_bound(o, best);
+            const float tb = tie_bound(o, best), cut = best - (tb - best);
             hp = -1;
             nd = 0;
             best = tb;
-            closest_walk<true, COUNT, true>(s.ref, o, d, best, hp, nd, tie, stk, c);
+            closest_walk<true, COUNT, true, TIE_CUT>(s.ref, o, d, best, hp, nd, tie, stk, c, cut);
             if (hp >= 0) return s.ref.tri_orig[hp];
         }
         hp = -1;

@@ -207,6 +207,19 @@ __device__ __forceinline__ float box_exact(v3 lo, v3 hi, v3 o, v3 d) {
     tmax = fminf(tmax, fmaxf(tz1, tz2));
     return (tmax >= tmin && tmax > 0) ? tmin : FMAX;
 }
+// box_exact's entry (bit for bit: the same operations) and the slab's exit in `out` (the tie re-walk's cut)
+__device__ __forceinline__ float box_exact_out(v3 lo, v3 hi, v3 o, v3 d, float& out) {
+    float tx1 = (lo.x - o.x) / d.x, tx2 = (hi.x - o.x) / d.x;
+    float tmin = fminf(tx1, tx2), tmax = fmaxf(tx1, tx2);
+    float ty1 = (lo.y - o.y) / d.y, ty2 = (hi.y - o.y) / d.y;
+    tmin = fmaxf(tmin, fminf(ty1, ty2));
+    tmax = fminf(tmax, fmaxf(ty1, ty2));
+    float tz1 = (lo.z - o.z) / d.z, tz2 = (hi.z - o.z) / d.z;
+    tmin = fmaxf(tmin, fminf(tz1, tz2));
+    tmax = fminf(tmax, fmaxf(tz1, tz2));
+    out = tmax;
+    return (tmax >= tmin && tmax > 0) ? tmin : FMAX;
+}
 
 // ---------------------------------------------------------------- reciprocal slab test (fast kernel)
 // t = lo * inv - o * inv via one FMA per plane; tmax widened by 2 ulp so that the test never rejects

@@ -158,6 +158,29 @@ __device__ __forceinline__ void children(const DBvh& B, int ref, v3 o, v3 d, con
     }
 }
 
+// children<true> with each child's slab exit as well (nx, fx): the strict order and entries bit for bit
+__device__ __forceinline__ void children_out(const DBvh& B, int ref, v3 o, v3 d, int& ni, float& nt, float& nx, int& fi,
+                                             float& ft, float& fx) {
+    const float4* N = B.nodes + 4 * ref;
+    const float4 a = N[0], b = N[1], e = N[2], r = N[3];
+    ni = __float_as_int(r.x);
+    fi = __float_as_int(r.y);
+    nt = box_exact_out(mk(a.x, a.y, a.z), mk(a.w, b.x, b.y), o, d, nx);
+    ft = box_exact_out(mk(b.z, b.w, e.x), mk(e.y, e.z, e.w), o, d, fx);
+    if (ni == EMPTY_REF) nt = FMAX;
+    if (fi == EMPTY_REF) ft = FMAX;
+    if (ft < nt) {
+        const int ti = ni;
+        const float tt = nt, tx = nx;
+        ni = fi;
+        nt = ft;
+        nx = fx;
+        fi = ti;
+        ft = tt;
+        fx = tx;
+    }
+}
+
 // Is a child whose box is entered at t worth visiting? Strict: the reference's test (bvh.c:343-352).
 template <bool STRICT>
 __device__ __forceinline__ bool visit(float t, float best) {
@@ -184,9 +207,13 @@ __device__ __forceinline__ int opaque(int v) {
 // LDS round trip less on the dependent chain of most steps).
 // Returns the leaf position of the best hit in hp (-1: none); `tie` = the final best was matched by
 // another triangle (fast walk only).
-template <bool STRICT, bool COUNT, bool REG = true>
+// CUT (the strict walk of an exact tie, closest()): also skip a child the ray leaves before `cut` -- the reference
+// would visit it, but every triangle in it is hit before cut or not at all, and no triangle is hit before the tie's
+// t, so it holds none the walk could take: the same triangles are taken in the same order, the same one wins, without
+// the walk through every box the ray crosses on its way to the tie (most of what the bounded re-walk visited).
+template <bool STRICT, bool COUNT, bool REG = true, bool CUT = false>
 __device__ __forceinline__ void closest_walk(const DBvh& B, v3 o, v3 d, float& best, int& hp, int& nd, bool& tie,
-                                             int* __restrict__ stk, Ctr& c) {
+                                             int* __restrict__ stk, Ctr& c, float cut = 0.0f) {
     RayPre p = {};
     if (!STRICT) p = ray_pre(o, d);
     int sp = 0, cur = B.root;
@@ -225,8 +252,17 @@ __device__ __forceinline__ void closest_walk(const DBvh& B, v3 o, v3 d, float& b
             }
             int ni, fi;
             float nt, ft;
-            children<STRICT>(B, cur, o, d, p, ni, nt, fi, ft);
-            const bool vn = visit<STRICT>(nt, best), vf = visit<STRICT>(ft, best);
+            bool vn, vf;
+            if constexpr (CUT) {
+                float nx, fx;
+                children_out(B, cur, o, d, ni, nt, nx, fi, ft, fx);
+                vn = visit<STRICT>(nt, best) && !(nx < cut);
+                vf = visit<STRICT>(ft, best) && !(fx < cut);
+            } else {
+                children<STRICT>(B, cur, o, d, p, ni, nt, fi, ft);
+                vn = visit<STRICT>(nt, best);
+                vf = visit<STRICT>(ft, best);
+            }
             if (sp + 2 > STACK) {  // cannot happen for depth <= 32 BVHs; reported, never silent
                 CTR_INC(c, err, C_ERR);
                 break;
@@ -1082,6 +1118,10 @@ __device__ __forceinline__ const DWide& wide_for(const DScene& s, bool unit) {
 #define PRT_TIE_BOUNDED 1
 #endif
 constexpr bool TIE_BOUNDED = PRT_TIE_BOUNDED != 0;
+#ifndef PRT_TIE_CUT
+#define PRT_TIE_CUT 1
+#endif
+constexpr bool TIE_CUT = PRT_TIE_CUT != 0;
 __device__ __forceinline__ float tie_bound(v3 o, float tmin) {
     const float om = fmaxf(fmaxf(__builtin_fabsf(o.x), __builtin_fabsf(o.y)), __builtin_fabsf(o.z));
     return tmin + (tmin + om) * 0x1p-10f;
@@ -1109,12 +1149,13 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
             if (!tie) return hp >= 0 ? s.acc.tri_orig[hp] : -1;
         }
         CTR_INC(c, fb, C_FALLBACK);
-        if (TIE_BOUNDED) {  // an exact tie at t = best: the reference walk bounded just past it (tie_bound)
-            const float tb = tie_bound(o, best);
+        if (TIE_BOUNDED) {  // an exact tie at t = best: the reference walk bounded just past it (tie_bound), and cut
+                            // as far before it (boxes the ray leaves before then hold nothing it could take)
+            const float tb = tie_bound(o, best), cut = best - (tb - best);
             hp = -1;
             nd = 0;
             best = tb;
-            closest_walk<true, COUNT, REG>(s.ref, o, d, best, hp, nd, tie, bstk, c);
+            closest_walk<true, COUNT, REG, TIE_CUT>(s.ref, o, d, best, hp, nd, tie, bstk, c, cut);
             if (hp >= 0) return s.ref.tri_orig[hp];
         }
         hp = -1;
