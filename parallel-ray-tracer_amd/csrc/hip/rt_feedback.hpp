@@ -34,6 +34,11 @@ struct FbArgs {
     int moved;             // the camera differs from the last frame's: the costs have moved with the image by up to
                            // about a tile, so each tile is priced as the costliest of itself and its 4 neighbours (a
                            // car_boxed walkthrough -7 %; kept off for a fixed camera, where it costs +5 %)
+    unsigned* cost_next;   // [n_tiles + 1]: this frame's durations, cleared by k_fb_max (not read by the builder)
+    unsigned long long* zero64;  // nullable: the frame's ray counters, n64 of them, cleared by k_fb_max
+    int n64;
+    unsigned* zero32;      // the persistent kernels' work counters, n32 words, cleared by k_fb_max
+    int n32;
 };
 
 constexpr int FB_NB = 64;  // cost buckets: 8 per octave below the costliest tile, 8 octaves (cheaper: the last)
@@ -103,7 +108,16 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_max(FbArgs F) {
     __shared__ unsigned part[FB_THREADS / 64];
     const int t1 = fb_t1(F);
     unsigned m = 0u;
-    for (int t = fb_t0(F) + (int)threadIdx.x; t < t1; t += FB_THREADS) m = max(m, F.cost[t]);
+    for (int t = fb_t0(F) + (int)threadIdx.x; t < t1; t += FB_THREADS) {
+        m = max(m, F.cost[t]);
+        F.cost_next[t] = 0u;  // (this frame's buffer: the three memsets a frame launched before, folded in here)
+    }
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) F.cost_next[F.n_tiles] = 0u;
+        if (F.zero64)
+            for (int i = threadIdx.x; i < F.n64; i += FB_THREADS) F.zero64[i] = 0ull;
+        for (int i = threadIdx.x; i < F.n32; i += FB_THREADS) F.zero32[i] = 0u;
+    }
     for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
     __syncthreads();

@@ -201,7 +201,9 @@ struct rt_ctx {
         // their maximum after them); a decided shape's frames build their lists from the previous frame's on the device
         // (d_fb: [hot: 4 x n_tiles][cold: 9 + n_tiles][counts: 4][the builder's table: FB_G x FB_TK]); h_fb_cnt: a
         // recent frame's hot count, read back without waiting (grid sizes)
-        unsigned* d_cost = nullptr;
+        unsigned* d_cost = nullptr;  // two buffers of fb_cap + 1 words: the last frame's (cost_at(cost_cur)), the next
+        int cost_cur = 0;            // frame's (cleared by the list builder, k_fb_max: no memset launch per frame)
+        unsigned* cost_at(int i) const { return d_cost + (size_t)i * (fb_cap + 1); }
         int* d_fb = nullptr;
         unsigned char* d_info = nullptr;  // rtd::fb_tile_info of every tile, for info_mode
         int info_mode = -1;
@@ -1636,7 +1638,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 h.d_fb = nullptr;
                 h.d_info = nullptr;
                 h.fb_cap = 0;
-                hipError_t e = hipMalloc((void**)&h.d_cost, sizeof(unsigned) * (h.n_tiles + 1));
+                hipError_t e = hipMalloc((void**)&h.d_cost, sizeof(unsigned) * 2 * (h.n_tiles + 1));
                 if (e == hipSuccess) e = hipMalloc((void**)&h.d_fb, sizeof(int) * (5 * h.n_tiles + 13 + rtd::FB_G * rtd::FB_TK));
                 if (e == hipSuccess) e = hipMalloc((void**)&h.d_info, h.n_tiles);
                 if (e == hipSuccess && !h.h_fb_cnt) e = hipHostMalloc((void**)&h.h_fb_cnt, sizeof(int) * 4, hipHostMallocDefault);
@@ -1800,9 +1802,15 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     // one frame of configuration (variant, cap); d_work holds the persistent grids' work counters, and the
     // ray counters restart with every launch (rt_get_stats reports the frame, not the trial launches)
     auto dispatch = [&](int md, int cp) -> int {
-        if (!ctx->batch_sum)  // a per-frame loop of a batch keeps adding to the batch's counters
-            HIPC(hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT, ctx->stream));
-        HIPC(hipMemsetAsync(ctx->d_work, 0, 1024, ctx->stream));
+        auto clear = [&]() -> int {
+            if (!ctx->batch_sum)  // a per-frame loop of a batch keeps adding to the batch's counters
+                HIPC(hipMemsetAsync(ctx->d_counters, 0, sizeof(unsigned long long) * rtd::NCOUNT, ctx->stream));
+            HIPC(hipMemsetAsync(ctx->d_work, 0, 1024, ctx->stream));
+            return RT_OK;
+        };
+        // (a hybrid frame on device-built lists has its list builder clear them instead: after the pick)
+        if (!(PRT_FEEDBACK && md == RT_VARIANT_HYBRID))
+            if (int rc = clear()) return rc;
         li.variant = md;
         if (kernel == RT_KERNEL_STRICT) {
             li.variant = 0;
@@ -1832,15 +1840,17 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             int rc = RT_OK;
             const Pick pk = hybrid_pick(rc);
             if (rc) return rc;
+            rt_ctx::Hybrid& h = ctx->hy;
+            const bool fb = PRT_FEEDBACK && pk.kind == 2 && h.fb_ok && h.d_cost;
+            if (PRT_FEEDBACK && !fb)
+                if (int rc2 = clear()) return rc2;
             // the frame's HIP-event time starts here, after the host work of the pick (the trials compare them)
             HIPC(hipEventRecord(ctx->ev0, ctx->stream));
-            rt_ctx::Hybrid& h = ctx->hy;
             // every frame of the shape records its tiles' durations (rt_feedback.hpp); a hybrid candidate's frame --
             // tried or chosen -- builds its lists from the previous frame's first, on the device (the memset follows
             // that build: k_coop's hot tiles combine their group tiles' times by atomic max). The trials too: with a
             // moving camera the measuring frame's lists age frame by frame, and a candidate tried later would be
             // priced with older lists than one tried first (a car_boxed walkthrough settled on the wrong candidate).
-            const bool fb = PRT_FEEDBACK && pk.kind == 2 && h.fb_ok;
             if (PRT_FEEDBACK && h.d_cost) {
                 if (fb) {
                     li.hot_pct = h.pct[pk.c];
@@ -1851,9 +1861,11 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                     h.fb_ok = r2 == RT_OK;
                     return r2;
                 }
-                HIPC(hipMemsetAsync(h.d_cost, 0, sizeof(unsigned) * (h.n_tiles + 1), ctx->stream));
-                P.tile_cost = h.d_cost;
-                A.tile_cost = h.d_cost;
+                unsigned* w = h.cost_at(h.cost_cur ^ 1);
+                HIPC(hipMemsetAsync(w, 0, sizeof(unsigned) * (h.n_tiles + 1), ctx->stream));
+                P.tile_cost = w;
+                A.tile_cost = w;
+                h.cost_cur ^= 1;
                 h.fb_ok = true;  // (this frame, in stream order, fills it)
             }
             if (pk.kind == 2) {
@@ -2094,8 +2106,12 @@ int launch_hybrid_fb(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsign
     }
     // (hot set: at most half the 8x8 tiles, as the host's lists, counted in hot-kernel tiles)
     // (d_cost holds n_tiles + 1 words: A.n_tiles is this shape's n_tiles, the maximum's word right after the tiles)
-    rtd::FbArgs F{h.d_cost, A.n_tiles, tx, ty, h.pct[c], (int)(h.n_tiles / 2) * (8 / tw) * (8 / th), tw, th, ctw, cth, h.cold_mode,
-                        h.d_info, d_hot, d_cold, d_cnt, (unsigned*)(d_cnt + 4), 0};
+    // the last frame's times in, this frame's buffer cleared by k_fb_max (with the frame's counters and work words)
+    unsigned* const cost_in = h.cost_at(h.cost_cur);
+    unsigned* const cost_out = h.cost_at(h.cost_cur ^ 1);
+    rtd::FbArgs F{cost_in, A.n_tiles, tx, ty, h.pct[c], (int)(h.n_tiles / 2) * (8 / tw) * (8 / th), tw, th, ctw, cth, h.cold_mode,
+                  h.d_info, d_hot, d_cold, d_cnt, (unsigned*)(d_cnt + 4), 0, cost_out,
+                  ctx->batch_sum ? nullptr : ctx->d_counters, rtd::NCOUNT, ctx->d_work, 1024 / 4};
     {  // the camera against the last feedback frame's (rt_feedback.hpp FbArgs::moved)
         float cam[12];
         std::memcpy(cam, A.pos, sizeof(float) * 3);
@@ -2110,7 +2126,7 @@ int launch_hybrid_fb(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsign
     rtd::k_fb_count<<<rtd::FB_G, rtd::FB_THREADS, 0, ctx->stream>>>(F);
     rtd::k_fb_place<<<rtd::FB_G, rtd::FB_THREADS, 0, ctx->stream>>>(F);
     HIPC(hipGetLastError());
-    HIPC(hipMemsetAsync(h.d_cost, 0, sizeof(unsigned) * (h.n_tiles + 1), ctx->stream));
+    h.cost_cur ^= 1;
     if (h.fb_pending) {  // a recent frame's hot count (grid size), if its copy has landed: a query, never a wait
         const hipError_t q = hipEventQuery(h.fb_ev);
         if (q == hipSuccess) {
@@ -2137,11 +2153,11 @@ int launch_hybrid_fb(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsign
     B.tile_order = d_hot;
     B.region_off = nullptr;
     B.work = A.work + 224;
-    B.tile_cost = h.d_cost;
+    B.tile_cost = cost_out;
     rtd::KArgs P = A;  // the cold 8x8 tiles by region, costliest first (the region offsets hold their number)
     P.region_off = d_cold;
     P.tile_order = d_cold + 9;
-    P.tile_cost = h.d_cost;
+    P.tile_cost = cost_out;
     size_t dyn = 0;
     const KFn kp = persist_kernel<MAXB>(P, h.cold[c], count, ctx->device, dyn, ctx->pk_ok, ctx->tq_ok, build);
     if (build) *build |= RT_BUILD_FEEDBACK;

@@ -13,5 +13,6 @@ run() {  # name args...
 run dragon
 run sportscar --scene sportscar
 run car_boxed --scene car_boxed
+run dragon871k --scene dragon871k
 run two_cars_4k --scene two_cars --width 3840 --height 2160
 run car_boxed_4k_64spp --scene car_boxed --width 3840 --height 2160 --spp 64 --steps 2 --warmup 1 --frames 1
