@@ -262,7 +262,7 @@ __device__ __forceinline__ int closest_g(const DScene& s, v3 o, v3 d, float& bes
     bool tie = false;
     best = FMAX;
     nd = 0;
-    if (!degenerate(d)) {
+    if (!degenerate(d) || (!unit && degenerate_ok(d, s.prim_axes))) {  // (as closest)
         const DWide& W = wide_for(s, unit);
         closest_wide_g<G, COUNT>(W, o, d, best, hp, nd, tie, stk, c, q);
         if (!tie) return hp >= 0 ? W.tri_orig[hp] : -1;

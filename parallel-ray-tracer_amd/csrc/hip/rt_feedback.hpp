@@ -17,8 +17,7 @@
 namespace rtd {
 
 struct FbArgs {
-    unsigned* cost;        // [n_tiles + 1]: the last frame's 8x8 tile durations (KArgs::tile_cost), then their maximum
-                           // (k_fb_max; cleared with the durations)
+    unsigned* cost;        // [n_tiles]: the last frame's 8x8 tile durations (KArgs::tile_cost)
     int n_tiles, tx, ty;   // the 8x8 tile grid of the frame's compact rows
     int pct;               // hot tiles: cost > pct % of the costliest (0: none)
     int hot_cap;           // at most this many hot-kernel tiles (the hottest; k_coop spends ~2x the wave time per ray)
@@ -31,6 +30,7 @@ struct FbArgs {
     int* cold;             // [9 region offsets into the tile part][the cold 8x8 tiles, region by region, costliest first]
     int* counts;           // [0]: the hot kernel's tiles
     unsigned* table;       // [FB_G][FB_TK]: each workgroup's key counts (k_fb_count -> k_fb_place)
+    unsigned* part;        // [3 FB_G]: k_fb_max's per-workgroup maxima and totals (fb_frame)
     int moved;             // the camera differs from the last frame's: the costs have moved with the image by up to
                            // about a tile, so each tile is priced as the costliest of itself and its 4 neighbours (a
                            // car_boxed walkthrough -7 %; kept off for a fixed camera, where it costs +5 %)
@@ -72,7 +72,7 @@ __host__ __device__ inline unsigned char fb_tile_info(int t, int tx, int ty, int
 // The three kernels (FB_G workgroups of FB_THREADS each, workgroup g owning a contiguous 1/FB_G of the tiles, tile
 // t = t0 + thread + FB_THREADS j) form a counting sort by (group, bucket) -- hot tiles by bucket, costliest first, then
 // each region's cold tiles by bucket; tile order within a bucket does not matter (any order renders the same frame):
-//   k_fb_max   the costliest tile (the buckets are relative to it)
+//   k_fb_max   the costliest tile (the buckets are relative to it) and the tiles' total, per workgroup
 //   k_fb_count each workgroup's key counts, in its LDS, to table
 //   k_fb_place every workgroup sums the table (its cursors: the keys before, the workgroups before it), caps the hot
 //              set at hot_cap (cheapest hot buckets to the cold lists), and scatters its tiles through LDS cursors.
@@ -80,7 +80,30 @@ struct FbTile {  // a tile's key and weight under the frame's costliest tile
     int b, grp;  // bucket; group: -1 past the tiles, 0 hot, 1 + region cold
     unsigned w;  // hot: its hot-kernel tiles
 };
-__device__ __forceinline__ FbTile fb_tile(const FbArgs& F, int t, unsigned cmax) {
+// The frame's costliest tile and its tiles' total, from k_fb_max's per-workgroup partials (part: [FB_G] maxima, then
+// [FB_G] totals as lo, hi word pairs), read once per workgroup into LDS by its first thread
+struct FbFrame {
+    unsigned cmax;
+    unsigned long long sum;
+};
+__device__ __forceinline__ FbFrame fb_frame(const FbArgs& F) {
+    __shared__ FbFrame s;
+    if (threadIdx.x == 0) {
+        FbFrame f{1u, 0ull};
+        for (int g = 0; g < FB_G; g++) {
+            f.cmax = max(f.cmax, F.part[g]);
+            f.sum += (unsigned long long)F.part[FB_G + 2 * g] | (unsigned long long)F.part[FB_G + 2 * g + 1] << 32;
+        }
+        s = f;
+    }
+    __syncthreads();
+    return s;
+}
+// hot: over pct % of the costliest tile AND over twice the mean tile -- a frame of even cost (a camera that looks
+// past the model) has no hot tiles at all; by the first test alone half its tiles went to k_coop (a dragon871k
+// walkthrough's frames 0.33 -> 2-4 ms when the model left the view under a choice made while it was in it)
+__device__ __forceinline__ FbTile fb_tile(const FbArgs& F, int t, const FbFrame& fr) {
+    const unsigned cmax = fr.cmax;
     FbTile r{0, -1, 1u};
     if (t >= F.n_tiles) return r;
     unsigned v = F.cost[t];
@@ -93,7 +116,8 @@ __device__ __forceinline__ FbTile fb_tile(const FbArgs& F, int t, unsigned cmax)
     }
     const int inf = F.info[t];
     r.b = v == 0u ? FB_NB - 1 : min(FB_NB - 1, fb_log8(cmax) - fb_log8(v));
-    if (F.pct > 0 && (unsigned long long)v * 100ull > (unsigned long long)F.pct * cmax) {
+    if (F.pct > 0 && (unsigned long long)v * 100ull > (unsigned long long)F.pct * cmax &&
+        (unsigned long long)v * (unsigned long long)F.n_tiles > 2ull * fr.sum) {
         r.grp = 0;
         r.w = (unsigned)(F.tw == 4 ? (inf >> 3) & 7 : inf >> 6);
     } else {
@@ -106,12 +130,19 @@ __device__ __forceinline__ int fb_t1(const FbArgs& F) { return min(F.n_tiles, fb
 
 __global__ __launch_bounds__(FB_THREADS) void k_fb_max(FbArgs F) {
     __shared__ unsigned part[FB_THREADS / 64];
+    __shared__ unsigned long long s_sum;
+    if (threadIdx.x == 0) s_sum = 0ull;
+    __syncthreads();
     const int t1 = fb_t1(F);
     unsigned m = 0u;
+    unsigned long long sum = 0ull;
     for (int t = fb_t0(F) + (int)threadIdx.x; t < t1; t += FB_THREADS) {
-        m = max(m, F.cost[t]);
+        const unsigned v = F.cost[t];
+        m = max(m, v);
+        sum += v;
         F.cost_next[t] = 0u;  // (this frame's buffer: the three memsets a frame launched before, folded in here)
     }
+    if (sum) atomicAdd(&s_sum, sum);
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) F.cost_next[F.n_tiles] = 0u;
         if (F.zero64)
@@ -124,18 +155,21 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_max(FbArgs F) {
     if (threadIdx.x < 64) {
         m = threadIdx.x < FB_THREADS / 64 ? part[threadIdx.x] : 0u;
         for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
-        if (threadIdx.x == 0 && m) atomicMax(F.cost + F.n_tiles, m);
+        if (threadIdx.x == 0) {  // this workgroup's partials (no atomics, nothing to clear between frames)
+            F.part[blockIdx.x] = m;
+            F.part[FB_G + 2 * blockIdx.x] = (unsigned)s_sum;
+            F.part[FB_G + 2 * blockIdx.x + 1] = (unsigned)(s_sum >> 32);
+        }
     }
 }
 
 __global__ __launch_bounds__(FB_THREADS) void k_fb_count(FbArgs F) {
     __shared__ unsigned h[FB_TK];
     for (int k = threadIdx.x; k < FB_TK; k += FB_THREADS) h[k] = 0u;
-    __syncthreads();
-    const unsigned cmax = max(1u, F.cost[F.n_tiles]);
+    const FbFrame fr = fb_frame(F);  // (its barrier also orders the clearing above)
     const int t1 = fb_t1(F);
     for (int t = fb_t0(F) + (int)threadIdx.x; t < t1; t += FB_THREADS) {
-        const FbTile q = fb_tile(F, t, cmax);
+        const FbTile q = fb_tile(F, t, fr);
         if (q.grp == 0) {
             atomicAdd(&h[q.b], q.w);
             atomicAdd(&h[FB_KEYS + (F.info[t] & 7) * FB_NB + q.b], 1u);
@@ -208,10 +242,10 @@ __global__ __launch_bounds__(FB_THREADS) void k_fb_place(FbArgs F) {
         if (tid >= FB_NB && tid < FB_KEYS && tid % FB_NB == 0) F.cold[tid / FB_NB - 1] = (int)(start - nhot);
         if (tid == FB_KEYS) F.cold[8] = (int)(start - nhot);
     }
-    const unsigned cmax = max(1u, F.cost[F.n_tiles]);
+    const FbFrame fr = fb_frame(F);
     const int t1 = fb_t1(F);
     for (int t = fb_t0(F) + tid; t < t1; t += FB_THREADS) {
-        const FbTile q = fb_tile(F, t, cmax);
+        const FbTile q = fb_tile(F, t, fr);
         if (q.grp == 0 && q.b < cut) {  // a hot tile: its hot-kernel tiles
             int p = (int)atomicAdd(&cur[q.b], q.w);
             const int sx = 8 / F.tw, sy = 8 / F.th, x0 = (t % F.tx) * sx, y0 = (t / F.tx) * sy;

@@ -96,6 +96,8 @@ struct rt_ctx {
     // view), packed triangle-test jobs a 26-bit triangle (rtd::TQ_MAX_TRIS); larger scenes run the unpacked builds
     bool pk_ok = true, tq_ok = true;
     float amb[3] = {0.5f, 0.5f, 0.5f};
+    // every face coordinate of the reference tree's child boxes, per axis, sorted (rtd::DScene::prim_axes)
+    std::vector<float> faces[3];
     bool has_scene = false;
     rt_scene_info info{};  // what the last upload built (rt_get_scene_info)
     float t_ploc = 0.0f, t_treelet = 0.0f, t_collapse = 0.0f;  // the upload's build stages (ms; rt_scene_info)
@@ -199,7 +201,8 @@ struct rt_ctx {
         hipStream_t s2 = nullptr;
         // per-frame feedback (rt_feedback.hpp): every frame of the shape records its 8x8 tiles' durations in d_cost (and
         // their maximum after them); a decided shape's frames build their lists from the previous frame's on the device
-        // (d_fb: [hot: 4 x n_tiles][cold: 9 + n_tiles][counts: 4][the builder's table: FB_G x FB_TK]); h_fb_cnt: a
+        // (d_fb: [hot: 4 x n_tiles][cold: 9 + n_tiles][counts: 4][the builder's table: FB_G x FB_TK][its partials:
+        // 3 FB_G]); h_fb_cnt: a
         // recent frame's hot count, read back without waiting (grid sizes)
         unsigned* d_cost = nullptr;  // two buffers of fb_cap + 1 words: the last frame's (cost_at(cost_cur)), the next
         int cost_cur = 0;            // frame's (cleared by the list builder, k_fb_max: no memset launch per frame)
@@ -741,6 +744,20 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     int wide_depth = 0;
     int rc = build_view(ctx, sc->bvh, sc->n_nodes, sc->tri_idx, sc->triangles, n, 0.0f, hr);
     if (rc) return rc;
+    for (int a = 0; a < 3; a++) ctx->faces[a].clear();
+    for (size_t r = 0; r + 3 < hr.nodes.size(); r += 4) {  // node record: L.min, L.max, R.min, R.max (build_view)
+        const float4 p = hr.nodes[r], q = hr.nodes[r + 1], e = hr.nodes[r + 2];
+        const float fx[4] = {p.x, p.w, q.z, e.y}, fy[4] = {p.y, q.x, q.w, e.z}, fz[4] = {p.z, q.y, e.x, e.w};
+        for (int k = 0; k < 4; k++) {
+            ctx->faces[0].push_back(fx[k]);
+            ctx->faces[1].push_back(fy[k]);
+            ctx->faces[2].push_back(fz[k]);
+        }
+    }
+    for (int a = 0; a < 3; a++) {
+        std::sort(ctx->faces[a].begin(), ctx->faces[a].end());
+        ctx->faces[a].erase(std::unique(ctx->faces[a].begin(), ctx->faces[a].end()), ctx->faces[a].end());
+    }
     bool own_acc = sc->accel != RT_ACCEL_REFERENCE;
     int built = sc->accel == RT_ACCEL_REFERENCE ? RT_ACCEL_REFERENCE : RT_ACCEL_HOST;
     float gpu_ms = 0.0f;
@@ -1305,6 +1322,18 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     A.s.amb_x = ctx->amb[0];
     A.s.amb_y = ctx->amb[1];
     A.s.amb_z = ctx->amb[2];
+    // axes on which no frame's camera coordinate is a face of the reference tree's boxes: its primary rays with a zero
+    // direction component there take the fast walk (rt_kernels.hpp degenerate_ok; -0 == +0 counts as a face)
+    A.s.prim_axes = 0;
+    for (int a = 0; a < 3; a++) {
+        bool ok = true;
+        for (int i = 0; i < n_frames && ok; i++) {
+            const float c = a == 0 ? cams[i].pos.x : a == 1 ? cams[i].pos.y : cams[i].pos.z;
+            const auto it = std::lower_bound(ctx->faces[a].begin(), ctx->faces[a].end(), c);
+            ok = c == c && !(it != ctx->faces[a].end() && *it == c);
+        }
+        if (ok) A.s.prim_axes |= 1 << a;
+    }
     const rt_vec3* cv[4] = {&cam->pos, &cam->ul, &cam->inc_x, &cam->inc_y};
     float* dst[4] = {A.pos, A.ul, A.ix, A.iy};
     for (int i = 0; i < 4; i++) {
@@ -1639,7 +1668,7 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 h.d_info = nullptr;
                 h.fb_cap = 0;
                 hipError_t e = hipMalloc((void**)&h.d_cost, sizeof(unsigned) * 2 * (h.n_tiles + 1));
-                if (e == hipSuccess) e = hipMalloc((void**)&h.d_fb, sizeof(int) * (5 * h.n_tiles + 13 + rtd::FB_G * rtd::FB_TK));
+                if (e == hipSuccess) e = hipMalloc((void**)&h.d_fb, sizeof(int) * (5 * h.n_tiles + 13 + rtd::FB_G * (rtd::FB_TK + 3)));
                 if (e == hipSuccess) e = hipMalloc((void**)&h.d_info, h.n_tiles);
                 if (e == hipSuccess && !h.h_fb_cnt) e = hipHostMalloc((void**)&h.h_fb_cnt, sizeof(int) * 4, hipHostMallocDefault);
                 if (e == hipSuccess && !h.fb_ev) e = hipEventCreateWithFlags(&h.fb_ev, hipEventDisableTiming);
@@ -1663,10 +1692,11 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
             // the tile lists of every candidate threshold: [hot tiles][cold 8x8 tiles], one after another
             const int tx = A.tiles_x, ty = A.n_tiles / A.tiles_x;
             std::vector<long long> dur(h.n_tiles);
-            long long cmax = 1;
+            long long cmax = 1, dsum = 0;
             for (size_t t = 0; t < h.n_tiles; t++) {
                 dur[t] = (long long)(h.h_tr[4 * t + 1] - h.h_tr[4 * t]);
                 cmax = std::max(cmax, dur[t]);
+                dsum += dur[t];
             }
             std::vector<int> ord = centre_out(tx, ty);
             if (!dealt_centre_out)
@@ -1697,7 +1727,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
                 if (h.pct[c] == 0 && !h.lpt[c]) continue;
                 std::vector<int> hot8;
                 for (size_t t = 0; t < h.n_tiles && h.pct[c] > 0; t++)
-                    if (dur[t] * 100 > (long long)h.pct[c] * cmax) hot8.push_back((int)t);
+                    if (dur[t] * 100 > (long long)h.pct[c] * cmax && dur[t] * (long long)h.n_tiles > 2 * dsum)
+                        hot8.push_back((int)t);  // (and over twice the mean: rt_feedback.hpp fb_tile)
                 std::stable_sort(hot8.begin(), hot8.end(), [&](int a, int b) { return dur[a] > dur[b]; });
                 if (hot8.size() > h.n_tiles / 2) hot8.resize(h.n_tiles / 2);  // k_coop costs ~2x the wave time
                 std::vector<char> is_hot(h.n_tiles, 0);
@@ -2110,7 +2141,8 @@ int launch_hybrid_fb(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsign
     unsigned* const cost_in = h.cost_at(h.cost_cur);
     unsigned* const cost_out = h.cost_at(h.cost_cur ^ 1);
     rtd::FbArgs F{cost_in, A.n_tiles, tx, ty, h.pct[c], (int)(h.n_tiles / 2) * (8 / tw) * (8 / th), tw, th, ctw, cth, h.cold_mode,
-                  h.d_info, d_hot, d_cold, d_cnt, (unsigned*)(d_cnt + 4), 0, cost_out,
+                  h.d_info, d_hot, d_cold, d_cnt, (unsigned*)(d_cnt + 4), (unsigned*)(d_cnt + 4) + rtd::FB_G * rtd::FB_TK, 0,
+                  cost_out,
                   ctx->batch_sum ? nullptr : ctx->d_counters, rtd::NCOUNT, ctx->d_work, 1024 / 4};
     {  // the camera against the last feedback frame's (rt_feedback.hpp FbArgs::moved)
         float cam[12];
@@ -2164,7 +2196,11 @@ int launch_hybrid_fb(rt_ctx* ctx, const rtd::KArgs& A, bool count, int c, unsign
     const int rp = resident(kp, ctx->device, 8, dyn);
     const int rcp = resident(kc, ctx->device);
     const int est = h.fb_hot_est >= 0 && h.fb_est_c == c ? h.fb_hot_est : h.n_hot[c];  // (another candidate's: its own)
-    const int nc = hot ? std::max(1, std::min((est + 3) / 4, rcp / 2)) : 0;
+    // the hot kernel's grid from a count a few frames old: with headroom (2x + 64 tiles), since a hot set that grew
+    // past its grid's waves -- a moving camera's, after frames of few hot tiles -- is rendered by too few waves (dragon
+    // walkthrough frames of 3-6 ms among ~1.1 ms ones); a persistent grid's waves that find no tile exit at once
+    const int est_h = 2 * est + 64;
+    const int nc = hot ? std::max(1, std::min((est_h + 3) / 4, rcp / 2)) : 0;
     const int np = std::max(1, std::min(rp - (int)((long long)nc * rp / rcp), (A.n_tiles + 3) / 4));
     if (!hot) {  // (the whole frame, costliest first)
         kp<<<np, rtd::BLOCK, dyn, ctx->stream>>>(with_slots(P, dyn));

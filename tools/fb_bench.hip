@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
     unsigned char* d_info;
     int *d_hot, *d_cold, *d_counts;
     CK(hipMalloc(&d_cost, (nt + 1) * 4));
-    CK(hipMalloc(&d_table, rtd::FB_G * rtd::FB_TK * 4));
+    CK(hipMalloc(&d_table, rtd::FB_G * (rtd::FB_TK + 3) * 4));
     unsigned* d_next;
     CK(hipMalloc(&d_next, (nt + 1) * 4));
     cost.push_back(0u);
@@ -45,7 +45,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&d_counts, 16));
     CK(hipMemcpy(d_cost, cost.data(), (nt + 1) * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_info, info.data(), nt, hipMemcpyHostToDevice));
-    rtd::FbArgs F{d_cost, nt, tx, ty, pct, nt, 4, 4, (W + 3) / 4, (H + 3) / 4, 3, d_info, d_hot, d_cold, d_counts, d_table, 0, d_next, nullptr, 0, nullptr, 0};
+    rtd::FbArgs F{d_cost, nt, tx, ty, pct, nt, 4, 4, (W + 3) / 4, (H + 3) / 4, 3, d_info, d_hot, d_cold, d_counts, d_table, d_table + rtd::FB_G * rtd::FB_TK, 0, d_next, nullptr, 0, nullptr, 0};
     auto run = [&]() {
         rtd::k_fb_max<<<rtd::FB_G, rtd::FB_THREADS>>>(F);
         rtd::k_fb_count<<<rtd::FB_G, rtd::FB_THREADS>>>(F);
