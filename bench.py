@@ -619,17 +619,17 @@ def main():
         sd = seam(lambda i: cam, n_after=72)
         sw = seam(walk, n_after=16)
         # the walk against fixed cameras where it was: at 3 of its measured cameras (its quartiles), the fixed camera's
-        # settled median vs the walk's frames at and beside that camera (the walk's cameras differ in cost -- one may
-        # look past the model -- so a frame is compared with its own camera, not with the walk's median)
+        # settled median vs the walk's frame at that camera (the walk's cameras differ in cost -- one may look past the
+        # model, one may put the centre column's primary rays on a box face -- so a frame is compared with its own
+        # camera, not with the walk's median or its neighbours)
         wcams, wat, wfix = [], [], []
         for q in (1, 2, 3):
             j = min(len(sw["idx"]) - 1, q * len(sw["idx"]) // 4)
             if j < 0:
                 break
             k = sw["idx"][j]
-            near = sorted(sw["ts"][max(0, j - 1):j + 2])
             wcams.append(k)
-            wat.append(near[len(near) // 2])
+            wat.append(sw["ts"][j])
             wfix.append(seam(lambda i, k=k: walk(k))["median"])
         sf = {"median": wfix[1] if len(wfix) > 1 else nan}
     else:
@@ -736,7 +736,7 @@ def main():
                                              "fixed_at_walk_ms: the fixed "
                                              "camera placed at the walkthrough's middle measured camera (walk_mid_camera); "
                                              "walk_vs_fixed: the mean over walk_cameras (the walk's measured quartiles) of "
-                                             "the walk's median frame at and beside that camera (walk_at_cameras_ms) / "
+                                             "the walk's frame at that camera (walk_at_cameras_ms) / "
                                              "the settled median of a fixed camera there (fixed_at_cameras_ms)"},
             "roofline": {**roof, "traffic": traffic,
                          "kernel_ms": k_avg_ms, "alg_bytes_per_launch": bytes_launch, "frames_per_launch": F,

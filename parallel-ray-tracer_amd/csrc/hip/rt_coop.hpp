@@ -262,7 +262,7 @@ __device__ __forceinline__ int closest_g(const DScene& s, v3 o, v3 d, float& bes
     bool tie = false;
     best = FMAX;
     nd = 0;
-    if (!degenerate(d) || (!unit && degenerate_ok(d, s.prim_axes))) {  // (as closest)
+    if (!degenerate(d) || degenerate_ok(s, o, d)) {  // (as closest)
         const DWide& W = wide_for(s, unit);
         closest_wide_g<G, COUNT>(W, o, d, best, hp, nd, tie, stk, c, q);
         if (!tie) return hp >= 0 ? W.tri_orig[hp] : -1;
@@ -288,7 +288,8 @@ __device__ __forceinline__ int closest_g(const DScene& s, v3 o, v3 d, float& bes
 template <int G, bool COUNT>
 __device__ __forceinline__ bool visible_g(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c,
                                           unsigned q) {
-    if (!degenerate(d)) return visible_wide_g<G, COUNT>(wide_for(s, true), o, d, ld2, stk, c, q);  // |d| = 1
+    if (!degenerate(d) || degenerate_ok(s, o, d))  // |d| = 1
+        return visible_wide_g<G, COUNT>(wide_for(s, true), o, d, ld2, stk, c, q);
     CTR_INC(c, fb, C_FALLBACK);
     return visible_walk<true, COUNT, true>(s.ref, o, d, ld2, stk, c);
 }

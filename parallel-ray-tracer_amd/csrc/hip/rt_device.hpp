@@ -61,10 +61,12 @@ struct DScene {
     const float4* __restrict__ lights;
     int n_lights;
     float amb_x, amb_y, amb_z;
-    // the axes on which a primary ray with a zero direction component may still take the fast walk (bit a: no child
-    // box of the reference tree has a face at the camera's coordinate a, so the reference's slab test divides no 0 by
-    // 0 there and culls nothing the ordinary test keeps; rt_hip.hip prim_axes). Other degenerate rays walk strictly.
-    int prim_axes;
+    // every face coordinate of the reference tree's child boxes, per axis, sorted: [n_face[0] x][n_face[1] y]
+    // [n_face[2] z] (rt_hip.hip upload; nullable): a ray with a zero direction component whose origin lies on no face
+    // of that axis divides no 0 by 0 in the reference's slab test, which then culls nothing the ordinary test keeps,
+    // so it may take the fast walk (rt_kernels.hpp degenerate_ok)
+    int n_face[3];
+    const float* __restrict__ faces;
     // the fast walk's view for unit-length directions (reflection and shadow rays): `wide` without the triangles
     // no such ray can hit — hit_triangle culls |det| < EPS and |det| <= |n| |d| (rt_hip.hip unit_view); nodes ==
     // nullptr: `wide` serves every ray
@@ -129,7 +131,7 @@ struct KArgs {
 // agree on every offset (an LDS pointer, 32-bit on gfx950 but 64-bit on the host, once shifted every
 // later field and hung a kernel). Pinned sizes catch such drift at compile time in whichever pass
 // disagrees; never put address-space-qualified pointers in these structs.
-static_assert(sizeof(DWide) == 32 && sizeof(DScene) == 224 && sizeof(KArgs) == 488,
+static_assert(sizeof(DWide) == 32 && sizeof(DScene) == 240 && sizeof(KArgs) == 504,
               "kernel-argument layout changed: update the pinned sizes only after checking both passes agree");
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

@@ -96,8 +96,10 @@ struct rt_ctx {
     // view), packed triangle-test jobs a 26-bit triangle (rtd::TQ_MAX_TRIS); larger scenes run the unpacked builds
     bool pk_ok = true, tq_ok = true;
     float amb[3] = {0.5f, 0.5f, 0.5f};
-    // every face coordinate of the reference tree's child boxes, per axis, sorted (rtd::DScene::prim_axes)
+    // every face coordinate of the reference tree's child boxes, per axis, sorted; on the device one after another
+    // (rtd::DScene::faces)
     std::vector<float> faces[3];
+    float* d_faces = nullptr;
     bool has_scene = false;
     rt_scene_info info{};  // what the last upload built (rt_get_scene_info)
     float t_ploc = 0.0f, t_treelet = 0.0f, t_collapse = 0.0f;  // the upload's build stages (ms; rt_scene_info)
@@ -307,8 +309,10 @@ void free_scene(rt_ctx* ctx) {
     ctx->prim_nodes = ctx->prim_tris = nullptr;
     ctx->prim_orig = nullptr;
     ctx->prim_n = ctx->prim_depth = ctx->prim_tris_n = 0;
-    for (void* p : {(void*)ctx->d_shade, (void*)ctx->d_mats, (void*)ctx->d_lights})
+    for (void* p : {(void*)ctx->d_shade, (void*)ctx->d_mats, (void*)ctx->d_lights, (void*)ctx->d_faces})
         if (p) (void)hipFree(p);
+    ctx->d_faces = nullptr;
+    for (auto& f : ctx->faces) f.clear();
     ctx->d_shade = nullptr;
     ctx->d_mats = nullptr;
     ctx->d_lights = nullptr;
@@ -744,19 +748,21 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     int wide_depth = 0;
     int rc = build_view(ctx, sc->bvh, sc->n_nodes, sc->tri_idx, sc->triangles, n, 0.0f, hr);
     if (rc) return rc;
-    for (int a = 0; a < 3; a++) ctx->faces[a].clear();
+    // the reference tree's child-box faces per axis, sorted (rtd::DScene::faces), uploaded with the scene below
+    std::vector<float> faces[3], all_faces;
     for (size_t r = 0; r + 3 < hr.nodes.size(); r += 4) {  // node record: L.min, L.max, R.min, R.max (build_view)
         const float4 p = hr.nodes[r], q = hr.nodes[r + 1], e = hr.nodes[r + 2];
         const float fx[4] = {p.x, p.w, q.z, e.y}, fy[4] = {p.y, q.x, q.w, e.z}, fz[4] = {p.z, q.y, e.x, e.w};
         for (int k = 0; k < 4; k++) {
-            ctx->faces[0].push_back(fx[k]);
-            ctx->faces[1].push_back(fy[k]);
-            ctx->faces[2].push_back(fz[k]);
+            faces[0].push_back(fx[k]);
+            faces[1].push_back(fy[k]);
+            faces[2].push_back(fz[k]);
         }
     }
     for (int a = 0; a < 3; a++) {
-        std::sort(ctx->faces[a].begin(), ctx->faces[a].end());
-        ctx->faces[a].erase(std::unique(ctx->faces[a].begin(), ctx->faces[a].end()), ctx->faces[a].end());
+        std::sort(faces[a].begin(), faces[a].end());
+        faces[a].erase(std::unique(faces[a].begin(), faces[a].end()), faces[a].end());
+        all_faces.insert(all_faces.end(), faces[a].begin(), faces[a].end());
     }
     bool own_acc = sc->accel != RT_ACCEL_REFERENCE;
     int built = sc->accel == RT_ACCEL_REFERENCE ? RT_ACCEL_REFERENCE : RT_ACCEL_HOST;
@@ -937,7 +943,7 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
     free_scene(ctx);
     if ((rc = upload_view(ctx, hr, ctx->ref)) || (own_acc && (rc = upload_view(ctx, ha, ctx->acc))) ||
         (rc = upload(ctx, &ctx->d_shade, shade)) || (rc = upload(ctx, &ctx->d_mats, mats)) ||
-        (rc = upload(ctx, &ctx->d_lights, lights)) ||
+        (rc = upload(ctx, &ctx->d_lights, lights)) || (rc = upload(ctx, &ctx->d_faces, all_faces)) ||
         (!wide_nodes.empty() && ((rc = upload(ctx, &ctx->wide_nodes, wide_nodes)) ||
                                  (rc = upload(ctx, &ctx->wide_tris, wide_tris)) ||
                                  (rc = upload(ctx, &ctx->wide_orig, wide_orig)))) ||
@@ -950,6 +956,7 @@ extern "C" int rt_upload_scene(rt_ctx* ctx, const rt_scene* sc) {
         free_scene(ctx);
         return rc;
     }
+    for (int a = 0; a < 3; a++) ctx->faces[a].swap(faces[a]);
     ctx->wide_n = (int)(wide_nodes.size() / 5);
     ctx->wide_depth = wide_depth;
     ctx->unit_n = (int)(unit_nodes.size() / 5);
@@ -1322,18 +1329,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     A.s.amb_x = ctx->amb[0];
     A.s.amb_y = ctx->amb[1];
     A.s.amb_z = ctx->amb[2];
-    // axes on which no frame's camera coordinate is a face of the reference tree's boxes: its primary rays with a zero
-    // direction component there take the fast walk (rt_kernels.hpp degenerate_ok; -0 == +0 counts as a face)
-    A.s.prim_axes = 0;
-    for (int a = 0; a < 3; a++) {
-        bool ok = true;
-        for (int i = 0; i < n_frames && ok; i++) {
-            const float c = a == 0 ? cams[i].pos.x : a == 1 ? cams[i].pos.y : cams[i].pos.z;
-            const auto it = std::lower_bound(ctx->faces[a].begin(), ctx->faces[a].end(), c);
-            ok = c == c && !(it != ctx->faces[a].end() && *it == c);
-        }
-        if (ok) A.s.prim_axes |= 1 << a;
-    }
+    A.s.faces = ctx->d_faces;  // (rt_kernels.hpp degenerate_ok)
+    for (int a = 0; a < 3; a++) A.s.n_face[a] = (int)ctx->faces[a].size();
     const rt_vec3* cv[4] = {&cam->pos, &cam->ul, &cam->inc_x, &cam->inc_y};
     float* dst[4] = {A.pos, A.ul, A.ix, A.iy};
     for (int i = 0; i < 4; i++) {

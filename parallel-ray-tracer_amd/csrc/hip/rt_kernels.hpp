@@ -115,13 +115,27 @@ __device__ __forceinline__ void flush(const Ctr& c, unsigned long long* g) {
 }
 
 __device__ __forceinline__ bool degenerate(v3 d) { return d.x == 0.0f || d.y == 0.0f || d.z == 0.0f; }
-// a degenerate direction whose zero components all lie on axes in `ok` (DScene::prim_axes, for primary rays): the
-// reference's slab test then behaves as the ordinary one -- (lo - o) / 0 is an infinity, never 0 / 0 -- so the fast
-// walk finds what it finds (the even-width centre column: ~1,300 strict walks per dragon frame on half the cameras
-// of a walkthrough, +0.2-0.4 ms per single frame)
-__device__ __forceinline__ bool degenerate_ok(v3 d, int ok) {
-    const int z = (d.x == 0.0f ? 1 : 0) | (d.y == 0.0f ? 2 : 0) | (d.z == 0.0f ? 4 : 0);
-    return (z & ~ok) == 0;
+// v is one of the n sorted face coordinates f (lower bound; -0 == +0 counts as equal)
+__device__ __forceinline__ bool on_face(const float* __restrict__ f, int n, float v) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (f[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < n && f[lo] == v;
+}
+// a degenerate direction (a zero component) whose origin lies on no box face of the reference tree along each zero
+// axis: the reference's slab test then divides no 0 by 0 -- (lo - o) / 0 is an infinity -- and behaves as the
+// ordinary one, so the fast walk finds what the reference finds (the even-width centre column's primary rays: ~1,300
+// strict walks per dragon frame on most cameras of a walkthrough, +0.2-0.4 ms per single frame; their reflections
+// off axis-aligned walls). An origin on such a face (a camera coordinate a vertex shares) walks strictly.
+__device__ __forceinline__ bool degenerate_ok(const DScene& s, v3 o, v3 d) {
+    if (!s.faces) return false;
+    if (d.x == 0.0f && on_face(s.faces, s.n_face[0], o.x)) return false;
+    if (d.y == 0.0f && on_face(s.faces + s.n_face[0], s.n_face[1], o.y)) return false;
+    if (d.z == 0.0f && on_face(s.faces + s.n_face[0] + s.n_face[1], s.n_face[2], o.z)) return false;
+    return o.x == o.x && o.y == o.y && o.z == o.z;
 }
 
 // fast-walk pruning: visit a box whose entry is within 4 ulp of the best hit, so that a triangle tied
@@ -1147,7 +1161,7 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
     bool tie = false;
     best = FMAX;
     nd = 0;
-    if (!STRICT && (!degenerate(d) || (!unit && degenerate_ok(d, s.prim_axes)))) {
+    if (!STRICT && (!degenerate(d) || degenerate_ok(s, o, d))) {
         if (s.wide.nodes) {
             const DWide& W = wide_for(s, unit);
             closest_wide<COUNT, PIPE, PK, TQ>(W, o, d, best, hp, nd, tie, stk, c, wcap, tq, c.top[unit ? 1 : 0]);
@@ -1180,7 +1194,7 @@ template <bool STRICT, bool COUNT, bool REG = true, bool PIPE = false, bool PK =
 __device__ __forceinline__ bool visible(const DScene& s, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c,
                                         int* __restrict__ sstk = nullptr, int wcap = WSTACK, int* tq = nullptr) {
     int* __restrict__ bstk = sstk ? sstk : stk;
-    if (!STRICT && !degenerate(d)) {
+    if (!STRICT && (!degenerate(d) || degenerate_ok(s, o, d))) {
         if (s.wide.nodes)  // |d| = 1
             return visible_wide<COUNT, PIPE, PK, TQ>(wide_for(s, true), o, d, ld2, stk, c, wcap, tq, c.top[1]);
         return visible_walk<false, COUNT, REG>(s.acc, o, d, ld2, bstk, c);

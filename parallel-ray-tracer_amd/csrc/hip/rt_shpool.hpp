@@ -161,7 +161,7 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
                 ld2 = dot(tmp, tmp);
                 o = ipo;
                 d = l;
-                if (degenerate(d)) {  // zero direction component: the reference's NaN slabs, walked strictly
+                if (degenerate(d) && !degenerate_ok(s, o, d)) {  // a 0 / 0 in the reference's slabs: walked strictly
                     CTR_INC(c, fb, C_FALLBACK);
                     if (visible_walk<true, COUNT, true>(s.ref, o, d, ld2, sstk ? sstk : stk, c))
                         atomicOr(reinterpret_cast<unsigned*>(lvl + (wo & 511)) + 3, 1u << ((wo >> 9) & 31));
