@@ -67,6 +67,11 @@ struct DScene {
     // so it may take the fast walk (rt_kernels.hpp degenerate_ok)
     int n_face[3];
     const float* __restrict__ faces;
+    // the reference tree's paths (rt_hip.hip build_view): [n_tris: original triangle -> its leaf][leaf -> the record
+    // holding its box]; a record's parent is its 4th float4's z (-1: the root). rt_kernels.hpp ref_reaches
+    const int* __restrict__ ref_path;
+    int n_tris;
+    int pad_path;
     // the fast walk's view for unit-length directions (reflection and shadow rays): `wide` without the triangles
     // no such ray can hit — hit_triangle culls |det| < EPS and |det| <= |n| |d| (rt_hip.hip unit_view); nodes ==
     // nullptr: `wide` serves every ray
@@ -131,7 +136,7 @@ struct KArgs {
 // agree on every offset (an LDS pointer, 32-bit on gfx950 but 64-bit on the host, once shifted every
 // later field and hung a kernel). Pinned sizes catch such drift at compile time in whichever pass
 // disagrees; never put address-space-qualified pointers in these structs.
-static_assert(sizeof(DWide) == 32 && sizeof(DScene) == 240 && sizeof(KArgs) == 504,
+static_assert(sizeof(DWide) == 32 && sizeof(DScene) == 256 && sizeof(KArgs) == 520,
               "kernel-argument layout changed: update the pinned sizes only after checking both passes agree");
 
 // ---------------------------------------------------------------- vec_t arithmetic (cpu/src/vec.c)

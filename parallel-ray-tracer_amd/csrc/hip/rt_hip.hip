@@ -47,6 +47,7 @@ struct DevView {
     int2* leaves = nullptr;
     float4* tris = nullptr;
     int* orig = nullptr;
+    int* path = nullptr;  // [n_tris: original triangle -> its leaf][n_leaves: leaf -> parent record] (ref view)
     int root = 0, n_inner = 0, n_leaves = 0;
     size_t bytes = 0;
 };
@@ -55,6 +56,7 @@ struct HostView {
     std::vector<float4> nodes, tris;
     std::vector<int2> leaves;
     std::vector<int> orig;
+    std::vector<int> path;  // DevView::path
     int root = 0;
 };
 
@@ -286,7 +288,7 @@ int arg_err(rt_ctx* c, const char* msg) {
 }
 
 void free_view(DevView& v) {
-    for (void* p : {(void*)v.nodes, (void*)v.leaves, (void*)v.tris, (void*)v.orig})
+    for (void* p : {(void*)v.nodes, (void*)v.leaves, (void*)v.tris, (void*)v.orig, (void*)v.path})
         if (p) (void)hipFree(p);
     v = DevView();
 }
@@ -389,6 +391,19 @@ int build_view(rt_ctx* ctx, const rt_bvh_node* B, int nn, const int* tri_idx, co
     if (ref[0] == rtd::EMPTY_REF) return arg_err(ctx, "rt_upload_scene: empty root");
     v.root = ref[0];
     v.nodes.resize(4 * inner.size());
+    // parents: a record's in its 4th float4's z (-1: the root), a leaf's in path[n + leaf]; path[t]: triangle t's leaf
+    std::vector<int> parent(inner.size(), -1);
+    v.path.assign((size_t)n + v.leaves.size(), -1);
+    for (size_t r = 0; r < inner.size(); r++) {
+        const rt_bvh_node& p = B[inner[r]];
+        for (int k = 0; k < 2; k++) {
+            const int c = ref[p.child + k];
+            if (c >= 0) parent[c] = (int)r;
+            else if (c != rtd::EMPTY_REF) v.path[(size_t)n + ~c] = (int)r;
+        }
+    }
+    for (size_t l = 0; l < v.leaves.size(); l++)
+        for (int i = v.leaves[l].x; i < v.leaves[l].x + v.leaves[l].y; i++) v.path[tri_idx[i]] = (int)l;
     for (size_t r = 0; r < inner.size(); r++) {
         const rt_bvh_node& p = B[inner[r]];
         rt_bvh_node L = B[p.child], R = B[p.child + 1];
@@ -404,7 +419,7 @@ int build_view(rt_ctx* ctx, const rt_bvh_node* B, int nn, const int* tri_idx, co
         v.nodes[4 * r + 0] = make_float4(L.min.x, L.min.y, L.min.z, L.max.x);
         v.nodes[4 * r + 1] = make_float4(L.max.y, L.max.z, R.min.x, R.min.y);
         v.nodes[4 * r + 2] = make_float4(R.min.z, R.max.x, R.max.y, R.max.z);
-        v.nodes[4 * r + 3] = make_float4(i2f(ref[p.child]), i2f(ref[p.child + 1]), 0.0f, 0.0f);
+        v.nodes[4 * r + 3] = make_float4(i2f(ref[p.child]), i2f(ref[p.child + 1]), i2f(parent[r]), 0.0f);
     }
     tri_records(T, tri_idx, n, v.tris, v.orig);
     return RT_OK;
@@ -414,7 +429,8 @@ int upload_view(rt_ctx* ctx, const HostView& h, DevView& d) {
     int rc;
     d.bytes = 0;
     if ((rc = upload(ctx, &d.nodes, h.nodes, &d.bytes)) || (rc = upload(ctx, &d.leaves, h.leaves, &d.bytes)) ||
-        (rc = upload(ctx, &d.tris, h.tris, &d.bytes)) || (rc = upload(ctx, &d.orig, h.orig, &d.bytes)))
+        (rc = upload(ctx, &d.tris, h.tris, &d.bytes)) || (rc = upload(ctx, &d.orig, h.orig, &d.bytes)) ||
+        (rc = upload(ctx, &d.path, h.path, &d.bytes)))
         return rc;
     d.root = h.root;
     d.n_inner = (int)(h.nodes.size() / 4);
@@ -1330,6 +1346,8 @@ int render_batch(rt_ctx* ctx, const rt_camera* cams, int n_frames, const rt_fram
     A.s.amb_y = ctx->amb[1];
     A.s.amb_z = ctx->amb[2];
     A.s.faces = ctx->d_faces;  // (rt_kernels.hpp degenerate_ok)
+    A.s.ref_path = ctx->ref.path;  // (rt_kernels.hpp ref_reaches)
+    A.s.n_tris = ctx->n_tris;
     for (int a = 0; a < 3; a++) A.s.n_face[a] = (int)ctx->faces[a].size();
     const rt_vec3* cv[4] = {&cam->pos, &cam->ul, &cam->inc_x, &cam->inc_y};
     float* dst[4] = {A.pos, A.ul, A.ix, A.iy};

@@ -138,6 +138,29 @@ __device__ __forceinline__ bool degenerate_ok(const DScene& s, v3 o, v3 d) {
     return o.x == o.x && o.y == o.y && o.z == o.z;
 }
 
+// The reference walk reaches triangle t (original index) of a degenerate ray (a zero component of d): no child box
+// on its reference path, leaf to root, has a face at the origin's coordinate along a zero axis -- those the
+// reference's slab test culls (0 / 0, §2). Every box on the path holds the hit point, so it is on no other side of the
+// origin there. The fast walk's winner t, reached, is then the reference's (nothing is hit before it).
+__device__ __forceinline__ bool ref_reaches(const DScene& s, int t, v3 o, v3 d) {
+    const int leaf = s.ref_path[t];
+    int cur = ~leaf, r = s.ref_path[s.n_tris + leaf];
+    for (int depth = 0; r >= 0; depth++) {
+        if (depth > 64) return false;  // (a malformed path: the strict walk decides)
+        const float4* N = s.ref.nodes + 4 * r;
+        const float4 a = N[0], b = N[1], e = N[2], q = N[3];
+        const bool left = __float_as_int(q.x) == cur;
+        const v3 lo = left ? mk(a.x, a.y, a.z) : mk(b.z, b.w, e.x);
+        const v3 hi = left ? mk(a.w, b.x, b.y) : mk(e.y, e.z, e.w);
+        if (d.x == 0.0f && (lo.x == o.x || hi.x == o.x)) return false;
+        if (d.y == 0.0f && (lo.y == o.y || hi.y == o.y)) return false;
+        if (d.z == 0.0f && (lo.z == o.z || hi.z == o.z)) return false;
+        cur = r;
+        r = __float_as_int(q.z);
+    }
+    return true;
+}
+
 // fast-walk pruning: visit a box whose entry is within 4 ulp of the best hit, so that a triangle tied
 // with the best hit is always reached (and the tie detected) despite the reciprocal test's rounding.
 constexpr float PRUNE_SLACK = 1.0000005f;
@@ -1161,18 +1184,31 @@ __device__ __forceinline__ int closest(const DScene& s, v3 o, v3 d, float& best,
     bool tie = false;
     best = FMAX;
     nd = 0;
-    if (!STRICT && (!degenerate(d) || degenerate_ok(s, o, d))) {
+    // a degenerate ray whose origin lies on a face: the fast walk, then its winner's reference path checked (chk)
+    const bool face = degenerate(d) && !degenerate_ok(s, o, d);
+    const bool chk = face && s.ref_path != nullptr && o.x == o.x && o.y == o.y && o.z == o.z;
+    if (!STRICT && (!face || chk)) {
+        bool done = false;  // the fast walk's answer stands
+        int orig = -1;
         if (s.wide.nodes) {
             const DWide& W = wide_for(s, unit);
             closest_wide<COUNT, PIPE, PK, TQ>(W, o, d, best, hp, nd, tie, stk, c, wcap, tq, c.top[unit ? 1 : 0]);
-            if (!tie) return hp >= 0 ? W.tri_orig[hp] : -1;
+            if (!tie) {
+                orig = hp >= 0 ? W.tri_orig[hp] : -1;
+                done = true;
+            }
         } else {
             closest_walk<false, COUNT, REG>(s.acc, o, d, best, hp, nd, tie, bstk, c);
-            if (!tie) return hp >= 0 ? s.acc.tri_orig[hp] : -1;
+            if (!tie) {
+                orig = hp >= 0 ? s.acc.tri_orig[hp] : -1;
+                done = true;
+            }
         }
+        if (done && (!chk || orig < 0 || ref_reaches(s, orig, o, d))) return orig;
         CTR_INC(c, fb, C_FALLBACK);
-        if (TIE_BOUNDED) {  // an exact tie at t = best: the reference walk bounded just past it (tie_bound), and cut
-                            // as far before it (boxes the ray leaves before then hold nothing it could take)
+        if (TIE_BOUNDED && !done) {  // an exact tie at t = best: the reference walk bounded just past it (tie_bound),
+                                     // and cut as far before it (boxes the ray leaves before then hold nothing it
+                                     // could take)
             const float tb = tie_bound(o, best), cut = best - (tb - best);
             hp = -1;
             nd = 0;
