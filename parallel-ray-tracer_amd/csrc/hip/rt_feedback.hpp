@@ -2,12 +2,13 @@
 //
 // The reference renders and waits frame by frame (cpu/src/main.c:171-185; gpu/src/main.cu:111-114 -> gpu.cu:98-127), so
 // a single frame is as long as its slowest tile, and the order in which the persistent waves take the tiles decides
-// how much of the chip that tail leaves idle. Once the default rule has chosen a configuration for the frame shape,
-// every frame's kernels record each 8x8 tile's duration (one s_memrealtime pair per tile, KArgs::tile_cost), and the
-// next frame's tile lists are built from them on the device, before its kernels, on the same stream: the tiles over
-// pct % of the costliest go to k_coop (the chosen candidate's hot tiles, hottest first), the others to the cold kernel
-// costliest first within each XCD region (longest processing time first). No measuring frame, no host round trip: a
-// moving camera's lists are one frame old instead of up to 64 (the periodic refresh they replace).
+// how much of the chip that tail leaves idle. Every frame's kernels record each 8x8 tile's duration (one s_memrealtime
+// pair per tile, KArgs::tile_cost), and a hybrid candidate's frame -- tried or chosen by the default rule -- builds its
+// tile lists from the previous frame's on the device, before its kernels, on the same stream: the tiles over pct % of
+// the costliest (and over twice the mean) go to k_coop (hottest first), the others to the cold kernel costliest first
+// within each XCD region (longest processing time first). No measuring frame after the first, no host round trip: a
+// moving camera's lists are one frame old instead of up to 64 (the periodic refresh they replace), priced by each
+// tile's neighbourhood when the camera moved (FbArgs::moved).
 //
 // The order of the tiles changes which wave renders a pixel and when, never what it computes: every frame is bit-exact
 // whatever the lists hold (tests/test_gpu_seam.py).

@@ -1,4 +1,4 @@
-// Stand-alone timing of the feedback list builder (rt_feedback.hpp k_fb_lists) on synthetic tile costs, away from the
+// Stand-alone timing of the feedback list builder (rt_feedback.hpp: k_fb_max, k_fb_count, k_fb_place) on synthetic tile costs, away from the
 // frame's kernels: 1080p's 8x8 tile grid, costs log-normal around ~5 us of s_memrealtime ticks, region layout 3.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -Iinclude -Iparallel-ray-tracer_amd/csrc/hip tools/fb_bench.hip -o /tmp/fb_bench
 #include <hip/hip_runtime.h>
