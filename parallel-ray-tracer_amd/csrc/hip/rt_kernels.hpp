@@ -535,6 +535,72 @@ __device__ __forceinline__ float fma_half(unsigned h2, int hi, float k, float a)
     else __asm__("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h2), "v"(k), "v"(a));
     return r;
 }
+// fma_half with the result clamped to [0, 1] by the instruction's clamp bit (the shadow walks' rescaled t, below)
+__device__ __forceinline__ float fma_half_clamp(unsigned h2, int hi, float k, float a) {
+    float r;
+    if (hi)
+        __asm__("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0] clamp" : "=v"(r) : "v"(h2), "v"(k), "v"(a));
+    else __asm__("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0] clamp" : "=v"(r) : "v"(h2), "v"(k), "v"(a));
+    return r;
+}
+
+// Shadow walks on rescaled t (PRT_SHADOW_CLAMP). A shadow walk's box interval is tested against [BOX_TMIN, reach]
+// with reach fixed per ray (shadow_reach: a hit beyond it cannot occlude, and the walk ends at the first occluder, so
+// the running `best` only ever pruned between the light and reach). With t' = (t - BOX_TMIN) / (reach - BOX_TMIN) the
+// interval is [0, 1], which the plane FMA's clamp bit applies for free: the ray's constants are rescaled once
+// (ray_pre_shadow), and the slot test is max3(clamped near) < min3(clamped far) -- 2 VALU per slot (16 per visit)
+// fewer than the max / min with BOX_TMIN and lim. Strict <: a box left before BOX_TMIN or entered after reach clamps
+// both ends to 0 or both to 1 and fails it; a box holding a point t* in (BOX_TMIN, reach] has every computed near
+// below t*' and every far above it by the inflation's margin (the rescale adds 2-3 ulp of max|coord| / |d| of rounding
+// to the few the plane FMA had, still covered >= 10x by 2^-16 max|coord|), so lo' < t*' <= hi' or lo' <= t*' < hi'.
+#ifndef PRT_SHADOW_CLAMP
+#define PRT_SHADOW_CLAMP 1
+#endif
+constexpr bool SHADOW_CLAMP = PRT_SHADOW_CLAMP != 0;
+__device__ __forceinline__ RayPre ray_pre_shadow(v3 o, v3 d, float reach) {
+    RayPre p = ray_pre(o, d);
+    if (SHADOW_CLAMP) {
+        // s <= 1 / (reach - BOX_TMIN) up to one rounding, then 2^-20 smaller: the [0, 1] of t' covers [BOX_TMIN, reach]
+        // (reach <= BOX_TMIN: nothing can occlude; any positive scale is then conservative)
+        const float span = reach - BOX_TMIN;
+        const float s = span > 1e-30f ? (1.0f / span) * 0.999999f : 1.0f;
+        p.ox = (p.ox + BOX_TMIN) * s;
+        p.ix *= s;
+        p.iy *= s;
+        p.iz *= s;
+        p.oy = (p.oy + BOX_TMIN) * s;
+        p.oz = (p.oz + BOX_TMIN) * s;
+    }
+    return p;
+}
+// The closest walks' lim moves with every hit, so their t is only shifted and scaled by the exact 2^-40
+// (ray_pre_closest; PRT_CLOSEST_CLAMP): [BOX_TMIN, BOX_TMIN + 2^40] is [0, 1], the clamp bit applies the lower end, and
+// the upper end stays an explicit min with the scaled lim (closest_lim): 1 VALU per slot fewer. No hit distance of
+// a scene comes near 2^40, and 2^-40 keeps the planes' scale 2^e / d far from the denormals; a zero direction
+// component's 1e20 reciprocal (safe_dir) only sends that axis' slab ends to 0 and 1 together, as to -/+huge before.
+#ifndef PRT_CLOSEST_CLAMP
+#define PRT_CLOSEST_CLAMP 0
+#endif
+constexpr bool CLOSEST_CLAMP = PRT_CLOSEST_CLAMP != 0;
+constexpr float CLAMP_SCALE = 0x1p-40f;
+__device__ __forceinline__ RayPre ray_pre_closest(v3 o, v3 d) {
+    RayPre p = ray_pre(o, d);
+    if (CLOSEST_CLAMP) {
+        p.ox = (p.ox + BOX_TMIN) * CLAMP_SCALE;
+        p.oy = (p.oy + BOX_TMIN) * CLAMP_SCALE;
+        p.oz = (p.oz + BOX_TMIN) * CLAMP_SCALE;
+        p.ix *= CLAMP_SCALE;
+        p.iy *= CLAMP_SCALE;
+        p.iz *= CLAMP_SCALE;
+    }
+    return p;
+}
+// the closest walks' box limit: best * PRUNE_SLACK, or under CLOSEST_CLAMP that limit in the rescaled t (one FMA, one
+// rounding of a value 4 ulp above best: ties stay reached)
+__device__ __forceinline__ float closest_lim(float best) {
+    if (CLOSEST_CLAMP) return __builtin_fmaf(best, PRUNE_SLACK * CLAMP_SCALE, -BOX_TMIN * CLAMP_SCALE);
+    return best * PRUNE_SLACK;
+}
 
 // Tests the 8 children of wide node `node`: nh = hit interior slots as bits (s ^ oct), th = triangle
 // bits (relative to tbase) of every hit leaf slot.
@@ -602,7 +668,9 @@ __device__ __forceinline__ WNode wload_at(gnodes base, int node, const float4* t
 #define PRT_LATE_TRIS 1
 #endif
 constexpr bool LATE_TRIS = PRT_LATE_TRIS != 0;
-template <bool COUNT, bool LATE = false>
+// CLAMP 1: p is ray_pre_shadow's (t rescaled so that [BOX_TMIN, reach] is [0, 1]); lim is unused. CLAMP 2: p is
+// ray_pre_closest's, lim closest_lim's
+template <bool COUNT, bool LATE = false, int CLAMP = 0>
 __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsigned oct, float lim, unsigned& nh,
                                           unsigned& th, int& cbase, int& tbase, unsigned& imask, unsigned& nleaf,
                                           unsigned ord_xor = 0u) {
@@ -639,6 +707,32 @@ __device__ __forceinline__ void wide_node(const WNode& nd, const RayPre& p, unsi
 #pragma unroll
     for (int s = HIT_ADDC ? 7 : 0; HIT_ADDC ? s >= 0 : s < 8; s += HIT_ADDC ? -1 : 1) {
         const int j = s >> 1, hb = s & 1;
+        if constexpr (CLAMP == 2) {  // (ray_pre_closest)
+            const float tnx = fma_half_clamp(plane_pair(wx[j], nsx), hb, kx, ax);
+            const float tfx = fma_half(plane_pair(wx[j], fsx), hb, kx, ax);
+            const float tny = fma_half_clamp(plane_pair(wy[j], nsy), hb, ky, ay);
+            const float tfy = fma_half(plane_pair(wy[j], fsy), hb, ky, ay);
+            const float tnz = fma_half_clamp(plane_pair(wz[j], nsz), hb, kz, az);
+            const float tfz = fma_half(plane_pair(wz[j], fsz), hb, kz, az);
+            const float lo = max3_raw(tnx, tny, tnz);
+            const float hi = min3_raw(tfx, tfy, min_raw(tfz, lim));
+            if (HIT_ADDC) hit8 = shift_in(hit8, lo < hi);
+            else hit8 |= lo < hi ? (1u << s) : 0u;
+            continue;
+        }
+        if constexpr (CLAMP == 1) {  // (ray_pre_shadow)
+            const float tnx = fma_half_clamp(plane_pair(wx[j], nsx), hb, kx, ax);
+            const float tfx = fma_half_clamp(plane_pair(wx[j], fsx), hb, kx, ax);
+            const float tny = fma_half_clamp(plane_pair(wy[j], nsy), hb, ky, ay);
+            const float tfy = fma_half_clamp(plane_pair(wy[j], fsy), hb, ky, ay);
+            const float tnz = fma_half_clamp(plane_pair(wz[j], nsz), hb, kz, az);
+            const float tfz = fma_half_clamp(plane_pair(wz[j], fsz), hb, kz, az);
+            const float lo = max3_raw(tnx, tny, tnz);
+            const float hi = min3_raw(tfx, tfy, tfz);
+            if (HIT_ADDC) hit8 = shift_in(hit8, lo < hi);
+            else hit8 |= lo < hi ? (1u << s) : 0u;
+            continue;
+        }
         const float tnx = fma_half(plane_pair(wx[j], nsx), hb, kx, ax);
         const float tfx = fma_half(plane_pair(wx[j], fsx), hb, kx, ax);
         const float tny = fma_half(plane_pair(wy[j], nsy), hb, ky, ay);
@@ -966,7 +1060,7 @@ template <bool COUNT, bool PIPE = false, bool PK = false, bool TQ = false>
 __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& best, int& hp, int& nd, bool& tie,
                                              int* __restrict__ stk, Ctr& c, int wcap = WSTACK, int* tq = nullptr,
                                              const float4* top = nullptr) {
-    const RayPre p = ray_pre(o, d);
+    const RayPre p = ray_pre_closest(o, d);
     const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
     int sp = 0;
     TopC tc;
@@ -976,7 +1070,7 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
         unsigned nh, th, imask, nl;
         int cb, tb;
         pin_node(N);
-        wide_node<COUNT, LATE_TRIS>(N, p, oct, best * PRUNE_SLACK, nh, th, cb, tb, imask, nl);
+        wide_node<COUNT, LATE_TRIS, CLOSEST_CLAMP ? 2 : 0>(N, p, oct, closest_lim(best), nh, th, cb, tb, imask, nl);
         const unsigned m0 = __float_as_uint(N.f1.z), m1 = __float_as_uint(N.f1.w);
         const int next = wide_step_next<PK>(nh, cb, imask, oct, sp, tc, stk, wcap);
         // the next node's loads go out before this node's triangle tests, unconditionally (a walk that has ended
@@ -1057,10 +1151,10 @@ __device__ __forceinline__ void closest_wide(const DWide& W, v3 o, v3 d, float& 
 template <bool COUNT, bool PIPE = false, bool PK = false, bool TQ = false>
 __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float ld2, int* __restrict__ stk, Ctr& c,
                                              int wcap = WSTACK, int* tq = nullptr, const float4* top = nullptr) {
-    const RayPre p = ray_pre(o, d);
+    const float reach = shadow_reach(o, ld2);
+    const RayPre p = ray_pre_shadow(o, d, reach);
     const unsigned oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
     float best = FMAX;
-    const float reach = shadow_reach(o, ld2);
     int sp = 0;
     TopC tc;
     const gnodes nbase = walk_base(W.nodes);
@@ -1069,8 +1163,8 @@ __device__ __forceinline__ bool visible_wide(const DWide& W, v3 o, v3 d, float l
         unsigned nh, th, imask, nl;
         int cb, tb;
         pin_node(N);
-        wide_node<COUNT, LATE_TRIS>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nl,
-                                    SHADOW_ORDER_XOR);
+        wide_node<COUNT, LATE_TRIS, SHADOW_CLAMP ? 1 : 0>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask,
+                                                  nl, SHADOW_ORDER_XOR);
         const unsigned m0 = __float_as_uint(N.f1.z), m1 = __float_as_uint(N.f1.w);
         const int next = wide_step_next<PK>(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, tc, stk, wcap);
         N = wload_at(nbase, next >= 0 ? next : 0, top);  // unconditional (closest_wide)

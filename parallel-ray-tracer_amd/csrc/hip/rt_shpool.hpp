@@ -166,10 +166,10 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
                     if (visible_walk<true, COUNT, true>(s.ref, o, d, ld2, sstk ? sstk : stk, c))
                         atomicOr(reinterpret_cast<unsigned*>(lvl + (wo & 511)) + 3, 1u << ((wo >> 9) & 31));
                 } else {
-                    p = ray_pre(o, d);
+                    reach = shadow_reach(o, ld2);
+                    p = ray_pre_shadow(o, d, reach);
                     oct = (p.ix < 0.0f ? 1u : 0u) | (p.iy < 0.0f ? 2u : 0u) | (p.iz < 0.0f ? 4u : 0u);
                     best = FMAX;
-                    reach = shadow_reach(o, ld2);
                     sp = 0;
                     N = wload_at(nbase, 0, c.top[1]);
                     busy = true;
@@ -186,8 +186,8 @@ __device__ __forceinline__ void shadow_pool(const DScene& s, OKM okm, float4* lv
                 unsigned nh, imask, nlf;
                 int cb;
                 pin_node(N);
-                wide_node<COUNT, LATE_TRIS>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb, imask, nlf,
-                                            SHADOW_ORDER_XOR);
+                wide_node<COUNT, LATE_TRIS, SHADOW_CLAMP ? 1 : 0>(N, p, oct, fminf(best * PRUNE_SLACK, reach), nh, th, cb, tb,
+                                                          imask, nlf, SHADOW_ORDER_XOR);
                 const unsigned m0 = __float_as_uint(N.f1.z), m1 = __float_as_uint(N.f1.w);
                 next = wide_step_next<true>(nh, cb, imask, oct ^ SHADOW_ORDER_XOR, sp, tc, stk, wcap);
                 N = wload_at(nbase, next >= 0 ? next : 0, c.top[1]);  // unconditional (closest_wide)
