@@ -579,7 +579,7 @@ __device__ __forceinline__ RayPre ray_pre_shadow(v3 o, v3 d, float reach) {
 // a scene comes near 2^40, and 2^-40 keeps the planes' scale 2^e / d far from the denormals; a zero direction
 // component's 1e20 reciprocal (safe_dir) only sends that axis' slab ends to 0 and 1 together, as to -/+huge before.
 #ifndef PRT_CLOSEST_CLAMP
-#define PRT_CLOSEST_CLAMP 0
+#define PRT_CLOSEST_CLAMP 1
 #endif
 constexpr bool CLOSEST_CLAMP = PRT_CLOSEST_CLAMP != 0;
 constexpr float CLAMP_SCALE = 0x1p-40f;

@@ -761,3 +761,38 @@ def test_kernel_errors_fail_sync_and_download(dev):
         with pytest.raises(dev.RtError, match="-8"):
             r.stats()
         r.close()
+
+
+@pytest.mark.parametrize("scale", [0.25, 8.0, 1000.0])
+def test_scaled_scene_vs_oracle(dev, tmp_path, scale):
+    """car_boxed with every vertex and light position scaled (the camera stays): the fast walks' box tests on
+    rescaled t (the shadow walks' [BOX_TMIN, reach] -> [0, 1], the closest walks' 2^-40 scale) and the inflation
+    margins hold from a scene a quarter the size to one a thousand times it; every kernel against the oracle"""
+    import shutil
+    from tests.oracle_bind import OracleScene
+    from tests.scenes import scene_paths
+    obj, mtl, lts = scene_paths("car_boxed")
+    out_lines = []
+    for ln in open(obj).read().splitlines():
+        if ln.startswith("v "):
+            x, y, z = (float(v) * scale for v in ln.split()[1:4])
+            ln = f"v {x:.6f} {y:.6f} {z:.6f}"
+        out_lines.append(ln)
+    o2, m2, l2 = tmp_path / "triangles.obj", tmp_path / "triangles.mtl", tmp_path / "lights.obj"
+    o2.write_text("\n".join(out_lines) + "\n")
+    shutil.copy(mtl, m2)
+    lines = []
+    for ln in open(lts).read().splitlines():
+        f = ln.split()
+        lines.append(" ".join([f"{float(v) * scale:.6f}" for v in f[:3]] + f[3:]))
+    l2.write_text("\n".join(lines) + "\n")
+    o = OracleScene.load(str(o2), str(m2), str(l2))
+    o.build_bvh(3)
+    ref = o.render(96, 54)
+    s = host.Scene.load(str(o2), str(m2), str(l2)).build_bvh(3)
+    assert ref["counters"]["shadow"] > 0
+    for k in KERNELS:
+        out = render(dev, s, 96, 54, k, counters=True)
+        np.testing.assert_array_equal(out["hit"], ref["hit"], err_msg=f"{k} x{scale}")
+        assert same_bits(out["rgb"], ref["rgb"]), (k, scale)
+        assert out["stats"]["shadow"] == ref["counters"]["shadow"], (k, scale)
