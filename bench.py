@@ -752,6 +752,12 @@ def main():
                          "survey_bytes_per_launch": survey_launch,
                          "survey_achieved": survey_launch / (k_avg_ms / 1e3) / 1e9,
                          "survey_frac": survey_launch / (k_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                         # (read first: neither byte fraction is a bound, both may exceed 1)
+                         "byte_fracs_are_bounds": False,
+                         "byte_fracs_note": "alg_byte_frac and survey_frac price every record a ray reads as an HBM "
+                                            "byte; the records are L1/L2/MALL hits (hbm_frac_measured is the real HBM "
+                                            "share), so values above 1 are expected and bound nothing; frac is the "
+                                            "binding (issue) roofline",
                          "simd_efficiency": simd_eff,
                          # VALU instructions per walk step (PMC SQ_INSTS_VALU of the launch / its wave-level node steps)
                          "valu_per_wave_step": (pmc["sq_insts_valu_per_launch"] / max(1, stc["wave_steps"])
